@@ -1,0 +1,113 @@
+// Row-wise normalisation / reduction kernels: LayerNorm, softmax over channels, row-mean pool.
+#include "svk_common.h"
+
+namespace svk {
+
+// One wave per row; PER = ceil(C / 64) values per lane kept in registers (two-pass mean/var,
+// biased variance, f32 statistics — nn.LayerNorm semantics).  PER == 0: generic loop.
+template <typename T, int PER>
+__global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ X, long ldx, T* __restrict__ Y, long ldy,
+                                                        const float* __restrict__ g, const float* __restrict__ b,
+                                                        int M, int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* x = X + row * ldx;
+  T* y = Y + row * ldy;
+  if constexpr (PER > 0) {
+    float v[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      v[i] = c < C ? to_f(x[c]) : 0.f;
+      s += v[i];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      float d = c < C ? v[i] - mean : 0.f;
+      q += d * d;
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      int c = lane + 64 * i;
+      if (c < C) y[c] = from_f<T>((v[i] - mean) * rstd * g[c] + b[c]);
+    }
+  } else {
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += to_f(x[c]);
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+    for (int c = lane; c < C; c += 64) { float d = to_f(x[c]) - mean; q += d * d; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    for (int c = lane; c < C; c += 64) y[c] = from_f<T>((to_f(x[c]) - mean) * rstd * g[c] + b[c]);
+  }
+}
+
+// Softmax over C (small) channels per row, one thread per row (MS-TCN's 14-class softmax).
+__global__ void softmax_rows_kernel(const float* __restrict__ X, long ldx, float* __restrict__ Y, long ldy, int M, int C) {
+  const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= M) return;
+  const float* x = X + r * ldx;
+  float* y = Y + r * ldy;
+  float m = -INFINITY;
+  for (int c = 0; c < C; ++c) m = fmaxf(m, x[c]);
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s += expf(x[c] - m);
+  const float inv = 1.0f / s;
+  for (int c = 0; c < C; ++c) y[c] = expf(x[c] - m) * inv;
+}
+
+// Y[b, c] = mean over R rows; one thread per (b, c), rows strided by ldx (coalesced over c).
+template <typename T>
+__global__ void mean_rows_kernel(const T* __restrict__ X, long ldx, float* __restrict__ Y, int B, int R, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= C) return;
+  const T* x = X + (long)b * R * ldx + c;
+  float s = 0.f;
+  for (int r = 0; r < R; ++r) s += to_f(x[(long)r * ldx]);
+  Y[(long)b * C + c] = s / R;
+}
+
+}  // namespace svk
+
+using namespace svk;
+
+extern "C" int svk_layernorm(int dtype, const void* X, long ldx, void* Y, long ldy, const float* gamma,
+                             const float* beta, int M, int C, float eps, void* stream) {
+  if (M < 0 || C <= 0 || !X || !Y || !gamma || !beta || ldx < C || ldy < C) { set_error("svk_layernorm: bad args"); return SVK_EINVAL; }
+  if (M == 0) return SVK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((M + 3) / 4), block(256);
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    const T* x = (const T*)X; T* y = (T*)Y;
+    if (C <= 64) hipLaunchKernelGGL((layernorm_kernel<T, 1>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
+    else if (C <= 128) hipLaunchKernelGGL((layernorm_kernel<T, 2>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
+    else if (C <= 256) hipLaunchKernelGGL((layernorm_kernel<T, 4>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
+    else if (C <= 512) hipLaunchKernelGGL((layernorm_kernel<T, 8>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
+    else hipLaunchKernelGGL((layernorm_kernel<T, 0>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
+    return check_launch("layernorm");
+  });
+}
+
+extern "C" int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C, void* stream) {
+  if (M < 0 || C <= 0 || !X || !Y || ldx < C || ldy < C) { set_error("svk_softmax_rows: bad args"); return SVK_EINVAL; }
+  if (M == 0) return SVK_OK;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((M + 255) / 256), dim3(256), 0, (hipStream_t)stream, X, ldx, Y, ldy, M, C);
+  return check_launch("softmax_rows");
+}
+
+extern "C" int svk_mean_rows(int dtype, const void* X, long ldx, float* Y, int B, int R, int C, void* stream) {
+  if (B < 0 || R <= 0 || C <= 0 || !X || !Y || ldx < C) { set_error("svk_mean_rows: bad args"); return SVK_EINVAL; }
+  if (B == 0) return SVK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((mean_rows_kernel<T>), dim3((C + 255) / 256, B), dim3(256), 0, st, (const T*)X, ldx, Y, B, R, C);
+    return check_launch("mean_rows");
+  });
+}

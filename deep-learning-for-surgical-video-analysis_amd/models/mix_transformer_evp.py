@@ -1,0 +1,510 @@
+"""MiT (SegFormer) backbone with EVP prompt generator and optical-flow fusion — MI355X build.
+
+Drop-in for the reference's ``models/mix_transformer_evp.py``: same classes, constructor
+signatures, submodule names (so ``state_dict`` keys are identical: 458 for mit_b2_evp)
+and ``forward(x, y, flow=None, return_features=False)`` contract
+(mix_transformer_evp.py:418-449).  The arithmetic runs in the svk HIP kernels on
+NHWC token maps that never leave that layout: patch embeds and the sequence-reduction
+conv are implicit-GEMM MFMA convolutions, every Linear is an MFMA GEMM with its
+bias / GELU / residual add fused into the epilogue, the MixFFN depthwise 3x3 carries
+its GELU, and the efficient self-attention is one kernel per (frame, head, 64 queries).
+The reference's NCHW round trips between stages (:376, :388, :400, :412) disappear.
+
+Compute dtype: ``model.svk_dtype`` (torch.float32 -> f32 MFMA, the parity path;
+torch.bfloat16 -> bf16 MFMA with f32 accumulation), default bf16 under CUDA autocast
+else f32.  Eval-mode forward only (see models._common.check_inference).
+"""
+from functools import partial
+
+import torch
+import torch.nn as nn
+
+from svk import ops
+from svk.pack import get_packed, lin_w, lin_b, conv_w, fold_bn
+from visualizer import get_local
+from ._common import pair, compute_dtype, check_inference, to_nhwc, DropPath
+from .segformer_head import SegFormerHead
+
+
+def _ln_params(norm):
+    return norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous()
+
+
+class DWConv(nn.Module):
+    """Depthwise 3x3 conv of MixFFN (mix_transformer_evp.py:19-30)."""
+
+    def __init__(self, dim=768):
+        super().__init__()
+        self.dwconv = nn.Conv2d(dim, dim, 3, 1, 1, bias=True, groups=dim)
+
+    def _pack(self, dt):
+        c = self.dwconv.weight.shape[0]
+        return dict(taps=self.dwconv.weight.detach().float().reshape(c, 9).t().contiguous(),
+                    b=self.dwconv.bias.detach().float().contiguous())
+
+    def forward(self, x, H, W, act=None):
+        """x [B, N, C] tokens (N = H*W) -> [B, N, C]; ``act`` lets Mlp fuse its GELU."""
+        B, N, C = x.shape
+        p = get_packed(self, x.dtype, self._pack)
+        y = ops.dwconv3x3(x.contiguous().view(B, H, W, C), p["taps"], p["b"], act=act)
+        return y.view(B, N, C)
+
+
+class Mlp(nn.Module):
+    """MixFFN: fc1 -> DWConv -> GELU -> fc2 (mix_transformer_evp.py:32-67)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU, drop=0.):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        if act_layer is not nn.GELU:
+            raise ValueError("Mlp: the svk path implements the reference's act_layer=nn.GELU only")
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.dwconv = DWConv(hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+    def _pack(self, dt):
+        return dict(w1=lin_w(self.fc1, dt), b1=lin_b(self.fc1), w2=lin_w(self.fc2, dt), b2=lin_b(self.fc2))
+
+    def forward(self, x, H, W, residual=None):
+        p = get_packed(self, x.dtype, self._pack)
+        h = ops.gemm(x, p["w1"], p["b1"])
+        h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)
+        return ops.gemm(h, p["w2"], p["b2"], residual=residual)
+
+
+class Attention(nn.Module):
+    """Efficient self-attention with sequence reduction (mix_transformer_evp.py:71-131)."""
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, qk_scale=None, attn_drop=0., proj_drop=0., sr_ratio=1):
+        super().__init__()
+        assert dim % num_heads == 0, f"dim {dim} should be divided by num_heads {num_heads}."
+        self.dim = dim
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        self.scale = qk_scale or head_dim ** -0.5
+        self.q = nn.Linear(dim, dim, bias=qkv_bias)
+        self.kv = nn.Linear(dim, dim * 2, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.sr_ratio = sr_ratio
+        if sr_ratio > 1:
+            self.sr = nn.Conv2d(dim, dim, kernel_size=sr_ratio, stride=sr_ratio)
+            self.norm = nn.LayerNorm(dim)
+
+    def _pack(self, dt):
+        p = dict(wq=lin_w(self.q, dt), bq=lin_b(self.q), wkv=lin_w(self.kv, dt), bkv=lin_b(self.kv),
+                 wp=lin_w(self.proj, dt), bp=lin_b(self.proj))
+        if self.sr_ratio > 1:
+            p["wsr"] = conv_w(self.sr.weight, dt)
+            p["bsr"] = self.sr.bias.detach().float().contiguous()
+            p["gn"], p["bn"] = _ln_params(self.norm)
+        return p
+
+    @get_local("attn")
+    def forward(self, x, H, W, residual=None):
+        B, N, C = x.shape
+        p = get_packed(self, x.dtype, self._pack)
+        x = x.contiguous()
+        q = ops.gemm(x, p["wq"], p["bq"])
+        if self.sr_ratio > 1:
+            r = self.sr_ratio
+            xs = ops.conv2d_nhwc(x.view(B, H, W, C), p["wsr"], r, r, 0, bias=p["bsr"])   # patchify GEMM, K = C*r*r
+            xs = xs.view(B, -1, C)
+            ops.layernorm(xs, p["gn"], p["bn"], self.norm.eps, out=xs)
+        else:
+            xs = x
+        kv = ops.gemm(xs, p["wkv"], p["bkv"])                                # [B, Nk, 2C]: k | v
+        o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], self.num_heads, self.scale)
+        return ops.gemm(o, p["wp"], p["bp"], residual=residual)
+
+
+class Block(nn.Module):
+    """x + attn(LN(x)); x + mlp(LN(x)) (mix_transformer_evp.py:134-171), residual adds fused in the GEMMs."""
+
+    def __init__(self, dim, num_heads, mlp_ratio=4., qkv_bias=False, qk_scale=None, drop=0., attn_drop=0.,
+                 drop_path=0., act_layer=nn.GELU, norm_layer=nn.LayerNorm, sr_ratio=1):
+        super().__init__()
+        self.norm1 = norm_layer(dim)
+        self.attn = Attention(dim, num_heads=num_heads, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                              attn_drop=attn_drop, proj_drop=drop, sr_ratio=sr_ratio)
+        self.drop_path = DropPath(drop_path) if drop_path > 0. else nn.Identity()
+        self.norm2 = norm_layer(dim)
+        self.mlp = Mlp(in_features=dim, hidden_features=int(dim * mlp_ratio), act_layer=act_layer, drop=drop)
+
+    def _pack(self, dt):
+        g1, b1 = _ln_params(self.norm1)
+        g2, b2 = _ln_params(self.norm2)
+        return dict(g1=g1, b1=b1, g2=g2, b2=b2)
+
+    def forward(self, x, H, W):
+        p = get_packed(self, x.dtype, self._pack)
+        x = x.contiguous()
+        h = ops.layernorm(x, p["g1"], p["b1"], self.norm1.eps)
+        x = self.attn(h, H, W, residual=x)
+        h = ops.layernorm(x, p["g2"], p["b2"], self.norm2.eps)
+        return self.mlp(h, H, W, residual=x)
+
+
+class OverlapPatchEmbed(nn.Module):
+    """Conv2d(k, s, k//2) -> tokens -> LayerNorm (mix_transformer_evp.py:174-215)."""
+
+    def __init__(self, img_size=224, patch_size=7, stride=4, in_chans=3, embed_dim=768):
+        super().__init__()
+        img_size = pair(img_size)
+        patch_size = pair(patch_size)
+        self.img_size = img_size
+        self.patch_size = patch_size
+        self.H, self.W = img_size[0] // patch_size[0], img_size[1] // patch_size[1]
+        self.num_patches = self.H * self.W
+        self.stride = stride
+        self.proj = nn.Conv2d(in_chans, embed_dim, kernel_size=patch_size, stride=stride,
+                              padding=(patch_size[0] // 2, patch_size[1] // 2))
+        self.norm = nn.LayerNorm(embed_dim)
+
+    def _pack(self, dt):
+        g, b = _ln_params(self.norm)
+        return dict(w=conv_w(self.proj.weight, dt), b=self.proj.bias.detach().float().contiguous(), g=g, beta=b)
+
+    def embed_nhwc(self, x):
+        """x [B, H, W, Cin] NHWC (compute dtype) -> (tokens [B, OH*OW, C], OH, OW)."""
+        p = get_packed(self, x.dtype, self._pack)
+        k = self.patch_size[0]
+        y = ops.conv2d_nhwc(x, p["w"], k, self.stride, k // 2, bias=p["b"])
+        B, OH, OW, C = y.shape
+        y = y.view(B, OH * OW, C)
+        ops.layernorm(y, p["g"], p["beta"], self.norm.eps, out=y)
+        return y, OH, OW
+
+    def forward(self, x):
+        """Reference signature: NCHW map -> (tokens, H, W)."""
+        check_inference(self, x)
+        return self.embed_nhwc(to_nhwc(x, compute_dtype(self)))
+
+
+class GaussianFilter(nn.Module):
+    """Reflect-pad 2 + binomial 5x5/256 depthwise filter (mix_transformer_evp.py:495-514).  The
+    reference keeps the kernel as a plain tensor moved to a module-global device (:463, 508);
+    here it is a non-persistent buffer (moves with the module, state_dict keys unchanged)."""
+
+    def __init__(self):
+        super().__init__()
+        self.register_buffer("kernel", self.gauss_kernel(), persistent=False)
+
+    def gauss_kernel(self, channels=3):
+        k = torch.tensor([1., 4., 6., 4., 1.])
+        return (torch.outer(k, k) / 256.).repeat(channels, 1, 1, 1)
+
+    def conv_gauss(self, img):
+        """NCHW f32 -> filtered map, returned NHWC in the compute dtype."""
+        return ops.gauss5x5_reflect(img.float(), compute_dtype(self))
+
+
+class PromptGenerator(nn.Module):
+    """EVP prompt generator, input_type 'gaussian', adaptor 'adaptor' (mix_transformer_evp.py:550-815) —
+    the only configuration MixVisionTransformerEVP builds (:278-289)."""
+
+    def __init__(self, scale_factor, prompt_type, embed_dims, tuning_stage, depths, input_type,
+                 freq_nums, handcrafted_tune, embedding_tune, adaptor, img_size):
+        super().__init__()
+        if input_type != "gaussian" or adaptor != "adaptor" or not (handcrafted_tune and embedding_tune):
+            raise ValueError("PromptGenerator: the svk build implements input_type='gaussian', "
+                             "adaptor='adaptor' with handcrafted and embedding tuning (the reference's fixed config)")
+        self.scale_factor = scale_factor
+        self.prompt_type = prompt_type
+        self.embed_dims = embed_dims
+        self.input_type = input_type
+        self.freq_nums = freq_nums
+        self.tuning_stage = tuning_stage
+        self.depths = depths
+        self.handcrafted_tune = handcrafted_tune
+        self.embedding_tune = embedding_tune
+        self.adaptor = adaptor
+        self.img_size = img_size
+        self.gaussian_filter = GaussianFilter()
+        cin = 3
+        for s in range(4):
+            if str(s + 1) in tuning_stage:
+                k, st, div = (7, 4, 1) if s == 0 else (3, 2, 2 ** (s + 1))
+                co = embed_dims[s] // scale_factor
+                setattr(self, f"handcrafted_generator{s + 1}",
+                        OverlapPatchEmbed(img_size=img_size // (1 if s == 0 else div), patch_size=k, stride=st,
+                                          in_chans=cin, embed_dim=co))
+                cin = co
+        for s in range(4):
+            if str(s + 1) in tuning_stage:
+                setattr(self, f"embedding_generator{s + 1}", nn.Linear(embed_dims[s], embed_dims[s] // scale_factor))
+        for s in range(4):
+            if str(s + 1) in tuning_stage:
+                c4 = embed_dims[s] // scale_factor
+                for i in range(depths[s]):
+                    setattr(self, f"lightweight_mlp{s + 1}_{i}", nn.Sequential(nn.Linear(c4, c4), nn.GELU()))
+                setattr(self, f"shared_mlp{s + 1}", nn.Linear(c4, embed_dims[s]))
+
+    def init_handcrafted(self, x):
+        return self.init_prompts(x)
+
+    def init_prompts(self, segmap):
+        """Gaussian-filtered segmap -> handcrafted cascade (mix_transformer_evp.py:718-747);
+        returns the 4 token maps [B, N_s, C_s/4]."""
+        x = self.gaussian_filter.conv_gauss(segmap)
+        feats = [None] * 4
+        for s in range(4):
+            if str(s + 1) not in self.tuning_stage:
+                break
+            f, H, W = getattr(self, f"handcrafted_generator{s + 1}").embed_nhwc(x)
+            feats[s] = f
+            x = f.view(f.shape[0], H, W, -1)
+        return tuple(feats)
+
+    def init_prompt(self, embedding_feature, handcrafted_feature, block_num):
+        """(mix_transformer_evp.py:749-756) -> (handcrafted, embedding); the returned tuple also carries
+        their sum, formed in the embedding GEMM's epilogue, which get_prompt consumes."""
+        lin = getattr(self, f"embedding_generator{block_num}")
+        dt = embedding_feature.dtype
+        p = get_packed(lin, dt, lambda d: dict(w=lin_w(lin, d), b=lin_b(lin)))
+        emb = ops.gemm(embedding_feature, p["w"], p["b"])
+        summed = ops.gemm(embedding_feature, p["w"], p["b"], residual=handcrafted_feature)
+        return _Prompt((handcrafted_feature, emb), summed)
+
+    def get_prompt(self, x, prompt, block_num, depth_num):
+        """x + shared_mlp(GELU(lightweight_mlp(hc + emb))) (mix_transformer_evp.py:776-815)."""
+        summed = getattr(prompt, "summed", None)
+        if summed is None:
+            raise ValueError("get_prompt: pass the tuple returned by init_prompt")
+        lw = getattr(self, f"lightweight_mlp{block_num}_{depth_num}")[0]
+        sh = getattr(self, f"shared_mlp{block_num}")
+        dt = x.dtype
+        pl = get_packed(lw, dt, lambda d: dict(w=lin_w(lw, d), b=lin_b(lw)))
+        ps = get_packed(sh, dt, lambda d: dict(w=lin_w(sh, d), b=lin_b(sh)))
+        feat = ops.gemm(summed, pl["w"], pl["b"], act="gelu")
+        return ops.gemm(feat, ps["w"], ps["b"], residual=x)
+
+
+class _Prompt(tuple):
+    def __new__(cls, items, summed):
+        t = super().__new__(cls, items)
+        t.summed = summed
+        return t
+
+
+class OpticalFlowEncoder(nn.Module):
+    """4x (Conv2d + BN + ReLU) flow encoder (mix_transformer_evp.py:818-859); BN (eval) is folded
+    into the conv weights, ReLU into the implicit-GEMM epilogue."""
+
+    def __init__(self, out_dim_s3=320, out_dim_s4=512):
+        super().__init__()
+        self.conv1 = nn.Conv2d(2, 64, kernel_size=7, stride=4, padding=3)
+        self.bn1 = nn.BatchNorm2d(64)
+        self.act = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(64, 128, kernel_size=3, stride=2, padding=1)
+        self.bn2 = nn.BatchNorm2d(128)
+        self.conv3 = nn.Conv2d(128, out_dim_s3, kernel_size=3, stride=2, padding=1)
+        self.bn3 = nn.BatchNorm2d(out_dim_s3)
+        self.conv4 = nn.Conv2d(out_dim_s3, out_dim_s4, kernel_size=3, stride=2, padding=1)
+        self.bn4 = nn.BatchNorm2d(out_dim_s4)
+
+    def _pack(self, dt):
+        p = {}
+        for i in range(1, 5):
+            w, b = fold_bn(getattr(self, f"conv{i}").weight, getattr(self, f"conv{i}").bias, getattr(self, f"bn{i}"))
+            p[f"w{i}"] = conv_w(w, dt)
+            p[f"b{i}"] = b.float().contiguous()
+        return p
+
+    def forward(self, x):
+        """x [B, T, 2, H, W] or [B*T, 2, H, W] (f32) -> (tokens s3 [B*T, N3, C3], tokens s4 [B*T, N4, C4])."""
+        check_inference(self, x)
+        if x.dim() == 5:
+            B, T, C, H, W = x.shape
+            x = x.reshape(B * T, C, H, W)
+        dt = compute_dtype(self)
+        p = get_packed(self, dt, self._pack)
+        h = to_nhwc(x, dt)
+        feats = []
+        for i, (k, s, pad) in enumerate(((7, 4, 3), (3, 2, 1), (3, 2, 1), (3, 2, 1)), start=1):
+            h = ops.conv2d_nhwc(h, p[f"w{i}"], k, s, pad, bias=p[f"b{i}"], act="relu")
+            feats.append(h)
+        f3, f4 = feats[2], feats[3]
+        return f3.view(f3.shape[0], -1, f3.shape[3]), f4.view(f4.shape[0], -1, f4.shape[3])
+
+
+class MotionGuidedCrossAttention(nn.Module):
+    """LN(x_visual + MHA(q = x_visual, k = v = x_flow)) (mix_transformer_evp.py:862-890).
+    ``cross_attn`` is kept as torch's nn.MultiheadAttention purely as the parameter container
+    (in_proj_weight / in_proj_bias / out_proj); the math runs in svk GEMM + attention kernels."""
+
+    def __init__(self, dim, num_heads=8, attn_drop=0., proj_drop=0.):
+        super().__init__()
+        self.cross_attn = nn.MultiheadAttention(embed_dim=dim, num_heads=num_heads, dropout=attn_drop, batch_first=True)
+        self.proj_drop = nn.Dropout(proj_drop)
+        self.norm = nn.LayerNorm(dim)
+
+    def _pack(self, dt):
+        E = self.cross_attn.embed_dim
+        w = self.cross_attn.in_proj_weight.detach()
+        b = self.cross_attn.in_proj_bias.detach().float()
+        g, beta = _ln_params(self.norm)
+        return dict(wq=w[:E].to(dt).contiguous(), bq=b[:E].contiguous(), wkv=w[E:].to(dt).contiguous(),
+                    bkv=b[E:].contiguous(), wo=lin_w(self.cross_attn.out_proj, dt),
+                    bo=lin_b(self.cross_attn.out_proj), g=g, beta=beta)
+
+    def forward(self, x_visual, x_flow):
+        check_inference(self, x_visual, x_flow)
+        p = get_packed(self, x_visual.dtype, self._pack)
+        E = self.cross_attn.embed_dim
+        H = self.cross_attn.num_heads
+        x_visual = x_visual.contiguous()
+        q = ops.gemm(x_visual, p["wq"], p["bq"])
+        kv = ops.gemm(x_flow.contiguous(), p["wkv"], p["bkv"])
+        o = ops.attention(q, kv[:, :, :E], kv[:, :, E:], H, (E // H) ** -0.5)
+        o = ops.gemm(o, p["wo"], p["bo"], residual=x_visual)
+        return ops.layernorm(o, p["g"], p["beta"], self.norm.eps, out=o)
+
+
+class MixVisionTransformerEVP(nn.Module):
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, num_classes=14, embed_dims=[64, 128, 256, 512],
+                 num_heads=[1, 2, 4, 8], mlp_ratios=[4, 4, 4, 4], qkv_bias=False, qk_scale=None, drop_rate=0.,
+                 attn_drop_rate=0., drop_path_rate=0., norm_layer=nn.LayerNorm,
+                 depths=[3, 4, 6, 3], sr_ratios=[8, 4, 2, 1], **kwargs):
+        super().__init__()
+        self.num_classes = num_classes
+        self.depths = depths
+        self.embed_dims = embed_dims
+        self.svk_dtype = kwargs.pop("svk_dtype", None)
+        cins = [in_chans] + list(embed_dims[:3])
+        for s in range(4):
+            k, st = (7, 4) if s == 0 else (3, 2)
+            setattr(self, f"patch_embed{s + 1}",
+                    OverlapPatchEmbed(img_size=img_size // (1 if s == 0 else 2 ** (s + 1)), patch_size=k, stride=st,
+                                      in_chans=cins[s], embed_dim=embed_dims[s]))
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(depths))]
+        cur = 0
+        for s in range(4):
+            setattr(self, f"block{s + 1}", nn.ModuleList([
+                Block(dim=embed_dims[s], num_heads=num_heads[s], mlp_ratio=mlp_ratios[s], qkv_bias=qkv_bias,
+                      qk_scale=qk_scale, drop=drop_rate, attn_drop=attn_drop_rate, drop_path=dpr[cur + i],
+                      norm_layer=norm_layer, sr_ratio=sr_ratios[s]) for i in range(depths[s])]))
+            setattr(self, f"norm{s + 1}", norm_layer(embed_dims[s]))
+            cur += depths[s]
+        self.head = SegFormerHead(embed_dims, num_classes)
+        # EVP prompt config, fixed in the reference (mix_transformer_evp.py:277-289)
+        self.scale_factor = 4
+        self.prompt_type = "highpass"
+        self.tuning_stage = str(1234)
+        self.input_type = "gaussian"
+        self.freq_nums = 0.25
+        self.handcrafted_tune = True
+        self.embedding_tune = True
+        self.adaptor = "adaptor"
+        self.prompt_generator = PromptGenerator(self.scale_factor, self.prompt_type, self.embed_dims,
+                                                self.tuning_stage, self.depths, self.input_type, self.freq_nums,
+                                                self.handcrafted_tune, self.embedding_tune, self.adaptor, img_size)
+        self.flow_encoder = OpticalFlowEncoder(out_dim_s3=embed_dims[2], out_dim_s4=embed_dims[3])
+        self.cross_attn_s3 = MotionGuidedCrossAttention(dim=embed_dims[2])
+        self.cross_attn_s4 = MotionGuidedCrossAttention(dim=embed_dims[3])
+
+    # -- reference utility surface (mix_transformer_evp.py:320-350) --------------------------------
+    def reset_drop_path(self, drop_path_rate):
+        dpr = [x.item() for x in torch.linspace(0, drop_path_rate, sum(self.depths))]
+        cur = 0
+        for s in range(4):
+            for i in range(self.depths[s]):
+                getattr(self, f"block{s + 1}")[i].drop_path.drop_prob = dpr[cur + i]
+            cur += self.depths[s]
+
+    def freeze_patch_emb(self):
+        self.patch_embed1.requires_grad = False
+
+    @torch.jit.ignore
+    def no_weight_decay(self):
+        return {"pos_embed1", "pos_embed2", "pos_embed3", "pos_embed4", "cls_token"}
+
+    def get_classifier(self):
+        return self.head
+
+    def reset_classifier(self, num_classes, global_pool=""):
+        self.num_classes = num_classes
+        self.head = nn.Linear(self.embed_dims[3], num_classes) if num_classes > 0 else nn.Identity()
+
+    def _propagate_dtype(self, dt):
+        for m in self.modules():
+            if m is not self:
+                m.svk_dtype = dt
+
+    # -- forward --------------------------------------------------------------------------------------
+    def _stages(self, x, y):
+        """Token-level forward_features: returns [(tokens [B, H*W, C], H, W)] for the 4 stages."""
+        dt = compute_dtype(self)
+        self._propagate_dtype(dt)
+        x = x.reshape(-1, 3, x.shape[-2], x.shape[-1])
+        y = y.reshape(-1, 3, y.shape[-2], y.shape[-1])
+        hcs = self.prompt_generator.init_prompts(y)
+        h = to_nhwc(x, dt)
+        outs = []
+        for s in range(4):
+            t, H, W = getattr(self, f"patch_embed{s + 1}").embed_nhwc(h)
+            prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1)
+            for i, blk in enumerate(getattr(self, f"block{s + 1}")):
+                t = self.prompt_generator.get_prompt(t, prompt, s + 1, i)
+                t = blk(t, H, W)
+            norm = getattr(self, f"norm{s + 1}")
+            pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
+            ops.layernorm(t, pn[0], pn[1], norm.eps, out=t)
+            outs.append((t, H, W))
+            h = t.view(t.shape[0], H, W, -1)
+        return outs
+
+    def forward_features(self, x, y):
+        """(mix_transformer_evp.py:352-416) -> list of 4 NCHW stage maps (views of the NHWC tokens)."""
+        check_inference(self, x, y)
+        return [t.view(t.shape[0], H, W, -1).permute(0, 3, 1, 2) for t, H, W in self._stages(x, y)]
+
+    def forward(self, x, y, flow=None, return_features=False):
+        """(mix_transformer_evp.py:418-449): features [B, 2048] if return_features else (y [B, 7], y_ant [B, 7])."""
+        check_inference(self, x, y, flow)
+        outs = self._stages(x, y)
+        if flow is not None:
+            f3, f4 = self.flow_encoder(flow)
+            c3, H3, W3 = outs[2]
+            outs[2] = (self.cross_attn_s3(c3, f3), H3, W3)
+            c4, H4, W4 = outs[3]
+            outs[3] = (self.cross_attn_s4(c4, f4), H4, W4)
+        return self.head.forward_tokens(outs, return_features=return_features)
+
+
+def _variant(embed_dims, depths):
+    def init(self, **kwargs):
+        MixVisionTransformerEVP.__init__(
+            self, patch_size=4, embed_dims=embed_dims, num_heads=[1, 2, 5, 8], mlp_ratios=[4, 4, 4, 4],
+            qkv_bias=True, norm_layer=partial(nn.LayerNorm, eps=1e-6), depths=depths, sr_ratios=[8, 4, 2, 1],
+            drop_rate=0.0, drop_path_rate=0.1, **kwargs)
+    return init
+
+
+# mix_transformer_evp.py:893-944
+class mit_b0_evp(MixVisionTransformerEVP):
+    __init__ = _variant([32, 64, 160, 256], [2, 2, 2, 2])
+
+
+class mit_b1_evp(MixVisionTransformerEVP):
+    __init__ = _variant([64, 128, 320, 512], [2, 2, 2, 2])
+
+
+class mit_b2_evp(MixVisionTransformerEVP):
+    __init__ = _variant([64, 128, 320, 512], [3, 4, 6, 3])
+
+
+class mit_b3_evp(MixVisionTransformerEVP):
+    __init__ = _variant([64, 128, 320, 512], [3, 4, 18, 3])
+
+
+class mit_b4_evp(MixVisionTransformerEVP):
+    __init__ = _variant([64, 128, 320, 512], [3, 8, 27, 3])
+
+
+class mit_b5_evp(MixVisionTransformerEVP):
+    __init__ = _variant([64, 128, 320, 512], [3, 6, 40, 3])

@@ -1,0 +1,72 @@
+"""ctypes binding of the svk C ABI (include/svk.h).
+
+This is the reference-side binding a maintainer would add: the reference has no
+FFI of its own (its boundary is the Python module surface), so the
+build's ``models.*`` modules call these symbols through ctypes.  Loading fails
+loudly when the shared library is missing — there is no CPU fallback.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SVK_LIB", os.path.join(_HERE, "libsvk.so"))
+
+c_int, c_long, c_float, c_void_p, c_char_p = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_void_p, ctypes.c_char_p
+P = c_void_p
+
+# name -> argtypes; every entry point returns int status except the two string getters.
+SIGNATURES = {
+    "svk_gemm": [c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, c_int, c_int, c_int, c_int, P],
+    "svk_conv2d_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_layernorm": [c_int, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
+    "svk_attention": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
+                      c_int, c_int, c_int, c_int, c_int, c_float, P],
+    "svk_dwconv3x3": [c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_nchw_to_nhwc": [c_int, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_gauss5x5_reflect": [c_int, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_resize_bilinear": [c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_mean_rows": [c_int, P, c_long, P, c_int, c_int, c_int, P],
+    "svk_softmax_rows": [P, c_long, P, c_long, c_int, c_int, P],
+    "svk_mstcn_layer": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_window_unfold": [c_int, P, c_long, P, P, c_int, c_int, c_int, P],
+    "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
+    "svk_cast": [c_int, P, c_int, P, c_long, P],
+}
+STRING_FUNCS = ("svk_version", "svk_last_error")
+
+_lib = None
+
+
+class SvkError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libsvk.so once and declare every signature.  Raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SvkError(f"svk: HIP kernel library not found at {LIB_PATH}; build it with "
+                       f"`python -c 'import __graft_entry__ as g; g.build()'` (make -C csrc)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = c_int
+    for name in STRING_FUNCS:
+        fn = getattr(lib, name)
+        fn.argtypes = []
+        fn.restype = c_char_p
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != 0:
+        raise SvkError(f"{name} failed ({rc}): {load().svk_last_error().decode()}")
+
+
+def version():
+    return load().svk_version().decode()

@@ -1,0 +1,118 @@
+/*
+ * svk.h — C ABI of the MI355X (gfx950) kernel library behind the build's
+ * `models.*` drop-in surface for the surgical-phase hot path.
+ *
+ * The reference (THao712/Deep-Learning-for-Surgical-Video-Analysis) exposes no
+ * FFI: its boundary is the Python module/class surface.  Each
+ * entry point below replaces the PyTorch op(s) the reference calls at the cited
+ * file:line; the Python host (svk/_lib.py, ctypes) binds exactly these symbols.
+ *
+ * Conventions
+ *   - Caller owns all memory (device pointers; the library never allocates).
+ *   - Stream-ordered and asynchronous: `stream` is a hipStream_t (NULL = default
+ *     stream); no host synchronisation inside any call.
+ *   - Return 0 on success, negative SVK_E* on error; svk_last_error() gives a
+ *     thread-local message.  No exceptions cross the ABI.
+ *   - dtype selects the storage/compute type of activations and weights:
+ *     SVK_F32 (f32 MFMA, exact f32 products, parity path) or SVK_BF16 (bf16 MFMA,
+ *     f32 accumulation).  Biases, norm affine terms and depthwise taps are f32.
+ *   - Token layouts are row-major [rows, channels] with an explicit leading
+ *     dimension; image/feature maps are NHWC (token n = h*W + w, the reference's
+ *     own `flatten(2).transpose(1, 2)` order, mix_transformer_evp.py:212).
+ */
+#ifndef SVK_H
+#define SVK_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { SVK_F32 = 0, SVK_BF16 = 1 };
+enum { SVK_ACT_NONE = 0, SVK_ACT_GELU = 1, SVK_ACT_RELU = 2, SVK_ACT_TANH = 3 };
+enum { SVK_OK = 0, SVK_EINVAL = -1, SVK_EUNSUPPORTED = -2, SVK_ELAUNCH = -3 };
+
+const char* svk_version(void);
+const char* svk_last_error(void);
+
+/* C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]
+ * Replaces nn.Linear (+ activation, + residual add) at: Attention q/kv/proj
+ * (mix_transformer_evp.py:81-84, 112-128), Mlp fc1/fc2 (:37-40, 61-65), Block residuals
+ * (:168-169), PromptGenerator embedding/lightweight/shared MLPs (:599-642, 752, 800-812),
+ * SegFormerHead MLP/linear_fuse/fc (segformer_head.py:38-43, 74-80, 101-106),
+ * MS-TCN 1x1 Conv1d (mstcn.py:161, 171), Transformer fc (adapter_transformer.py:327, 346).
+ * bias, R may be NULL.  lda/ldw/ldr/ldc in elements. */
+int svk_gemm(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
+             const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act, void* stream);
+
+/* Implicit-GEMM Conv2d over an NHWC input, weights packed [Cout][k][k][Cin]:
+ * Y[b, oy, ox, co] = act(sum X[b, oy*s-p+i, ox*s-p+j, ci] * Wt[co, i, j, ci] + bias[co]) + R[...]
+ * OH = (H + 2p - k)/s + 1.  Replaces OverlapPatchEmbed.proj (mix_transformer_evp.py:188-189,
+ * 210), Attention.sr (:89, 116), PromptGenerator handcrafted convs (:582-595),
+ * OpticalFlowEncoder conv+BN(eval, folded)+ReLU (:823-853). */
+int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* Wt,
+                    const float* bias, const void* R, void* Y, int Cout, int k, int stride, int pad,
+                    int act, void* stream);
+
+/* Row LayerNorm: Y = (X - mean) / sqrt(var + eps) * gamma + beta over C channels.
+ * Replaces every nn.LayerNorm on the path (mix_transformer_evp.py:90, 139-146, 190,
+ * 245-269, 876). */
+int svk_layernorm(int dtype, const void* X, long ldx, void* Y, long ldy, const float* gamma,
+                  const float* beta, int M, int C, float eps, void* stream);
+
+/* Multi-head softmax attention, per batch b and head h (columns h*hd .. h*hd+hd-1):
+ * O = softmax(scale * Q K^T) V.  sb* = batch strides (elements).  Nk <= 256, hd <= 64.
+ * Replaces Attention q@k^T/softmax/@v (mix_transformer_evp.py:123-127) and
+ * nn.MultiheadAttention's core (:868-883). */
+int svk_attention(int dtype, const void* Q, long ldq, long sbq, const void* K, long ldk, long sbk,
+                  const void* V, long ldv, long sbv, void* O, long ldo, long sbo, int B, int Nq,
+                  int Nk, int heads, int hd, float scale, void* stream);
+
+/* Depthwise 3x3 conv (pad 1) + bias + activation over NHWC, taps w[9][C] (f32).
+ * Replaces DWConv.forward + Mlp.act (mix_transformer_evp.py:24-30, 62-63). */
+int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B,
+                  int H, int W, int C, int act, void* stream);
+
+/* NCHW f32 -> NHWC dtype (input packing of frames / flow; view(-1,3,224,224) at :354). */
+int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, void* stream);
+
+/* GaussianFilter.conv_gauss (mix_transformer_evp.py:511-514): reflect-pad 2 + binomial 5x5/256,
+ * NCHW f32 in -> NHWC dtype out. */
+int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W,
+                         void* stream);
+
+/* Bilinear resize (align_corners=False) of NHWC token maps [B, H*W, C] (row stride ldx)
+ * to [B, OH*OW, C] (row stride ldy).  Replaces resize() in SegFormerHead
+ * (segformer_head.py:150-156). */
+int svk_resize_bilinear(int dtype, const void* X, long ldx, void* Y, long ldy, int B, int H, int W,
+                        int C, int OH, int OW, void* stream);
+
+/* Y[b, c] = mean_r X[b*R + r, c] (f32 out).  Replaces AdaptiveAvgPool2d + flatten
+ * (segformer_head.py:167-169). */
+int svk_mean_rows(int dtype, const void* X, long ldx, float* Y, int B, int R, int C, void* stream);
+
+/* Row softmax over C channels (f32): MS-TCN inter-stage softmax over classes (mstcn.py:126). */
+int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C, void* stream);
+
+/* One MS-TCN DilatedResidualLayer (mstcn.py:208-214) over a time-major [T, F] f32 map:
+ * h = relu(sum_j Wd[j] x[t + off_j] + bd); y[t] = x[t] + W1 h + b1;
+ * causal: off = (-2d, -d, 0); else (-d, 0, +d); out-of-range taps read zero.
+ * Wd packed [3][F_out][F_in], W1 [F_out][F_in]. F <= 64. */
+int svk_mstcn_layer(const float* X, const float* Wd, const float* bd, const float* W1,
+                    const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
+
+/* Causal window unfold (adapter_transformer.py:336-343 as pad + unfold):
+ * Y[t, i, c] = X[t - len + 1 + i, c] (0 if negative) + pos[i, c] (pos may be NULL). */
+int svk_window_unfold(int dtype, const void* X, long ldx, const float* pos, void* Y, int T, int C,
+                      int len, void* stream);
+
+/* Y[r, c] = X[r, c] + P[r % period, c] over M contiguous rows of C (P f32): the fixed
+ * position table added to Transformer2_3_1's encoder input (build-defined, parity unpinned). */
+int svk_add_bcast(int dtype, const void* X, const float* P, void* Y, long M, int C, int period, void* stream);
+
+/* Elementwise dtype conversion (n elements). */
+int svk_cast(int dtype_in, const void* X, int dtype_out, void* Y, long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SVK_H */

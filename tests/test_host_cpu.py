@@ -1,0 +1,154 @@
+"""CPU-side tests of the build: C-ABI library exports, host-side module surface and weight
+packing, refusal of CPU execution (no fallback), index helpers."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import REPO
+from oracle import inputs as I, params as P, mit_evp as M, shapes as SH
+
+HEADER = os.path.join(REPO, "include", "svk.h")
+
+
+def _header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"\b(?:int|const char\*)\s+(svk_\w+)\s*\(([^)]*)\)\s*;", src):
+        args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        out[m.group(1)] = len(args)
+    return out
+
+
+def test_library_exports_every_header_symbol():
+    from svk import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    funcs = _header_functions()
+    assert len(funcs) >= 16
+    for name, nargs in funcs.items():
+        assert hasattr(lib, name), f"{name} declared in svk.h but not exported"
+        if name in _lib.SIGNATURES:
+            assert len(_lib.SIGNATURES[name]) == nargs, f"{name}: ctypes binding has wrong arity"
+        else:
+            assert name in _lib.STRING_FUNCS
+    assert set(_lib.SIGNATURES) | set(_lib.STRING_FUNCS) == set(funcs)
+
+
+def test_library_version_and_error_path():
+    from svk import _lib
+    lib = _lib.load()
+    assert lib.svk_version().decode().startswith("svk")
+    # argument validation happens on the host, before any HIP call: safe without a GPU
+    rc = lib.svk_gemm(0, None, 0, None, 0, None, None, 0, None, 0, 4, 4, 4, 0, None)
+    assert rc == -1 and b"svk_gemm" in lib.svk_last_error()
+    rc = lib.svk_attention(0, None, 0, 0, None, 0, 0, None, 0, 0, None, 0, 0, 1, 1, 300, 1, 64, 1.0, None)
+    assert rc == -1 and b"Nk" in lib.svk_last_error()
+
+
+@pytest.mark.parametrize("variant", ["mit_b0_evp", "mit_b2_evp", "mit_b3_evp"])
+def test_build_state_dict_matches_reference(golden, variant):
+    from models import mix_transformer_evp as mte
+    m = getattr(mte, variant)()
+    sd = m.state_dict()
+    assert sorted(sd) == list(golden[f"{variant}_keys"])
+    shapes = SH.mit_evp_shapes(variant)
+    for k, v in sd.items():
+        assert tuple(v.shape) == tuple(shapes[k]), k
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in sd.items()}, 0), strict=True)
+
+
+def test_mstcn_and_transformer_surface(golden):
+    from models import mstcn, adapter_transformer
+    m = mstcn.MultiStageModel_S(2, 8, 32, 2048, 14, True)
+    assert sorted(m.state_dict()) == list(golden["mstcn_2_8_32_2048_c_keys"])
+    assert len(m.state_dict()) == 72
+    t = adapter_transformer.Transformer(32, 2048, 14, 30)
+    assert sorted(t.state_dict()) == sorted(SH.transformer_shapes(32, 2048, 14))
+    with pytest.raises(ImportError):
+        mstcn.CausalMambaModel(2, 8, 64, 2048, 14, True)
+
+
+def test_no_cpu_fallback():
+    import svk
+    from models import mix_transformer_evp as mte, mstcn
+    m = mte.mit_b0_evp().eval()
+    with pytest.raises(svk.SvkError, match="GPU"):
+        m(I.frames(1), I.segmaps(1), None, return_features=True)
+    with pytest.raises(svk.SvkError, match="train-mode"):
+        mte.mit_b0_evp().train().flow_encoder.forward(torch.zeros(1, 2, 8, 8))
+    ms = mstcn.MultiStageModel_S(1, 2, 8, 16, 14, True).eval()
+    with pytest.raises(svk.SvkError):
+        ms(torch.zeros(1, 16, 10))
+
+
+def test_head_fold_is_exact_on_cpu():
+    """Host-side weight folding of SegFormerHead (resize-first + linear_c*/fuse/BN -> one matrix)
+    reproduces the reference op order (oracle) in fp64 on CPU."""
+    from models import mix_transformer_evp as mte
+    m = mte.mit_b2_evp()
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
+    p = m.head._pack(torch.float64)
+    sd = {k: v.double() for k, v in m.state_dict().items()}
+    g = torch.Generator().manual_seed(0)
+    dims = (64, 128, 320, 512)
+    sides = (56, 28, 14, 7)
+    outs = [(torch.randn(2, s * s, c, generator=g, dtype=torch.float64), s, s) for c, s in zip(dims, sides)]
+    ref = M.segformer_head(outs, sd, return_features=True)
+    r = []
+    for t, H, W in (outs[3], outs[2], outs[1], outs[0]):
+        nchw = t.transpose(1, 2).reshape(2, -1, H, W)
+        if H != 7:
+            nchw = torch.nn.functional.interpolate(nchw, (7, 7), None, "bilinear", False)
+        r.append(nchw.flatten(2).transpose(1, 2))
+    r = torch.cat(r, dim=2)
+    y = torch.relu(r @ p["w"].t() + p["b"].double()).mean(dim=1)
+    # the folded bias is stored f32 by design (kernel ABI: biases are f32) -> ~1e-8 absolute
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=0, atol=1e-6)
+
+
+def test_flow_bn_fold_is_exact_on_cpu():
+    from models import mix_transformer_evp as mte
+    from svk.pack import fold_bn
+    m = mte.mit_b0_evp()
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
+    fe = m.flow_encoder.double().eval()
+    x = torch.randn(2, 2, 32, 32, dtype=torch.float64)
+    ref = fe.bn1(fe.conv1(x))
+    w, b = fold_bn(fe.conv1.weight, fe.conv1.bias, fe.bn1)
+    got = torch.nn.functional.conv2d(x, w, b, stride=4, padding=3)
+    np.testing.assert_allclose(got.numpy(), ref.detach().numpy(), rtol=1e-10, atol=1e-10)
+
+
+def test_conv_weight_packing_order():
+    """[Cout, Cin, k, k] -> [Cout, (kh, kw, ci)] must match an NHWC im2col K order."""
+    from svk.pack import conv_w
+    w = torch.randn(5, 3, 7, 7, dtype=torch.float64)
+    x = torch.randn(1, 3, 20, 20, dtype=torch.float64)
+    ref = torch.nn.functional.conv2d(x, w, stride=4, padding=3)
+    xn = torch.nn.functional.pad(x, (3, 3, 3, 3)).permute(0, 2, 3, 1)   # NHWC padded
+    cols = xn.unfold(1, 7, 4).unfold(2, 7, 4)                            # [1, OH, OW, C, kh, kw]
+    cols = cols.permute(0, 1, 2, 4, 5, 3).reshape(1, ref.shape[2], ref.shape[3], -1)
+    got = cols @ conv_w(w, torch.float64).t()
+    np.testing.assert_allclose(got.permute(0, 3, 1, 2).numpy(), ref.numpy(), atol=1e-10)
+
+
+def test_useful_start_idx():
+    from models.data_process import get_useful_start_idx, get_useful_start_idx_LFB, SeqSampler
+    # reference semantics (data_process.py:307-315): per video, starts count..count+len-seq
+    assert get_useful_start_idx(3, [4, 5]) == [0, 1, 4, 5, 6]
+    assert get_useful_start_idx_LFB(1, [2, 1]) == [0, 1, 2]
+    assert list(SeqSampler(None, [3, 1, 2])) == [3, 1, 2]
+
+
+def test_synthetic_dataset_contract():
+    from models.data_process import SyntheticCholecFlowDataset
+    ds = SyntheticCholecFlowDataset(3)
+    img, seg, flow, ph, ant = ds[1]
+    assert img.shape == (3, 224, 224) and seg.shape == (3, 224, 224) and flow.shape == (2, 224, 224)
+    assert ph.dtype == np.int64 and ant.dtype == np.float64 and ant.shape == (7,)
+    img2 = ds[1][0]
+    assert torch.equal(img, img2)

@@ -1,0 +1,219 @@
+"""Per-kernel parity of the svk HIP kernels against plain torch CPU references (fp64 math on the
+same, dtype-rounded inputs).  Tolerances: f32 path (exact f32 MFMA products, f32 accumulation)
+rtol/atol 2e-5 relative to the output scale; bf16 path 1e-2 (inputs identical, outputs rounded to
+bf16 — 8 significant bits)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DTS = [torch.float32, torch.bfloat16]
+
+
+def _tol(dt):
+    return (2e-5, 2e-5) if dt == torch.float32 else (1.2e-2, 1.2e-2)
+
+
+def _close(got, ref, dt, scale=None):
+    rtol, atol = _tol(dt)
+    ref = ref.double()
+    s = float(ref.abs().max()) if scale is None else scale
+    torch.testing.assert_close(got.double().cpu(), ref, rtol=rtol, atol=atol * max(1.0, s))
+
+
+def _rand(*shape, dt, dev, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dt).to(dev)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("M,N,K", [(1, 7, 2048), (100, 64, 64), (777, 200, 320), (4096, 256, 64), (300, 14, 14),
+                                   (513, 2048, 1024), (49, 33, 147)])
+@pytest.mark.parametrize("act", [None, "gelu", "relu", "tanh"])
+def test_gemm(cuda, dt, M, N, K, act):
+    from svk import ops
+    a = _rand(M, K, dt=dt, dev=cuda, seed=1)
+    w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=2)
+    b = _rand(N, dt=torch.float32, dev=cuda, seed=3)
+    r = _rand(M, N, dt=dt, dev=cuda, seed=4)
+    got = ops.gemm(a, w, b, act=act, residual=r)
+    torch.cuda.synchronize()
+    ref = a.cpu().double() @ w.cpu().double().t() + b.cpu().double()
+    ref = {None: lambda t: t, "gelu": lambda t: F.gelu(t), "relu": torch.relu, "tanh": torch.tanh}[act](ref)
+    ref = ref + r.cpu().double()
+    _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_gemm_strided_views(cuda, dt):
+    """kv[:, :, :C] style inputs and writes into a column slice (head concat buffer)."""
+    from svk import ops
+    a_full = _rand(3, 50, 96, dt=dt, dev=cuda, seed=5)
+    a = a_full[:, :, 16:80]                       # row stride 96, K = 64
+    w = _rand(40, 64, dt=dt, dev=cuda, scale=0.125, seed=6)
+    out_full = torch.zeros(3, 50, 100, device=cuda, dtype=dt)
+    ops.gemm(a, w, out=out_full[:, :, 30:70])
+    torch.cuda.synchronize()
+    ref = a.cpu().double() @ w.cpu().double().t()
+    _close(out_full[:, :, 30:70], ref, dt)
+    assert float(out_full[:, :, :30].abs().max()) == 0 and float(out_full[:, :, 70:].abs().max()) == 0
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p", [(2, 224, 224, 3, 64, 7, 4, 3), (2, 56, 56, 64, 128, 3, 2, 1),
+                                                  (3, 56, 56, 64, 64, 8, 8, 0), (2, 224, 224, 2, 64, 7, 4, 3),
+                                                  (1, 14, 14, 320, 512, 3, 2, 1), (2, 28, 28, 32, 80, 3, 2, 1),
+                                                  (2, 14, 14, 320, 320, 2, 2, 0)])
+def test_conv2d_nhwc(cuda, dt, B, H, W, Cin, Cout, k, s, p):
+    from svk import ops
+    from svk.pack import conv_w
+    x = _rand(B, H, W, Cin, dt=dt, dev=cuda, seed=7)
+    w = _rand(Cout, Cin, k, k, dt=torch.float32, dev="cpu", scale=(Cin * k * k) ** -0.5, seed=8).to(dt)
+    b = _rand(Cout, dt=torch.float32, dev=cuda, seed=9)
+    got = ops.conv2d_nhwc(x, conv_w(w, dt).to(cuda), k, s, p, bias=b, act="relu")
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.cpu().double().permute(0, 3, 1, 2), w.double(), b.cpu().double(), stride=s, padding=p)
+    _close(got, torch.relu(ref).permute(0, 2, 3, 1), dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("M,C,eps", [(1000, 64, 1e-6), (333, 320, 1e-5), (64, 512, 1e-6), (17, 14, 1e-5),
+                                     (9, 2048, 1e-5), (5, 16, 1e-5)])
+def test_layernorm(cuda, dt, M, C, eps):
+    from svk import ops
+    x = _rand(M, C, dt=dt, dev=cuda, scale=3.0, seed=10) + 0.5
+    g = _rand(C, dt=torch.float32, dev=cuda, seed=11)
+    b = _rand(C, dt=torch.float32, dev=cuda, seed=12)
+    got = ops.layernorm(x, g, b, eps)
+    torch.cuda.synchronize()
+    ref = F.layer_norm(x.cpu().double(), (C,), g.cpu().double(), b.cpu().double(), eps)
+    _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("B,Nq,Nk,heads,hd", [(2, 3136, 49, 1, 64), (2, 784, 49, 2, 64), (3, 196, 196, 8, 40),
+                                              (2, 49, 49, 8, 64), (5, 30, 30, 4, 32), (7, 1, 1, 4, 32),
+                                              (2, 196, 49, 5, 32), (1, 100, 256, 1, 64)])
+def test_attention(cuda, dt, B, Nq, Nk, heads, hd):
+    from svk import ops
+    C = heads * hd
+    q = _rand(B, Nq, C, dt=dt, dev=cuda, seed=13)
+    kv = _rand(B, Nk, 2 * C, dt=dt, dev=cuda, seed=14)
+    k, v = kv[:, :, :C], kv[:, :, C:]
+    scale = hd ** -0.5
+    got = ops.attention(q, k, v, heads, scale)
+    torch.cuda.synchronize()
+    qh = q.cpu().double().reshape(B, Nq, heads, hd).transpose(1, 2)
+    kh = k.cpu().double().reshape(B, Nk, heads, hd).transpose(1, 2)
+    vh = v.cpu().double().reshape(B, Nk, heads, hd).transpose(1, 2)
+    ref = ((qh @ kh.transpose(-1, -2)) * scale).softmax(-1) @ vh
+    _close(got, ref.transpose(1, 2).reshape(B, Nq, C), dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 256), (1, 7, 7, 2048), (2, 14, 14, 1280), (1, 5, 6, 12)])
+def test_dwconv3x3_gelu(cuda, dt, B, H, W, C):
+    from svk import ops
+    x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=15)
+    w = _rand(C, 1, 3, 3, dt=torch.float32, dev="cpu", scale=0.4, seed=16)
+    b = _rand(C, dt=torch.float32, dev=cuda, seed=17)
+    got = ops.dwconv3x3(x, w.reshape(C, 9).t().contiguous().to(cuda), b, act="gelu")
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.cpu().double().permute(0, 3, 1, 2), w.double(), b.cpu().double(), padding=1, groups=C)
+    _close(got, F.gelu(ref).permute(0, 2, 3, 1), dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_pack_and_gauss(cuda, dt):
+    from svk import ops
+    x = _rand(2, 3, 224, 224, dt=torch.float32, dev=cuda, seed=18)
+    got = ops.nchw_to_nhwc(x, dt)
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), x.cpu().permute(0, 2, 3, 1).to(dt))
+    gg = ops.gauss5x5_reflect(x, dt)
+    torch.cuda.synchronize()
+    k = torch.tensor([1., 4., 6., 4., 1.], dtype=torch.float64)
+    k = (torch.outer(k, k) / 256.).repeat(3, 1, 1, 1)
+    ref = F.conv2d(F.pad(x.cpu().double(), (2, 2, 2, 2), mode="reflect"), k, groups=3)
+    _close(gg, ref.permute(0, 2, 3, 1), dt)
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("H,OH", [(56, 7), (28, 7), (14, 7), (7, 7), (10, 4)])
+def test_resize_bilinear(cuda, dt, H, OH):
+    from svk import ops
+    C = 24
+    x = _rand(2, H * H, C, dt=dt, dev=cuda, seed=19)
+    out = torch.zeros(2, OH * OH, 2 * C, device=cuda, dtype=dt)
+    ops.resize_bilinear(x, H, H, OH, OH, out=out[:, :, C:])
+    torch.cuda.synchronize()
+    ref = F.interpolate(x.cpu().double().transpose(1, 2).reshape(2, C, H, H), (OH, OH), None, "bilinear", False)
+    _close(out[:, :, C:], ref.flatten(2).transpose(1, 2), dt)
+    assert float(out[:, :, :C].abs().max()) == 0
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_mean_rows(cuda, dt):
+    from svk import ops
+    x = _rand(5 * 49, 2048, dt=dt, dev=cuda, seed=20)
+    got = ops.mean_rows(x, 49)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(got.cpu().double(), x.cpu().double().reshape(5, 49, 2048).mean(1), rtol=1e-5, atol=1e-5)
+
+
+def test_softmax_rows(cuda):
+    from svk import ops
+    x = _rand(1000, 14, dt=torch.float32, dev=cuda, scale=4.0, seed=21)
+    got = ops.softmax_rows(x)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(got.cpu().double(), x.cpu().double().softmax(-1), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("F_,T,d,causal", [(32, 300, 1, True), (32, 300, 64, True), (64, 2456, 512, True),
+                                           (64, 130, 4, False), (32, 77, 128, False), (20, 50, 2, True)])
+def test_mstcn_layer(cuda, F_, T, d, causal):
+    from svk import ops
+    x = _rand(T, F_, dt=torch.float32, dev=cuda, seed=22)
+    wd = _rand(F_, F_, 3, dt=torch.float32, dev="cpu", scale=F_ ** -0.5, seed=23)
+    bd = _rand(F_, dt=torch.float32, dev=cuda, seed=24)
+    w1 = _rand(F_, F_, dt=torch.float32, dev=cuda, scale=F_ ** -0.5, seed=25)
+    b1 = _rand(F_, dt=torch.float32, dev=cuda, seed=26)
+    got = ops.mstcn_layer(x, wd.permute(2, 0, 1).contiguous().to(cuda), bd, w1, b1, d, causal)
+    torch.cuda.synchronize()
+    xc = x.cpu().double().t()[None]
+    pad = 2 * d if causal else d
+    h = torch.relu(F.conv1d(xc, wd.double(), bd.cpu().double(), padding=pad, dilation=d))
+    if causal:
+        h = h[:, :, :-2 * d]
+    ref = xc + F.conv1d(h, w1.cpu().double()[:, :, None], b1.cpu().double())
+    torch.testing.assert_close(got.cpu().double(), ref[0].t(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("dt", DTS)
+def test_window_unfold_and_add(cuda, dt):
+    from svk import ops
+    x = _rand(75, 14, dt=dt, dev=cuda, seed=27)
+    pos = _rand(30, 14, dt=torch.float32, dev=cuda, seed=28)
+    got = ops.window_unfold(x, 30, pos=pos)
+    torch.cuda.synchronize()
+    xc = x.cpu().double()
+    padded = torch.cat([torch.zeros(29, 14, dtype=torch.float64), xc], 0)
+    ref = padded.unfold(0, 30, 1).transpose(1, 2) + pos.cpu().double()
+    _close(got, ref, dt)
+    plain = ops.window_unfold(x, 30)
+    added = ops.add_bcast(plain, pos)
+    torch.cuda.synchronize()
+    _close(added, ref, dt)
+
+
+def test_cast(cuda):
+    from svk import ops
+    x = _rand(1001, dt=torch.float32, dev=cuda, seed=29)
+    y = ops.cast(x, torch.bfloat16)
+    z = ops.cast(y, torch.float32)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), x.cpu().to(torch.bfloat16))
+    assert torch.equal(z.cpu(), y.cpu().float())
