@@ -77,6 +77,165 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ Q,
     if (d < hd && (d & 3) == sub) out[d] = from_f<T>(o[d]);
 }
 
+// ---------------------------------------------------------------------------------------------
+// bf16 MFMA attention (v_mfma_f32_16x16x32_bf16).  Workgroup = 4 waves = 64 queries of one
+// (batch, head); each wave owns 16 queries.  Keys are processed in chunks of 64 staged in LDS
+// (K row-major, V transposed), with an online softmax across chunks (one chunk for MiT's 49
+// reduced keys).
+//
+// Scores are computed transposed, S^T = K . Q^T (A = K rows from LDS, B = the wave's Q rows held
+// in registers), so a lane's accumulator column is ONE query (lane & 15) and its 4 rows are keys
+// 16t + 4g + r (g = lane >> 4).  The softmax max/sum over keys is then in-register + 2 shuffles
+// (across g), and the exponentiated scores feed the P.V MFMA as its A operand without leaving
+// registers: for k-step s the 8 elements of lane group g are keys {32s+4g+j} ++ {32s+16+4g+j}
+// (j < 4), a permutation of the 32 keys that the V fragment read from LDS follows exactly.
+template <int HDP>
+__global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restrict__ Q, long ldq, long sbq,
+                                                           const bf16* __restrict__ K, long ldk, long sbk,
+                                                           const bf16* __restrict__ V, long ldv, long sbv,
+                                                           bf16* __restrict__ O, long ldo, long sbo,
+                                                           int Nq, int Nk, int hd, float scale_log2) {
+  constexpr int KC = 64;
+  constexpr int KLD = HDP + 8;   // sK row stride (elements)
+  constexpr int VLD = KC + 8;    // sVt row stride (elements)
+  constexpr int NKS = HDP / 32;  // k-steps over the head dim
+  constexpr int NDT = HDP / 16;  // 16-wide output column tiles
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) bf16 sK[KC][KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sVt[HDP][VLD];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const int q0 = blockIdx.x * 64 + wave * 16;
+  const bf16* Qb = Q + (long)b * sbq + (long)h * hd;
+  const bf16* Kb = K + (long)b * sbk + (long)h * hd;
+  const bf16* Vb = V + (long)b * sbv + (long)h * hd;
+  const bool vec = (hd == HDP) && ((ldq | ldk | ldv) % 8 == 0) &&
+                   ((((uintptr_t)Qb) | ((uintptr_t)Kb) | ((uintptr_t)Vb)) & 15) == 0;
+
+  bf16x8 qf[NKS];
+  {
+    const int qr = q0 + c;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d0 = 32 * ks + 8 * g;
+      if (qr < Nq && vec) {
+        qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * ldq + d0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[ks][j] = (qr < Nq && d0 + j < hd) ? Qb[(long)qr * ldq + d0 + j] : (bf16)0.f;
+      }
+    }
+  }
+
+  f32x4 o[NDT];
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  for (int kc0 = 0; kc0 < Nk; kc0 += KC) {
+    __syncthreads();
+    for (int e = tid; e < KC * (HDP / 8); e += 256) {
+      const int key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
+      const int kg = kc0 + key;
+      bf16x8 kv, vv;
+      if (kg < Nk && vec) {
+        kv = *reinterpret_cast<const bf16x8*>(Kb + (long)kg * ldk + d0);
+        vv = *reinterpret_cast<const bf16x8*>(Vb + (long)kg * ldv + d0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const bool ok = kg < Nk && d0 + j < hd;
+          kv[j] = ok ? Kb[(long)kg * ldk + d0 + j] : (bf16)0.f;
+          vv[j] = ok ? Vb[(long)kg * ldv + d0 + j] : (bf16)0.f;
+        }
+      }
+      *reinterpret_cast<bf16x8*>(&sK[key][d0]) = kv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[j];
+    }
+    __syncthreads();
+
+    f32x4 s[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sK[16 * t + c][32 * ks + 8 * g]);
+        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], s[t], 0, 0, 0);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kc0 + 16 * t + 4 * g + r;
+        const float v = key < Nk ? s[t][r] * scale_log2 : -INFINITY;
+        s[t][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f(m_run - m_new);    // 0 on the first chunk
+    float ps = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = exp2f(s[t][r] - m_new);
+        s[t][r] = p;
+        ps += p;
+      }
+    ps += __shfl_xor(ps, 16, 64);
+    ps += __shfl_xor(ps, 32, 64);
+    l_run = l_run * alpha + ps;
+    m_run = m_new;
+    if (kc0 > 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) o[dt][r] *= ar;
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 pa;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pa[j] = (bf16)s[2 * s2][j];
+        pa[4 + j] = (bf16)s[2 * s2 + 1][j];
+      }
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) {
+        const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][32 * s2 + 4 * g]);
+        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][32 * s2 + 16 + 4 * g]);
+        bf16x8 vb;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { vb[j] = v0[j]; vb[4 + j] = v1[j]; }
+        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+      }
+    }
+  }
+
+  bf16* Ob = O + (long)b * sbo + (long)h * hd;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qr = q0 + 4 * g + r;
+    const float inv = 1.0f / __shfl(l_run, 4 * g + r, 64);
+    if (qr >= Nq) continue;
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) {
+      const int d = 16 * dt + c;
+      if (d < hd) Ob[(long)qr * ldo + d] = (bf16)(o[dt][r] * inv);
+    }
+  }
+}
+
 }  // namespace svk
 
 using namespace svk;
@@ -92,6 +251,16 @@ extern "C" int svk_attention(int dtype, const void* Q, long ldq, long sbq, const
   if (B > 65535 || heads > 65535) { set_error("svk_attention: grid too large"); return SVK_EUNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((Nq + 63) / 64, heads, B), block(256);
+  if (dtype == SVK_BF16) {
+    const float sl2 = scale * 1.4426950408889634f;   // softmax via exp2
+    if (hd <= 32)
+      hipLaunchKernelGGL((attention_mfma_bf16<32>), grid, block, 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K, ldk,
+                         sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);
+    else
+      hipLaunchKernelGGL((attention_mfma_bf16<64>), grid, block, 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K, ldk,
+                         sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);
+    return check_launch("attention_mfma_bf16");
+  }
   SVK_DISPATCH_DTYPE(dtype, T, {
     const size_t sm = (size_t)2 * Nk * hd * sizeof(float);
     if (hd <= 32) {
