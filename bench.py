@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--no-flow", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-gemm", default=None, help="write per-shape GEMM timings to this file (rank 0)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -126,14 +127,20 @@ def main():
     value = frames / elapsed
 
     # dominant kernel: the GEMM instantiation with the most measured device time
-    per = {}
-    for name, flops, nbytes, s, e in records:
+    per, shapes = {}, {}
+    for name, flops, nbytes, s, e, shape in records:
         ms = s.elapsed_time(e)
-        tot = per.setdefault(name, [0.0, 0.0, 0.0, 0])
-        tot[0] += ms
-        tot[1] += flops
-        tot[2] += nbytes
-        tot[3] += 1
+        for key, d in ((name, per), ((name, str(shape)), shapes)):
+            tot = d.setdefault(key, [0.0, 0.0, 0.0, 0])
+            tot[0] += ms
+            tot[1] += flops
+            tot[2] += nbytes
+            tot[3] += 1
+    if args.dump_gemm and rank == 0:
+        with open(args.dump_gemm, "w") as f:
+            for (name, shape), (ms, fl, nb, n) in sorted(shapes.items(), key=lambda kv: -kv[1][0]):
+                f.write(f"{ms / args.steps:8.3f} ms/step n={n // args.steps:3d} {fl / ms / 1e9:8.1f} TF/s "
+                        f"{nb / ms / 1e6:8.1f} GB/s  {shape:28s} {name}\n")
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
     achieved = flops / (ms * 1e-3) / 1e12

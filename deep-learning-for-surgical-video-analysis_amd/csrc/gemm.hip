@@ -7,15 +7,24 @@
 // holds 8 consecutive k of row (l & 15), so every fragment read is one 16-byte LDS
 // read and every global load is a 16-byte vector.
 //
-// Tile: BM x BN x 32, 256 threads = 4 waves arranged 2 x 2, each wave owning a
-// (BM/2) x (BN/2) sub-tile of 16x16 MFMA blocks.  LDS is double-buffered; the next
-// K-tile is fetched into registers while the MFMAs of the current one run (one
-// __syncthreads per K-step).
+// Tile: BM x BN x BK (BK = 64 bf16 / 32 f32), 256 threads = 4 waves arranged 2 x 2, each
+// wave owning a (BM/2) x (BN/2) sub-tile of 16x16 MFMA blocks.  LDS is double-buffered;
+// the next K-tile is fetched into registers while the MFMAs of the current one run (one
+// __syncthreads per K-step).  LDS rows are padded by 16 bytes: a 16-lane ds_read_b128
+// group then touches 16 distinct 4-bank slots (row stride 144 B).
+//
+// Epilogue: bias + activation are applied in registers, the f32 tile is staged through
+// LDS (reusing the operand buffers), and written back as 16-byte row chunks with the
+// residual read the same way — the MFMA C layout would otherwise scatter 2-byte stores.
+//
+// Workgroup -> tile mapping is XCD-aware: the hardware deals consecutive workgroups
+// round-robin over the 8 XCDs, so the 1-D grid is remapped so that each XCD receives a
+// contiguous run of tiles (n fastest), i.e. the tiles sharing an A row-panel share an L2.
 //
 // dtype f32 uses v_mfma_f32_16x16x4_f32 (exact f32 products, the parity path): the
-// 8 k a lane holds for one 32-deep K-step are consumed by 8 MFMAs, MFMA s using
-// element s of every lane group — a permutation of the k order inside the step,
-// which leaves the dot product mathematically unchanged.
+// 8 k a lane holds for one 32-deep step are consumed by 8 MFMAs, MFMA s using element s
+// of every lane group — a permutation of the k order inside the step, which leaves the
+// dot product mathematically unchanged.
 //
 // ASRC = 1 turns the A loader into an im2col gather from an NHWC map (implicit-GEMM
 // convolution, weights packed [Cout][kh][kw][Cin] so that k = (i*kw + j)*Cin + ci).
@@ -23,7 +32,6 @@
 
 namespace svk {
 
-constexpr int BK = 32;
 constexpr int NTHREADS = 256;
 
 struct GemmArgs {
@@ -33,6 +41,7 @@ struct GemmArgs {
   const void* R; long ldr;
   void* C; long ldc;
   int M, N, K, act;
+  int vec_out;          // C (and R) rows 16-byte aligned with whole chunks -> vector epilogue
   // implicit-GEMM conv geometry (ASRC == 1)
   int H, Wd, Cin, OH, OW, kw, stride, pad;
 };
@@ -54,7 +63,7 @@ __device__ __forceinline__ void zero8(Chunk<T>& c) {
   for (int j = 0; j < 8; ++j) c.v[j] = from_f<T>(0.f);
 }
 template <typename T>
-__device__ __forceinline__ void store_lds8(T* dst, const Chunk<T>& c) {
+__device__ __forceinline__ void store8(T* dst, const Chunk<T>& c) {
   if constexpr (sizeof(T) == 2) {
     *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(c.v);
   } else {
@@ -63,42 +72,81 @@ __device__ __forceinline__ void store_lds8(T* dst, const Chunk<T>& c) {
   }
 }
 
-// Dense row loader: 8 elements of row `row` starting at column k (zero outside [0,rows)x[0,K)).
+// All loaders are branch-free: the address is clamped into the valid range, the load is issued
+// unconditionally and out-of-range elements are zeroed by a select.  (A conditional load makes
+// hipcc branch around it and wait vmcnt(0) per load, serialising the whole K-loop prefetch.)
+// The zeroing select is applied when the chunk is written to LDS (after the K-step's MFMAs),
+// never right after the load, so that the loads stay in flight across the MFMAs.
+// `mask` bit e set = element e valid.
 template <typename T, bool VEC>
-__device__ __forceinline__ void load_dense(const T* base, long ld, int row, int rows, int k, int K, Chunk<T>& c) {
-  if (row >= rows) { zero8(c); return; }
-  const T* p = base + (long)row * ld + k;
-  if (VEC && k + 8 <= K) { load_vec8(p, c); return; }
+__device__ __forceinline__ void apply_mask8(Chunk<T>& c, unsigned mask) {
+  if constexpr (VEC) {   // all-or-nothing chunks
+    uint32_t* w = reinterpret_cast<uint32_t*>(c.v);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) c.v[j] = (k + j < K) ? p[j] : from_f<T>(0.f);
+    for (int j = 0; j < (int)(8 * sizeof(T) / 4); ++j) w[j] = mask ? w[j] : 0u;
+  } else if constexpr (sizeof(T) == 2) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(c.v);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t keep = ((mask >> (2 * j)) & 1 ? 0x0000FFFFu : 0u) | ((mask >> (2 * j + 1)) & 1 ? 0xFFFF0000u : 0u);
+      w[j] &= keep;
+    }
+  } else {
+    uint32_t* w = reinterpret_cast<uint32_t*>(c.v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w[j] = (mask >> j) & 1 ? w[j] : 0u;
+  }
+}
+
+// Dense row loader: 8 elements of row `row` starting at column k (zero outside [0,rows)x[0,K)).
+// VEC requires K % 8 == 0 and 16-byte aligned rows.  Returns the validity mask.
+template <typename T, bool VEC>
+__device__ __forceinline__ unsigned load_dense(const T* base, long ld, int row, int rows, int k, int K, Chunk<T>& c) {
+  const int rc = row < rows ? row : rows - 1;
+  if (VEC) {
+    const int kc = k < K ? k : K - 8;
+    load_vec8(base + (long)rc * ld + kc, c);
+    return (row < rows && k < K) ? 0xFFu : 0u;
+  }
+  const T* p = base + (long)rc * ld;
+  unsigned m = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int kk = k + j;
+    c.v[j] = p[kk < K ? kk : K - 1];
+    m |= (row < rows && kk < K) ? (1u << j) : 0u;
+  }
+  return m;
 }
 
 struct ConvRow { long base; int iy0, ix0; bool valid; };
 
 template <typename T, bool VEC>
-__device__ __forceinline__ void load_im2col(const T* X, const GemmArgs& p, const ConvRow& r, int k, Chunk<T>& c) {
-  if (!r.valid) { zero8(c); return; }
+__device__ __forceinline__ unsigned load_im2col(const T* X, const GemmArgs& p, const ConvRow& r, int k, Chunk<T>& c) {
   if (VEC) {  // Cin % 8 == 0: the 8 k of a chunk share one tap
-    if (k >= p.K) { zero8(c); return; }
-    int tap = k / p.Cin, ci = k - tap * p.Cin;
-    int i = tap / p.kw, j = tap - i * p.kw;
-    int iy = r.iy0 + i, ix = r.ix0 + j;
-    if (iy < 0 || iy >= p.H || ix < 0 || ix >= p.Wd) { zero8(c); return; }
-    load_vec8(X + r.base + ((long)iy * p.Wd + ix) * p.Cin + ci, c);
-    return;
+    const int kc = k < p.K ? k : p.K - 8;
+    const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+    const int i = tap / p.kw, j = tap - i * p.kw;
+    const int iy = r.iy0 + i, ix = r.ix0 + j;
+    const bool ok = r.valid && k < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.Wd;
+    const int iyc = min(max(iy, 0), p.H - 1), ixc = min(max(ix, 0), p.Wd - 1);
+    load_vec8(X + r.base + ((long)iyc * p.Wd + ixc) * p.Cin + ci, c);
+    return ok ? 0xFFu : 0u;
   }
+  unsigned m = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    int kk = k + e;
-    T v = from_f<T>(0.f);
-    if (kk < p.K) {
-      int tap = kk / p.Cin, ci = kk - tap * p.Cin;
-      int i = tap / p.kw, j = tap - i * p.kw;
-      int iy = r.iy0 + i, ix = r.ix0 + j;
-      if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.Wd) v = X[r.base + ((long)iy * p.Wd + ix) * p.Cin + ci];
-    }
-    c.v[e] = v;
+    const int kk = k + e;
+    const int kc = kk < p.K ? kk : p.K - 1;
+    const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+    const int i = tap / p.kw, j = tap - i * p.kw;
+    const int iy = r.iy0 + i, ix = r.ix0 + j;
+    const bool ok = r.valid && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.Wd;
+    const int iyc = min(max(iy, 0), p.H - 1), ixc = min(max(ix, 0), p.Wd - 1);
+    c.v[e] = X[r.base + ((long)iyc * p.Wd + ixc) * p.Cin + ci];
+    m |= ok ? (1u << e) : 0u;
   }
+  return m;
 }
 
 template <typename T>
@@ -113,33 +161,55 @@ __device__ __forceinline__ void mfma_step(const Chunk<T>& a, const Chunk<T>& b, 
   }
 }
 
+// Bijective XCD remap of a 1-D grid (cdna_hip_programming.md §5 "XCD swizzle must be bijective").
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <typename T> constexpr int bk_of() { return sizeof(T) == 2 ? 64 : 32; }
+
+template <typename T, int BM, int BN>
+constexpr int smem_bytes() {
+  constexpr int BK = bk_of<T>(), LDK = BK + 16 / (int)sizeof(T);
+  constexpr int main_b = 2 * (BM + BN) * LDK * (int)sizeof(T);
+  constexpr int epi_b = BM * (BN + 4) * 4;
+  return main_b > epi_b ? main_b : epi_b;
+}
+
 template <typename T, int BM, int BN, bool VEC, int ASRC>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
-  constexpr int PADK = 16 / sizeof(T);
-  constexpr int LDK = BK + PADK;
+  constexpr int BK = bk_of<T>();
+  constexpr int LDK = BK + 16 / sizeof(T);
+  constexpr int CPR = BK / 8;                       // 8-element chunks per tile row
+  constexpr int RPP = NTHREADS / CPR;               // rows covered per loader pass
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ACH = BM * (BK / 8) / NTHREADS;   // A chunks per thread
-  constexpr int BCH = BN * (BK / 8) / NTHREADS;
+  constexpr int ACH = BM / RPP, BCH = BN / RPP;     // loader chunks per thread
+  constexpr int LDC = BN + 4;                       // f32 epilogue tile row stride
   static_assert(ACH >= 1 && BCH >= 1, "tile too small");
 
-  __shared__ __attribute__((aligned(16))) T sA[2][BM][LDK];
-  __shared__ __attribute__((aligned(16))) T sB[2][BN][LDK];
+  __shared__ __attribute__((aligned(16))) char smem[smem_bytes<T, BM, BN>()];
+  T (*sA)[BM][LDK] = reinterpret_cast<T (*)[BM][LDK]>(smem);
+  T (*sB)[BN][LDK] = reinterpret_cast<T (*)[BN][LDK]>(smem + 2 * BM * LDK * sizeof(T));
+  float (*sC)[LDC] = reinterpret_cast<float (*)[LDC]>(smem);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int ntm = (p.M + BM - 1) / BM;
+  const int tile = xcd_remap(blockIdx.x, ntm * ntn);
+  const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
   const T* A = static_cast<const T*>(p.A);
   const T* Wt = static_cast<const T*>(p.W);
 
-  // Each thread loads chunk (row = tid/4 + 64*i, kc = tid%4) of the A and B tiles.
-  const int lrow = tid >> 2, lk = (tid & 3) * 8;
+  const int lrow = tid / CPR, lk = (tid % CPR) * 8;
   ConvRow crow[ACH];
   if constexpr (ASRC == 1) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      int m = m0 + lrow + 64 * i;
+      int m = m0 + lrow + RPP * i;
       crow[i].valid = m < p.M;
       int mm = crow[i].valid ? m : 0;
       int hw = p.OH * p.OW;
@@ -152,20 +222,21 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
   }
 
   Chunk<T> ra[ACH], rb[BCH];
+  unsigned ma[ACH], mb[BCH];
   auto fetch = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
-      if constexpr (ASRC == 1) load_im2col<T, VEC>(A, p, crow[i], k0 + lk, ra[i]);
-      else load_dense<T, VEC>(A, p.lda, m0 + lrow + 64 * i, p.M, k0 + lk, p.K, ra[i]);
+      if constexpr (ASRC == 1) ma[i] = load_im2col<T, VEC>(A, p, crow[i], k0 + lk, ra[i]);
+      else ma[i] = load_dense<T, VEC>(A, p.lda, m0 + lrow + RPP * i, p.M, k0 + lk, p.K, ra[i]);
     }
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) load_dense<T, VEC>(Wt, p.ldw, n0 + lrow + 64 * i, p.N, k0 + lk, p.K, rb[i]);
+    for (int i = 0; i < BCH; ++i) mb[i] = load_dense<T, VEC>(Wt, p.ldw, n0 + lrow + RPP * i, p.N, k0 + lk, p.K, rb[i]);
   };
   auto stash = [&](int buf) {
 #pragma unroll
-    for (int i = 0; i < ACH; ++i) store_lds8(&sA[buf][lrow + 64 * i][lk], ra[i]);
+    for (int i = 0; i < ACH; ++i) { apply_mask8<T, VEC>(ra[i], ma[i]); store8(&sA[buf][lrow + RPP * i][lk], ra[i]); }
 #pragma unroll
-    for (int i = 0; i < BCH; ++i) store_lds8(&sB[buf][lrow + 64 * i][lk], rb[i]);
+    for (int i = 0; i < BCH; ++i) { apply_mask8<T, VEC>(rb[i], mb[i]); store8(&sB[buf][lrow + RPP * i][lk], rb[i]); }
   };
 
   f32x4 acc[TM][TN];
@@ -182,37 +253,72 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
   const int fr = lane & 15, fk = (lane >> 4) * 8;
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) fetch((kt + 1) * BK);
-    Chunk<T> fa[TM], fb[TN];
+    fetch((kt + 1) * BK);     // past the end: clamped addresses, fully masked (no branch in the loop)
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
 #pragma unroll
-    for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const Chunk<T>*>(&sA[buf][wm * WM + i * 16 + fr][fk]);
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      Chunk<T> fa[TM], fb[TN];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const Chunk<T>*>(&sB[buf][wn * WN + j * 16 + fr][fk]);
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const Chunk<T>*>(&sA[buf][wm * WM + i * 16 + fr][ks * 32 + fk]);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const Chunk<T>*>(&sB[buf][wn * WN + j * 16 + fr][ks * 32 + fk]);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) mfma_step<T>(fa[i], fb[j], acc[i][j]);
-    if (kt + 1 < nk) stash(buf ^ 1);
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) mfma_step<T>(fa[i], fb[j], acc[i][j]);
+    }
+    stash(buf ^ 1);
     __syncthreads();
   }
 
-  // Epilogue: C/D map of the 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + r.
-  T* C = static_cast<T*>(p.C);
-  const T* R = static_cast<const T*>(p.R);
+  // Epilogue part 1: bias + activation in registers, f32 tile -> LDS.
+  // C/D map of the 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + r.
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + fr;
-    if (n >= p.N) continue;
-    const float bn = p.bias ? p.bias[n] : 0.f;
+    const int cl = wn * WN + j * 16 + fr;
+    const int n = n0 + cl;
+    const float bn = (p.bias && n < p.N) ? p.bias[n] : 0.f;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m >= p.M) continue;
-        float v = apply_act(acc[i][j][r] + bn, p.act);
-        if (R) v += to_f(R[(long)m * p.ldr + n]);
-        C[(long)m * p.ldc + n] = from_f<T>(v);
+      for (int r = 0; r < 4; ++r)
+        sC[wm * WM + i * 16 + (lane >> 4) * 4 + r][cl] = apply_act(acc[i][j][r] + bn, p.act);
+  }
+  __syncthreads();
+
+  // Epilogue part 2: 8-column row chunks, residual added in f32, 16-byte stores.
+  T* C = static_cast<T*>(p.C);
+  const T* R = static_cast<const T*>(p.R);
+  constexpr int CH = BN / 8;
+#pragma unroll
+  for (int it = 0; it < (BM * CH) / NTHREADS; ++it) {
+    const int cidx = tid + it * NTHREADS;
+    const int row = cidx / CH, c8 = (cidx % CH) * 8;
+    const int m = m0 + row, n = n0 + c8;
+    if (m >= p.M || n >= p.N) continue;
+    float v[8];
+    *reinterpret_cast<float4*>(&v[0]) = *reinterpret_cast<const float4*>(&sC[row][c8]);
+    *reinterpret_cast<float4*>(&v[4]) = *reinterpret_cast<const float4*>(&sC[row][c8 + 4]);
+    if (p.vec_out && n + 8 <= p.N) {
+      if (R) {
+        Chunk<T> rr;
+        load_vec8(R + (long)m * p.ldr + n, rr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += to_f(rr.v[e]);
+      }
+      Chunk<T> o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o.v[e] = from_f<T>(v[e]);
+      store8(C + (long)m * p.ldc + n, o);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (n + e >= p.N) break;
+        float x = v[e];
+        if (R) x += to_f(R[(long)m * p.ldr + n + e]);
+        C[(long)m * p.ldc + n + e] = from_f<T>(x);
       }
     }
   }
@@ -221,11 +327,14 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
 template <typename T, int ASRC>
-static int launch_gemm(const GemmArgs& a, bool vec, hipStream_t st) {
+static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
   const int M = a.M, N = a.N;
+  const long vw = 16 / (long)sizeof(T);
+  a.vec_out = aligned16(a.C) && (a.ldc % vw == 0) && (!a.R || (aligned16(a.R) && a.ldr % vw == 0));
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;
-    dim3 grid((N + BN - 1) / BN, (M + BM - 1) / BM);
+    const long nwg = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+    dim3 grid((unsigned)nwg);
     if (vec) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, ASRC>), grid, dim3(NTHREADS), 0, st, a);
     else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, ASRC>), grid, dim3(NTHREADS), 0, st, a);
   };
@@ -255,7 +364,7 @@ extern "C" int svk_gemm(int dtype, const void* A, long lda, const void* W, long 
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
     const long vecw = 16 / (long)sizeof(T);
-    bool vec = aligned16(A) && aligned16(W) && (lda % vecw == 0) && (ldw % vecw == 0);
+    bool vec = aligned16(A) && aligned16(W) && (lda % vecw == 0) && (ldw % vecw == 0) && (K % 8 == 0);
     return launch_gemm<T, 0>(a, vec, st);
   });
 }

@@ -48,6 +48,85 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const T* __restrict__ X,
   }
 }
 
+// Vectorised LayerNorm: each lane owns NCH 8-channel chunks (16-byte bf16 / 32-byte f32 loads),
+// LPR lanes cooperate on one row (LPR = power of two >= C/8), 64/LPR rows per wave; the row
+// reductions are xor-shuffles inside the LPR-lane group.  Used when C % 8 == 0 and rows are
+// 16-byte aligned (every LayerNorm of the MiT path: C = 16..512).
+template <typename T, int LPR, int NCH>
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const T* __restrict__ X, long ldx, T* __restrict__ Y,
+                                                            long ldy, const float* __restrict__ g,
+                                                            const float* __restrict__ b, int M, int C, float eps) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane % LPR;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool valid = row < M;
+  const int nchunks = C >> 3;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = sub + LPR * i;
+    if (valid && ch < nchunks) {
+      const T* src = X + row * ldx + ch * 8;
+      T t[8];
+      if constexpr (sizeof(T) == 2) {
+        *reinterpret_cast<uint4*>(t) = *reinterpret_cast<const uint4*>(src);
+      } else {
+        reinterpret_cast<uint4*>(t)[0] = reinterpret_cast<const uint4*>(src)[0];
+        reinterpret_cast<uint4*>(t)[1] = reinterpret_cast<const uint4*>(src)[1];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { v[i][e] = to_f(t[e]); s += v[i][e]; }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = sub + LPR * i;
+    if (ch < nchunks) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = 1.0f / sqrtf(q / C + eps);
+  if (!valid) return;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = sub + LPR * i;
+    if (ch >= nchunks) continue;
+    T t[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = ch * 8 + e;
+      t[e] = from_f<T>((v[i][e] - mean) * rstd * g[c] + b[c]);
+    }
+    T* dst = Y + row * ldy + ch * 8;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(t);
+    } else {
+      reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(t)[0];
+      reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(t)[1];
+    }
+  }
+}
+
+template <typename T, int LPR, int NCH>
+static void launch_ln_vec(const T* x, long ldx, T* y, long ldy, const float* g, const float* b, int M, int C,
+                          float eps, hipStream_t st) {
+  constexpr int RPB = 4 * (64 / LPR);   // rows per 256-thread block
+  hipLaunchKernelGGL((layernorm_vec_kernel<T, LPR, NCH>), dim3((M + RPB - 1) / RPB), dim3(256), 0, st, x, ldx, y, ldy,
+                     g, b, M, C, eps);
+}
+
 // Softmax over C (small) channels per row, one thread per row (MS-TCN's 14-class softmax).
 __global__ void softmax_rows_kernel(const float* __restrict__ X, long ldx, float* __restrict__ Y, long ldy, int M, int C) {
   const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -86,6 +165,22 @@ extern "C" int svk_layernorm(int dtype, const void* X, long ldx, void* Y, long l
   dim3 grid((M + 3) / 4), block(256);
   SVK_DISPATCH_DTYPE(dtype, T, {
     const T* x = (const T*)X; T* y = (T*)Y;
+    const long vw = 16 / (long)sizeof(T);
+    const bool vec = C % 8 == 0 && C <= 4096 && ldx % vw == 0 && ldy % vw == 0 && ((((uintptr_t)X) | ((uintptr_t)Y)) & 15) == 0;
+    if (vec) {
+      const int nch = C / 8;
+      if (nch <= 1) launch_ln_vec<T, 1, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 2) launch_ln_vec<T, 2, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 4) launch_ln_vec<T, 4, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 8) launch_ln_vec<T, 8, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 16) launch_ln_vec<T, 16, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 32) launch_ln_vec<T, 32, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 64) launch_ln_vec<T, 64, 1>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 128) launch_ln_vec<T, 64, 2>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else if (nch <= 256) launch_ln_vec<T, 64, 4>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      else launch_ln_vec<T, 64, 8>(x, ldx, y, ldy, gamma, beta, M, C, eps, st);
+      return check_launch("layernorm");
+    }
     if (C <= 64) hipLaunchKernelGGL((layernorm_kernel<T, 1>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
     else if (C <= 128) hipLaunchKernelGGL((layernorm_kernel<T, 2>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);
     else if (C <= 256) hipLaunchKernelGGL((layernorm_kernel<T, 4>), grid, block, 0, st, x, ldx, y, ldy, gamma, beta, M, C, eps);

@@ -84,12 +84,12 @@ def _prof_begin():
     return e
 
 
-def _prof_end(start, name, flops, nbytes):
+def _prof_end(start, name, flops, nbytes, shape=None):
     if start is None:
         return
     e = torch.cuda.Event(enable_timing=True)
     e.record()
-    _PROF.append((name, flops, nbytes, start, e))
+    _PROF.append((name, flops, nbytes, start, e, shape))
 
 
 def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None):
@@ -116,7 +116,7 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None):
         vw = 16 // es
         vec = a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and lda % vw == 0 and w.stride(0) % vw == 0
         nb = (M * K + N * K + M * N * (2 if residual is not None else 1)) * es
-        _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0), 2.0 * M * N * K, nb)
+        _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0), 2.0 * M * N * K, nb, (M, N, K))
     return out
 
 
@@ -142,7 +142,8 @@ def conv2d_nhwc(x, w_packed, k, stride, pad, bias=None, act=None, residual=None)
         M, K = B * OH * OW, k * k * Cin
         vec = x.data_ptr() % 16 == 0 and w_packed.data_ptr() % 16 == 0 and Cin % 8 == 0
         nb = (x.numel() + Cout * K + M * Cout) * x.element_size()
-        _prof_end(t0, _gemm_kernel_name(dtype_code(x.dtype), M, Cout, vec, 1), 2.0 * M * Cout * K, nb)
+        _prof_end(t0, _gemm_kernel_name(dtype_code(x.dtype), M, Cout, vec, 1), 2.0 * M * Cout * K, nb,
+                  (M, Cout, K, f"conv{k}s{stride}"))
     return out
 
 

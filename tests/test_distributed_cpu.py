@@ -1,0 +1,69 @@
+"""Multi-process (gloo, world size 2) test of the data-parallel extraction sharding: every frame is
+processed by exactly one rank and the gathered feature bank equals the single-process one, in
+order.  The per-frame 'extractor' here is a deterministic CPU stand-in (the real extractor needs
+the GPU); what is under test is the shard/gather plumbing bench.py and the LFB writer use."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _fake_features(idx):
+    g = torch.Generator().manual_seed(0)
+    w = torch.randn(1, 16, generator=g)
+    return torch.sin(idx.float()[:, None] * w)
+
+
+def _worker(rank, world, port, n, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "deep-learning-for-surgical-video-analysis_amd"))
+    from svk.shard import shard_range, gather_rows
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    a, b = shard_range(n, rank, world)
+    local = _fake_features(torch.arange(a, b))
+    full = gather_rows(local, n)
+    t = torch.tensor([float(b - a)])
+    dist.all_reduce(t)
+    out[rank] = (full.clone(), int(t.item()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [10, 7, 1])
+def test_shard_gather_world2(n):
+    world = 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_worker, args=(world, _free_port(), n, out), nprocs=world, join=True)
+    ref = _fake_features(torch.arange(n))
+    for r in range(world):
+        full, total = out[r]
+        assert total == n
+        torch.testing.assert_close(full, ref)
+
+
+def test_shard_range_properties():
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "deep-learning-for-surgical-video-analysis_amd"))
+    from svk.shard import shard_range
+    for n in (0, 1, 5, 1000, 98234):
+        for world in (1, 2, 3, 8):
+            spans = [shard_range(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(spans[i][1] == spans[i + 1][0] for i in range(world - 1))
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
