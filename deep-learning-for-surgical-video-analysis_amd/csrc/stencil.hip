@@ -82,14 +82,15 @@ __global__ void dwconv3x3_scalar(const T* __restrict__ X, const float* __restric
 // ---- NCHW f32 -> NHWC T --------------------------------------------------------------------
 // One thread per pixel, all C channels: reads coalesced along W within each channel plane.
 template <typename T>
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W) {
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W,
+                                    int Cpad) {
   const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long hw = (long)H * W;
   if (pix >= (long)B * hw) return;
   const long b = pix / hw, p = pix - b * hw;
   const float* src = X + b * C * hw + p;
-  T* dst = Y + pix * C;
-  for (int c = 0; c < C; ++c) dst[c] = from_f<T>(src[(long)c * hw]);
+  T* dst = Y + pix * Cpad;
+  for (int c = 0; c < Cpad; ++c) dst[c] = from_f<T>(c < C ? src[(long)c * hw] : 0.f);
 }
 
 // ---- GaussianFilter.conv_gauss: reflect pad 2 + binomial 5x5 / 256 (mix_transformer_evp.py:501-514)
@@ -102,7 +103,7 @@ __device__ __forceinline__ int reflect(int i, int n) {
 // One thread per output pixel, looping over channels: the 25 taps of neighbouring threads are
 // neighbouring addresses of one NCHW plane (coalesced), output written NHWC.
 template <typename T>
-__global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W) {
+__global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W, int Cpad) {
   const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (pix >= (long)B * H * W) return;
   const int x = (int)(pix % W);
@@ -120,8 +121,9 @@ __global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, 
     for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int j = 0; j < 5; ++j) acc += src[(long)yy[i] * W + xx[j]] * (k1[i] * k1[j] * (1.0f / 256.f));
-    Y[pix * C + c] = from_f<T>(acc);
+    Y[pix * Cpad + c] = from_f<T>(acc);
   }
+  for (int c = C; c < Cpad; ++c) Y[pix * Cpad + c] = from_f<T>(0.f);
 }
 
 // ---- bilinear resize, align_corners=False, no antialias (F.interpolate semantics) ----------
@@ -215,22 +217,24 @@ extern "C" int svk_dwconv3x3(int dtype, const void* X, const float* w, const flo
   });
 }
 
-extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, void* stream) {
-  if (B < 0 || C <= 0 || H <= 0 || W <= 0 || !X || !Y) { set_error("svk_nchw_to_nhwc: bad args"); return SVK_EINVAL; }
+extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
+                                void* stream) {
+  if (B < 0 || C <= 0 || Cpad < C || H <= 0 || W <= 0 || !X || !Y) { set_error("svk_nchw_to_nhwc: bad args"); return SVK_EINVAL; }
   if (B == 0) return SVK_OK;
   const long n = (long)B * H * W;   // one thread per pixel
   SVK_DISPATCH_DTYPE(dtype_out, T, {
-    hipLaunchKernelGGL((nchw_to_nhwc_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W);
+    hipLaunchKernelGGL((nchw_to_nhwc_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W, Cpad);
     return check_launch("nchw_to_nhwc");
   });
 }
 
-extern "C" int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, void* stream) {
-  if (B < 0 || C <= 0 || H < 3 || W < 3 || !X || !Y) { set_error("svk_gauss5x5_reflect: bad args"); return SVK_EINVAL; }
+extern "C" int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
+                                    void* stream) {
+  if (B < 0 || C <= 0 || Cpad < C || H < 3 || W < 3 || !X || !Y) { set_error("svk_gauss5x5_reflect: bad args"); return SVK_EINVAL; }
   if (B == 0) return SVK_OK;
   const long n = (long)B * H * W;   // one thread per pixel
   SVK_DISPATCH_DTYPE(dtype_out, T, {
-    hipLaunchKernelGGL((gauss5x5_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W);
+    hipLaunchKernelGGL((gauss5x5_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W, Cpad);
     return check_launch("gauss5x5_reflect");
   });
 }

@@ -28,10 +28,12 @@ def check_inference(module, *tensors):
 
 
 def to_nhwc(x, dtype):
-    """[B, C, H, W] (any float) -> contiguous NHWC in the compute dtype via the svk packing kernel."""
+    """[B, C, H, W] (any float) -> contiguous NHWC in the compute dtype via the svk packing kernel,
+    channels zero-padded per svk.pack.pad_channels (2/3-channel inputs -> 8)."""
+    from svk.pack import pad_channels
     if x.dtype != torch.float32:
         x = x.float()
-    return ops.nchw_to_nhwc(x.contiguous(), dtype)
+    return ops.nchw_to_nhwc(x.contiguous(), dtype, cpad=pad_channels(x.shape[1]))
 
 
 class DropPath(nn.Module):

@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from svk import ops
-from svk.pack import get_packed, lin_w, lin_b, conv_w, fold_bn
+from svk.pack import get_packed, lin_w, lin_b, conv_w, fold_bn, pad_channels
 from visualizer import get_local
 from ._common import pair, compute_dtype, check_inference, to_nhwc, DropPath
 from .segformer_head import SegFormerHead
@@ -167,10 +167,15 @@ class OverlapPatchEmbed(nn.Module):
 
     def _pack(self, dt):
         g, b = _ln_params(self.norm)
-        return dict(w=conv_w(self.proj.weight, dt), b=self.proj.bias.detach().float().contiguous(), g=g, beta=b)
+        cin = self.proj.weight.shape[1]
+        return dict(w=conv_w(self.proj.weight, dt, pad_channels(cin)), b=self.proj.bias.detach().float().contiguous(),
+                    g=g, beta=b)
 
     def embed_nhwc(self, x):
-        """x [B, H, W, Cin] NHWC (compute dtype) -> (tokens [B, OH*OW, C], OH, OW)."""
+        """x [B, H, W, Cin'] NHWC (compute dtype, Cin' = pad_channels(Cin)) -> (tokens [B, OH*OW, C], OH, OW)."""
+        if x.shape[-1] != pad_channels(self.proj.weight.shape[1]):
+            raise ValueError(f"OverlapPatchEmbed: NHWC input has {x.shape[-1]} channels, expected "
+                             f"{pad_channels(self.proj.weight.shape[1])}")
         p = get_packed(self, x.dtype, self._pack)
         k = self.patch_size[0]
         y = ops.conv2d_nhwc(x, p["w"], k, self.stride, k // 2, bias=p["b"])
@@ -199,8 +204,8 @@ class GaussianFilter(nn.Module):
         return (torch.outer(k, k) / 256.).repeat(channels, 1, 1, 1)
 
     def conv_gauss(self, img):
-        """NCHW f32 -> filtered map, returned NHWC in the compute dtype."""
-        return ops.gauss5x5_reflect(img.float(), compute_dtype(self))
+        """NCHW f32 -> filtered map, returned NHWC in the compute dtype (channels padded to 8)."""
+        return ops.gauss5x5_reflect(img.float(), compute_dtype(self), cpad=pad_channels(img.shape[1]))
 
 
 class PromptGenerator(nn.Module):
@@ -311,7 +316,7 @@ class OpticalFlowEncoder(nn.Module):
         p = {}
         for i in range(1, 5):
             w, b = fold_bn(getattr(self, f"conv{i}").weight, getattr(self, f"conv{i}").bias, getattr(self, f"bn{i}"))
-            p[f"w{i}"] = conv_w(w, dt)
+            p[f"w{i}"] = conv_w(w, dt, pad_channels(w.shape[1]))
             p[f"b{i}"] = b.float().contiguous()
         return p
 

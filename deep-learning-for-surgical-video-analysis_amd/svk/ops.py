@@ -184,21 +184,24 @@ def dwconv3x3(x, taps, bias, act=None):
     return out
 
 
-def nchw_to_nhwc(x, dtype):
+def nchw_to_nhwc(x, dtype, cpad=None):
+    """[B, C, H, W] f32 -> [B, H, W, cpad] (channels >= C zero) in ``dtype``."""
     _chk(x, "x", torch.float32)
     x = x.contiguous()
     B, C, H, W = x.shape
-    out = torch.empty(B, H, W, C, device=x.device, dtype=dtype)
-    _lib.call("svk_nchw_to_nhwc", dtype_code(dtype), _p(x), _p(out), B, C, H, W, _stream())
+    cpad = C if cpad is None else cpad
+    out = torch.empty(B, H, W, cpad, device=x.device, dtype=dtype)
+    _lib.call("svk_nchw_to_nhwc", dtype_code(dtype), _p(x), _p(out), B, C, H, W, cpad, _stream())
     return out
 
 
-def gauss5x5_reflect(x, dtype):
+def gauss5x5_reflect(x, dtype, cpad=None):
     _chk(x, "x", torch.float32)
     x = x.contiguous()
     B, C, H, W = x.shape
-    out = torch.empty(B, H, W, C, device=x.device, dtype=dtype)
-    _lib.call("svk_gauss5x5_reflect", dtype_code(dtype), _p(x), _p(out), B, C, H, W, _stream())
+    cpad = C if cpad is None else cpad
+    out = torch.empty(B, H, W, cpad, device=x.device, dtype=dtype)
+    _lib.call("svk_gauss5x5_reflect", dtype_code(dtype), _p(x), _p(out), B, C, H, W, cpad, _stream())
     return out
 
 

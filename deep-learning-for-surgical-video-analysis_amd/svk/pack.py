@@ -41,10 +41,21 @@ def lin_b(linear):
     return None if linear.bias is None else linear.bias.detach().float().contiguous()
 
 
-def conv_w(weight, dtype):
-    """[Cout, Cin, k, k] -> [Cout, k*k*Cin] in (kh, kw, ci) order (the implicit-GEMM K order)."""
-    co = weight.shape[0]
-    return weight.detach().permute(0, 2, 3, 1).reshape(co, -1).to(dtype).contiguous()
+def pad_channels(cin):
+    """Input channel count the NHWC maps of a conv with ``cin`` inputs are stored with: 2/3-channel
+    inputs (frames, segmap, flow) are zero-padded to 8 so the implicit-GEMM conv can use 16-byte
+    loads (one 8-channel chunk per tap)."""
+    return 8 if cin < 8 else cin
+
+
+def conv_w(weight, dtype, cin_pad=None):
+    """[Cout, Cin, k, k] -> [Cout, k*k*Cin'] in (kh, kw, ci) order (the implicit-GEMM K order),
+    Cin' = cin_pad (zero weights for the padded input channels) or Cin."""
+    co, ci = weight.shape[:2]
+    w = weight.detach().permute(0, 2, 3, 1)
+    if cin_pad is not None and cin_pad > ci:
+        w = torch.nn.functional.pad(w, (0, cin_pad - ci))
+    return w.reshape(co, -1).to(dtype).contiguous()
 
 
 def fold_bn(weight, bias, bn):

@@ -72,12 +72,14 @@ int svk_attention(int dtype, const void* Q, long ldq, long sbq, const void* K, l
 int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B,
                   int H, int W, int C, int act, void* stream);
 
-/* NCHW f32 -> NHWC dtype (input packing of frames / flow; view(-1,3,224,224) at :354). */
-int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, void* stream);
+/* NCHW f32 -> NHWC dtype with the channel dim zero-padded to Cpad >= C (input packing of frames /
+ * flow, view(-1,3,224,224) at :354; padding to 8 lets the first convs take the vector path). */
+int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
+                     void* stream);
 
 /* GaussianFilter.conv_gauss (mix_transformer_evp.py:511-514): reflect-pad 2 + binomial 5x5/256,
- * NCHW f32 in -> NHWC dtype out. */
-int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W,
+ * NCHW f32 in -> NHWC dtype out, channels zero-padded to Cpad >= C. */
+int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
                          void* stream);
 
 /* Bilinear resize (align_corners=False) of NHWC token maps [B, H*W, C] (row stride ldx)

@@ -139,6 +139,12 @@ def test_pack_and_gauss(cuda, dt):
     k = (torch.outer(k, k) / 256.).repeat(3, 1, 1, 1)
     ref = F.conv2d(F.pad(x.cpu().double(), (2, 2, 2, 2), mode="reflect"), k, groups=3)
     _close(gg, ref.permute(0, 2, 3, 1), dt)
+    # channel padding to 8 (vector path of the first convs): padded channels are exactly zero
+    p8 = ops.nchw_to_nhwc(x, dt, cpad=8)
+    g8 = ops.gauss5x5_reflect(x, dt, cpad=8)
+    torch.cuda.synchronize()
+    assert torch.equal(p8[..., :3].cpu(), got.cpu()) and float(p8[..., 3:].abs().max()) == 0
+    assert torch.equal(g8[..., :3].cpu(), gg.cpu()) and float(g8[..., 3:].abs().max()) == 0
 
 
 @pytest.mark.parametrize("dt", DTS)
