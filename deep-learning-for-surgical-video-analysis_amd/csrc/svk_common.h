@@ -24,6 +24,21 @@ template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// Branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute): one rcp, one exp, five
+// FMAs — no range-split branches, so a wave never diverges.  Used by the bf16 kernels, whose outputs
+// are rounded to 8 significant bits anyway; the f32 parity path keeps erff.
+__device__ __forceinline__ float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float y = 1.0f - p * t * __expf(-ax * ax);
+  return copysignf(y, x);
+}
+__device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
+
 __device__ __forceinline__ float apply_act(float v, int act) {
   switch (act) {
     case SVK_ACT_GELU: return gelu_erf(v);

@@ -70,6 +70,15 @@ class Mlp(nn.Module):
 
     def forward(self, x, H, W, residual=None):
         p = get_packed(self, x.dtype, self._pack)
+        B, N, C = x.shape
+        if (ops.FUSED_MIXFFN and residual is not None and x.dtype == torch.bfloat16 and C in ops.MIXFFN_CHANNELS
+                and self.fc1.out_features == 4 * C and self.fc2.out_features == C):
+            # one kernel: fc1 -> dwconv3x3 -> GELU -> fc2 -> + residual, hidden kept on chip
+            # (opt-in, SVK_FUSED_MIXFFN=1: measured slower than the three-kernel path so far)
+            pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
+            y = ops.mixffn_fused(x.contiguous().view(B, H, W, C), residual.contiguous().view(B, H, W, C),
+                                 p["w1"], p["b1"], pd["taps"], pd["b"], p["w2"], p["b2"])
+            return y.view(B, N, C)
         h = ops.gemm(x, p["w1"], p["b1"])
         h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)
         return ops.gemm(h, p["w2"], p["b2"], residual=residual)

@@ -30,6 +30,7 @@ SIGNATURES = {
     "svk_mstcn_layer": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_window_unfold": [c_int, P, c_long, P, P, c_int, c_int, c_int, P],
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
+    "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
 }
 STRING_FUNCS = ("svk_version", "svk_last_error")

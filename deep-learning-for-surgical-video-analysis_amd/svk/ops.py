@@ -5,6 +5,8 @@ output through the PyTorch caching allocator (the library never allocates) and
 launches on the current stream.  There is deliberately no CPU path: a CPU tensor
 is an error.
 """
+import os
+
 import torch
 
 from . import _lib
@@ -172,6 +174,31 @@ def attention(q, k, v, heads, scale, out=None):
     _lib.call("svk_attention", dtype_code(q.dtype), _p(q), q.stride(1), q.stride(0), _p(k), k.stride(1), k.stride(0),
               _p(v), v.stride(1), v.stride(0), _p(out), out.stride(1), out.stride(0), B, Nq, Nk, heads, hd,
               float(scale), _stream())
+    return out
+
+
+MIXFFN_CHANNELS = (32, 64, 128)
+FUSED_MIXFFN = os.environ.get("SVK_FUSED_MIXFFN", "0") == "1"
+
+
+def mixffn_fused(xn, x, w1, b1, taps, dbias, w2, b2):
+    """x + fc2(GELU(dwconv3x3(fc1(xn)))) on NHWC [B, H, W, C] bf16 maps (hidden kept on chip)."""
+    for t, nm in ((xn, "xn"), (x, "x"), (w1, "w1"), (w2, "w2")):
+        _chk(t, nm, torch.bfloat16)
+        if not t.is_contiguous():
+            raise _lib.SvkError(f"svk.mixffn_fused: {nm} must be contiguous")
+    for t, nm in ((b1, "b1"), (taps, "taps"), (dbias, "dbias"), (b2, "b2")):
+        _chk(t, nm, torch.float32)
+    B, H, W, C = xn.shape
+    if x.shape != xn.shape or w1.shape != (4 * C, C) or w2.shape != (C, 4 * C) or taps.shape != (9, 4 * C):
+        raise _lib.SvkError("svk.mixffn_fused: shape mismatch")
+    out = torch.empty_like(x)
+    t0 = _prof_begin()
+    _lib.call("svk_mixffn_fused", BF16, _p(xn), _p(x), _p(w1), _p(b1), _p(taps), _p(dbias), _p(w2), _p(b2),
+              _p(out), B, H, W, C, _stream())
+    if t0 is not None:
+        M = B * H * W
+        _prof_end(t0, f"mixffn_bf16<{C}>", 2.0 * M * C * 4 * C * 2, (3 * M * C + 8 * C * C) * 2, (M, C, "mixffn"))
     return out
 
 

@@ -72,6 +72,14 @@ int svk_attention(int dtype, const void* Q, long ldq, long sbq, const void* K, l
 int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B,
                   int H, int W, int C, int act, void* stream);
 
+/* Fused MixFFN + Block residual (mix_transformer_evp.py:32-67, 19-30, 169), bf16 only:
+ * Y = X + fc2(GELU(dwconv3x3(fc1(XN)))) over NHWC [B, H, W, C] maps, hidden 4C kept on chip.
+ * W1 [4C][C], W2 [C][4C] bf16; b1 [4C], taps [9][4C], dbias [4C], b2 [C] f32.  C in {32, 64, 128};
+ * SVK_EUNSUPPORTED otherwise (callers then run svk_gemm + svk_dwconv3x3 + svk_gemm). */
+int svk_mixffn_fused(int dtype, const void* XN, const void* X, const void* W1, const float* b1,
+                     const float* taps, const float* dbias, const void* W2, const float* b2, void* Y,
+                     int B, int H, int W, int C, void* stream);
+
 /* NCHW f32 -> NHWC dtype with the channel dim zero-padded to Cpad >= C (input packing of frames /
  * flow, view(-1,3,224,224) at :354; padding to 8 lets the first convs take the vector path). */
 int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,

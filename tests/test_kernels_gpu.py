@@ -126,6 +126,32 @@ def test_dwconv3x3_gelu(cuda, dt, B, H, W, C):
     _close(got, F.gelu(ref).permute(0, 2, 3, 1), dt)
 
 
+@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (2, 28, 28, 128), (3, 14, 14, 128), (2, 56, 56, 32),
+                                     (1, 10, 17, 64), (2, 7, 7, 32), (1, 28, 28, 64)])
+def test_mixffn_fused(cuda, B, H, W, C):
+    """Fused fc1 -> dwconv3x3 -> GELU -> fc2 + residual (bf16) against fp64 torch on the same
+    bf16-rounded inputs; the reference path also rounds the hidden to bf16 at the same two points
+    (after fc1, after GELU) as the unfused svk path does."""
+    from svk import ops
+    dt = torch.bfloat16
+    xn = _rand(B, H, W, C, dt=dt, dev=cuda, seed=40)
+    x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=41)
+    w1 = _rand(4 * C, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=42)
+    b1 = _rand(4 * C, dt=torch.float32, dev=cuda, scale=0.1, seed=43)
+    taps = _rand(9, 4 * C, dt=torch.float32, dev=cuda, scale=0.3, seed=44)
+    db = _rand(4 * C, dt=torch.float32, dev=cuda, scale=0.1, seed=45)
+    w2 = _rand(C, 4 * C, dt=dt, dev=cuda, scale=(4 * C) ** -0.5, seed=46)
+    b2 = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=47)
+    got = ops.mixffn_fused(xn, x, w1, b1, taps, db, w2, b2)
+    torch.cuda.synchronize()
+    h = (xn.cpu().double() @ w1.cpu().double().t() + b1.cpu().double()).to(dt).double()
+    hc = h.permute(0, 3, 1, 2)
+    k = taps.cpu().double().t().reshape(4 * C, 1, 3, 3)
+    g = F.gelu(F.conv2d(hc, k, db.cpu().double(), padding=1, groups=4 * C)).permute(0, 2, 3, 1).to(dt).double()
+    ref = x.cpu().double() + g @ w2.cpu().double().t() + b2.cpu().double()
+    _close(got, ref, dt)
+
+
 @pytest.mark.parametrize("dt", DTS)
 def test_pack_and_gauss(cuda, dt):
     from svk import ops
