@@ -1,10 +1,15 @@
-"""Benchmark: SegFormer/MiT-b2-EVP LFB feature extraction (generate_evp_LFB.py's hot loop) on
-MI355X — frames/s at 224x224 with optical-flow fusion, return_features=True ([B, 2048]).
+"""Benchmark of the surgical-phase hot path on MI355X.
 
-One step = one forward of a B-frame batch (default B = 256) whose frames, segmaps and flow are
-already resident in HBM.  Multi-GPU: one process per GPU (torchrun), frames shard across ranks
-with no data-path collective: weak scaling, value = all ranks' frames / the
-slowest rank's time.  Rank 0 prints ONE JSON line.
+Default workload (the headline, BASELINE.json metric): SegFormer/MiT-b2-EVP LFB feature
+extraction (generate_evp_LFB.py's hot loop) — frames/s at 224x224 with optical-flow fusion,
+return_features=True ([B, 2048]).  One step = one forward of a B-frame batch (default B = 256)
+whose frames, segmaps and flow are already resident in HBM.  Other workloads (``--workload``):
+``mstcn`` (config 3: MultiStageModel_S(4,10,64,256) over 40 full-length videos) and ``e2e``
+(config 5: SegFormer -> MS-TCN(2,8,32,2048) -> Transformer(len 30) on 256-frame chunks).
+
+Multi-GPU: one process per GPU (torchrun); units shard across ranks with no data-path collective
+(SURVEY.md §8(e)): weak scaling, value = all ranks' units / the slowest rank's time.  Rank 0
+prints ONE JSON line.
 
 Roofline: the dominant kernel (the MFMA GEMM / implicit-GEMM conv instantiation with the most
 device time) is timed live with HIP events around each of its launches inside the timed region;
@@ -17,6 +22,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -25,6 +31,7 @@ sys.path.insert(0, os.path.join(REPO, "deep-learning-for-surgical-video-analysis
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}     # MI355X dense MFMA (MI355X_MICROARCH.md)
+DATA = "synthetic (seeded Cholec80-shaped frames/segmaps/flow, resident in HBM; random-init weights)"
 
 
 def synthetic_batch(B, dev, seed):
@@ -42,10 +49,15 @@ def synthetic_batch(B, dev, seed):
     return x.contiguous(), y.contiguous(), flow
 
 
-def cpu_baseline(variant, budget_s=20.0, batch=4):
+def video_lengths(n=40, seed=0):
+    """Seeded test-split-like video lengths, U[1000, 6000] frames at 1 fps."""
+    return [int(t) for t in np.random.default_rng(6000 + seed).integers(1000, 6001, size=n)]
+
+
+# ---------------------------------------------------------------------------------------------
+def cpu_baseline_extract(variant, budget_s, batch=4):
     """Oracle (torch CPU, fp32, the reference's op order) on a bounded sample of the same workload."""
     from oracle import inputs as I, params as P, mit_evp as M, shapes as SH
-    cores = torch.get_num_threads()
     sd = P.make_state_dict(SH.mit_evp_shapes(variant), 0)
     x, y, fl = I.frames(batch, 1), I.segmaps(batch, 1), I.flow(batch, 1)
     with torch.no_grad():
@@ -55,8 +67,99 @@ def cpu_baseline(variant, budget_s=20.0, batch=4):
             M.forward(x, y, sd, variant, fl, return_features=True)
             n += 1
         dt = time.perf_counter() - t0
-    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": cores, "kind": "port",
+    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"{n} batches x {batch} frames ({variant} + flow, fp32, return_features) in {dt:.1f} s"}
+
+
+def cpu_baseline_mstcn(budget_s, T=2456):
+    from oracle import params as P, mstcn as MS, shapes as SH, inputs as I
+    sd = P.make_state_dict(SH.mstcn_shapes(4, 10, 64, 256, 14), 1)
+    x = I.lfb(T, 256, 7).transpose(2, 1)
+    with torch.no_grad():
+        MS.multi_stage_s(x, sd, 4, 10, True)
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s or n == 0:
+            MS.multi_stage_s(x, sd, 4, 10, True)
+            n += 1
+        dt = time.perf_counter() - t0
+    return {"value": round(n * T / dt, 1), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} videos x {T} frames (MultiStageModel_S(4,10,64,256,14,causal), fp32) in {dt:.1f} s"}
+
+
+# ---------------------------------------------------------------------------------------------
+def workload_extract(args, dev, rank, dtype):
+    from models import mix_transformer_evp as mte
+    torch.manual_seed(0)                      # random-init weights of the real architecture
+    model = getattr(mte, args.variant)()
+    model.svk_dtype = dtype
+    model = model.to(dev).eval()
+    for p in model.parameters():
+        p.requires_grad_(False)
+    x, y, fl = synthetic_batch(args.batch, dev, seed=1234 + rank)
+    if args.no_flow:
+        fl = None
+
+    def step():
+        return model(x, y, fl, return_features=True)
+
+    def check(out):
+        assert out.shape == (args.batch, 2048) and torch.isfinite(out).all()
+
+    config = {"workload": f"generate_evp_LFB feature extraction: {args.variant} + "
+                          f"{'no flow' if args.no_flow else 'optical-flow cross-attn fusion'}, "
+                          f"224x224, return_features -> [B, 2048]",
+              "model": args.variant, "per_gpu_batch": args.batch}
+    return step, args.batch, config, check, (lambda: cpu_baseline_extract(args.variant, args.cpu_baseline_seconds))
+
+
+def workload_mstcn(args, dev, rank, dtype):
+    from models import mstcn
+    torch.manual_seed(0)
+    model = mstcn.MultiStageModel_S(4, 10, 64, 256, 14, True).to(dev).eval()
+    lens = video_lengths(40, seed=rank)
+    feats = [torch.randn(1, T, 256, device=dev) for T in lens]
+
+    def step():
+        out = None
+        for f in feats:
+            out = model(f.transpose(2, 1))
+        return out
+
+    def check(out):
+        assert out.shape == (4, 1, 14, lens[-1]) and torch.isfinite(out).all()
+
+    config = {"workload": "tecno.py MS-TCN MultiStageModel_S(4 stages x 10 layers, f_maps 64, f_dim 256, causal) "
+                          "over 40 full-length videos (T ~ U[1000, 6000]) per step",
+              "model": "MultiStageModel_S(4,10,64,256,14,True)", "videos_per_step": 40}
+    return step, sum(lens), config, check, (lambda: cpu_baseline_mstcn(args.cpu_baseline_seconds))
+
+
+def workload_e2e(args, dev, rank, dtype):
+    from models import mix_transformer_evp as mte, mstcn, adapter_transformer
+    torch.manual_seed(0)
+    seg = getattr(mte, args.variant)()
+    seg.svk_dtype = dtype
+    seg = seg.to(dev).eval()
+    tc = mstcn.MultiStageModel_S(2, 8, 32, 2048, 14, True).to(dev).eval()
+    tr = adapter_transformer.Transformer(32, 2048, 14, 30).to(dev).eval()
+    x, y, fl = synthetic_batch(args.batch, dev, seed=1234 + rank)
+
+    def step():
+        f = seg(x, y, fl, return_features=True)[None]          # [1, T, 2048] LFB rows
+        out = tc(f.transpose(2, 1))[-1]                          # [1, 14, T]
+        return tr.original_forward(out, f)                       # [T, 1, 14]
+
+    def check(out):
+        assert out.shape == (args.batch, 1, 14) and torch.isfinite(out).all()
+
+    config = {"workload": f"trans_SV_output end-to-end: {args.variant}+flow features -> MS-TCN(2,8,32,2048,causal) "
+                          f"-> Transformer(len_q 30) on {args.batch}-frame chunks",
+              "model": f"{args.variant} + MultiStageModel_S(2,8,32,2048) + Transformer(32,2048,14,30)",
+              "per_gpu_batch": args.batch}
+    return step, args.batch, config, check, (lambda: cpu_baseline_extract(args.variant, args.cpu_baseline_seconds))
+
+
+WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "e2e": workload_e2e}
 
 
 def main():
@@ -64,6 +167,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="extract", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
     ap.add_argument("--variant", default="mit_b2_evp")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -83,21 +187,9 @@ def main():
 
     import svk
     from svk import ops
-    from models import mix_transformer_evp as mte
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    torch.manual_seed(0)                      # random-init weights of the real architecture
-    model = getattr(mte, args.variant)()
-    model.svk_dtype = dtype
-    model = model.to(dev).eval()
-    for p in model.parameters():
-        p.requires_grad_(False)
-    x, y, fl = synthetic_batch(args.batch, dev, seed=1234 + rank)
-    if args.no_flow:
-        fl = None
-
-    def step():
-        return model(x, y, fl, return_features=True)
+    step, units, config, check, cpu_fn = WORKLOADS[args.workload](args, dev, rank, dtype)
 
     with torch.no_grad():
         for _ in range(args.warmup):
@@ -117,14 +209,13 @@ def main():
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         ops.set_profiler(None)
-    assert out.shape == (args.batch, 2048) and torch.isfinite(out).all()
+    check(out)
 
     dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(dt, op=dist.ReduceOp.MAX)
     elapsed = float(dt.item())
-    frames = world * args.batch * args.steps
-    value = frames / elapsed
+    value = world * units * args.steps / elapsed
 
     # dominant kernel: the GEMM instantiation with the most measured device time
     per, shapes = {}, {}
@@ -144,7 +235,7 @@ def main():
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
     achieved = flops / (ms * 1e-3) / 1e12
-    peak = PEAK_TFLOPS[args.dtype]
+    peak = PEAK_TFLOPS[args.dtype if args.workload != "mstcn" else "fp32"]
     roofline = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
                 "launches_per_step": n // args.steps, "avg_launch_us": round(ms * 1e3 / n, 2),
@@ -153,18 +244,14 @@ def main():
                 "gemm_share_of_step": round(gemm_ms / (elapsed * 1e3), 3)}
 
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.variant, args.cpu_baseline_seconds)
-        line = {"metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
+        cpu = cpu_fn() if (world == 1 and not args.no_cpu_baseline) else None
+        config.update({"global_units_per_step": world * units,
+                       "parallelism": f"dp{world} (shards of independent units, no collective)"})
+        line = {"metric": METRIC if args.workload == "extract" else f"frames/s ({args.workload})",
+                "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
-                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
-                "data": "synthetic (seeded Cholec80-shaped frames/segmaps/flow, resident in HBM; random-init weights)",
-                "config": {"workload": f"generate_evp_LFB feature extraction: {args.variant} + "
-                                       f"{'no flow' if args.no_flow else 'optical-flow cross-attn fusion'}, "
-                                       f"224x224, return_features -> [B, 2048]",
-                           "model": args.variant, "global_batch": world * args.batch, "per_gpu_batch": args.batch,
-                           "parallelism": f"dp{world} (frame shards, no collective)"},
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+                "dtype": "fp32" if args.workload == "mstcn" else args.dtype, "data": DATA, "config": config,
                 "roofline": roofline, "cpu_baseline": cpu, "svk": svk.version()}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -146,6 +146,30 @@ def test_transformer_original_forward_vs_oracle(cuda, golden, T):
     np.testing.assert_allclose(out2.cpu().numpy(), ref.numpy(), rtol=0, atol=1e-4)
 
 
+def test_lfb_extraction_and_pickle(cuda, tmp_path):
+    """generate_evp_LFB-style extraction over a synthetic dataset: rows in index order, equal to a
+    direct forward of the same frames; pickle is the reference's float64 (N, 2048) format."""
+    import pickle
+    from models.data_process import SyntheticCholecFlowDataset
+    from svk.lfb import extract_lfb, save_lfb
+    m = _model("mit_b0_evp", cuda, torch.float32)
+    ds = SyntheticCholecFlowDataset(7, seed=3)
+    bank = extract_lfb(m, ds, batch_size=3)
+    torch.cuda.synchronize()
+    x = torch.stack([ds[i][0] for i in range(7)]).to(cuda)
+    y = torch.stack([ds[i][1] for i in range(7)]).to(cuda)
+    fl = torch.stack([ds[i][2] for i in range(7)]).to(cuda)
+    with torch.no_grad():
+        ref = m(x[:, None], y[:, None], fl[:, None], return_features=True)
+    np.testing.assert_allclose(bank.cpu().numpy(), ref.cpu().numpy(), rtol=0, atol=1e-5)
+    p = tmp_path / "evp_LFB_test.pkl"
+    save_lfb(bank, p, tmp_path / "evp_LFB_test.npy")
+    with open(p, "rb") as f:
+        arr = pickle.load(f)    # our own file
+    assert arr.dtype == np.float64 and arr.shape == (7, 2048)
+    np.testing.assert_allclose(arr, bank.cpu().numpy().astype(np.float64))
+
+
 def test_end_to_end_chunk(cuda):
     """SegFormer(b2) -> MS-TCN(2,8,32,2048) -> Transformer(30) on one synthetic 64-frame clip, fp32,
     against the oracle chain (config 5 shape at reduced length)."""
