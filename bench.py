@@ -4,8 +4,9 @@ Default workload (the headline, BASELINE.json metric): SegFormer/MiT-b2-EVP LFB 
 extraction (generate_evp_LFB.py's hot loop) — frames/s at 224x224 with optical-flow fusion,
 return_features=True ([B, 2048]).  One step = one forward of a B-frame batch (default B = 256)
 whose frames, segmaps and flow are already resident in HBM.  Other workloads (``--workload``):
-``mstcn`` (config 3: MultiStageModel_S(4,10,64,256) over 40 full-length videos) and ``e2e``
-(config 5: SegFormer -> MS-TCN(2,8,32,2048) -> Transformer(len 30) on 256-frame chunks).
+``mstcn`` (config 3: MultiStageModel_S(4,10,64,256) over 40 full-length videos), ``e2e``
+(config 5: SegFormer -> MS-TCN(2,8,32,2048) -> Transformer(len 30) on 256-frame chunks) and
+``train`` (configs 2/4: the train_evp.py stage-1 step, B = 88 per GPU, DDP over RCCL when N > 1).
 
 Multi-GPU: one process per GPU (torchrun); units shard across ranks with no data-path collective
 (SURVEY.md §8(e)): weak scaling, value = all ranks' units / the slowest rank's time.  Rank 0
@@ -159,7 +160,53 @@ def workload_e2e(args, dev, rank, dtype):
     return step, args.batch, config, check, (lambda: cpu_baseline_extract(args.variant, args.cpu_baseline_seconds))
 
 
-WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "e2e": workload_e2e}
+def cpu_baseline_train(variant, budget_s, batch=8):
+    """Oracle train step (torch CPU autograd, fp32, train mode, SGD) on a bounded sample."""
+    from oracle import inputs as I, params as P, shapes as SH, train_evp as TR
+    sd = P.make_state_dict(SH.mit_evp_shapes(variant), 0)
+    x, y, fl = I.frames(batch, 1), I.segmaps(batch, 1), I.flow(batch, 1)
+    lab = torch.randint(0, 7, (batch,), generator=torch.Generator().manual_seed(0))
+    at = torch.rand(batch, 7, generator=torch.Generator().manual_seed(1))
+    masks = TR.make_masks(batch, variant, seed=0)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        _, _, grads, _ = TR.loss_and_grads(x, y, fl, lab, at, sd, variant, masks, dtype=torch.float32)
+        TR.sgd_step({k: sd[k] for k in grads}, grads)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} train steps x {batch} frames ({variant} + flow, fp32 autograd + SGD) in {dt:.1f} s"}
+
+
+def workload_train(args, dev, rank, dtype):
+    """train_evp.py stage-1 step (config 2 / 4): frozen backbone, trainable head + prompts + flow
+    encoder + cross-attention, train mode, CE(sum) + SmoothL1(sum), SGD; DDP when world > 1."""
+    from models import mix_transformer_evp as mte
+    from svk.train import EVPTrainStep
+    torch.manual_seed(0)
+    model = getattr(mte, args.variant)().to(dev)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    tr = EVPTrainStep(model, dtype=dtype, seed=rank, process_group=dist.group.WORLD if world > 1 else None,
+                      world_size=world)
+    x, y, fl = synthetic_batch(args.batch, dev, seed=1234 + rank)
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    lab = torch.randint(0, 7, (args.batch,), generator=g, device=dev)
+    at = torch.rand(args.batch, 7, generator=g, device=dev)
+
+    def step():
+        return tr.step(x, y, fl, lab, at)[0]
+
+    def check(out):
+        assert torch.isfinite(out).all()
+
+    config = {"workload": f"train_evp.py stage-1 step: {args.variant} frozen backbone + trainable head/prompts/"
+                          f"flow encoder/cross-attn ({tr.n_trainable} params), train mode, CE+SmoothL1 (sum), "
+                          f"SGD(lr 5e-4, m 0.9, wd 1e-5)",
+              "model": args.variant, "per_gpu_batch": args.batch}
+    return step, args.batch, config, check, (lambda: cpu_baseline_train(args.variant, args.cpu_baseline_seconds))
+
+
+WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "e2e": workload_e2e, "train": workload_train}
 
 
 def main():
@@ -168,7 +215,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="extract", choices=sorted(WORKLOADS))
-    ap.add_argument("--batch", type=int, default=256, help="frames per GPU per step")
+    ap.add_argument("--batch", type=int, default=None, help="frames per GPU per step (256; train: 88)")
     ap.add_argument("--variant", default="mit_b2_evp")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-flow", action="store_true")
@@ -176,6 +223,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-gemm", default=None, help="write per-shape GEMM timings to this file (rank 0)")
     args = ap.parse_args()
+    if args.batch is None:
+        args.batch = 88 if args.workload == "train" else 256      # train_evp.py:28 / extraction chunk
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -245,9 +294,13 @@ def main():
 
     if rank == 0:
         cpu = cpu_fn() if (world == 1 and not args.no_cpu_baseline) else None
-        config.update({"global_units_per_step": world * units,
-                       "parallelism": f"dp{world} (shards of independent units, no collective)"})
+        par = (f"dp{world} (DDP: one RCCL all-reduce of the flat f32 gradient per step)" if args.workload == "train"
+               else f"dp{world} (shards of independent units, no collective)")
+        config.update({"global_units_per_step": world * units, "parallelism": par})
+        if args.workload == "train":
+            config["steps_per_s"] = round(args.steps / elapsed, 3)
         line = {"metric": METRIC if args.workload == "extract" else f"frames/s ({args.workload})",
+                **({"metric": "train_evp frames/s (step/s x 88 frames/GPU)"} if args.workload == "train" else {}),
                 "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,

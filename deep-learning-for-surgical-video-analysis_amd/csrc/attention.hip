@@ -275,3 +275,135 @@ extern "C" int svk_attention(int dtype, const void* Q, long ldq, long sbq, const
     return check_launch("attention");
   });
 }
+
+// ---- attention backward ------------------------------------------------------------------------
+// One workgroup per (frame, head, QB queries).  K, V (Nk x hd), the QB query rows and their output
+// gradients are staged in LDS as f32; P = softmax(scale Q K^T) is recomputed, then
+//   dP = dO V^T,  dS = P * (dP - rowsum(dO * O)),  dQ = scale dS K   (written directly, T)
+//   dK += scale dS^T Q,  dV += P^T dO                                   (f32 atomics, zeroed by caller)
+// The key/value gradients are partial sums over this workgroup's queries.  All contractions are
+// LDS-resident scalar FMAs (Nk <= 196 at the model's shapes; an MFMA version is future work).
+namespace svk {
+template <typename T>
+__global__ __launch_bounds__(256) void attention_bwd_kernel(const T* __restrict__ Q, long ldq, long sbq,
+                                                            const T* __restrict__ K, long ldk, long sbk,
+                                                            const T* __restrict__ V, long ldv, long sbv,
+                                                            const T* __restrict__ O, long ldo, long sbo,
+                                                            const T* __restrict__ dO, long lddo, long sbdo,
+                                                            T* __restrict__ dQ, long lddq, long sbdq,
+                                                            float* __restrict__ dK, float* __restrict__ dV, long lddk,
+                                                            long sbdk, int Nq, int Nk, int hd, int QB, float scale) {
+  extern __shared__ float sm[];
+  const int hp = hd + 1, kp = Nk + 1;
+  float* sK = sm;
+  float* sV = sK + Nk * hp;
+  float* sQ = sV + Nk * hp;
+  float* sdO = sQ + QB * hp;
+  float* sP = sdO + QB * hp;
+  float* sdS = sP + QB * kp;
+  float* sD = sdS + QB * kp;
+  const int tid = threadIdx.x;
+  const int q0 = blockIdx.x * QB, h = blockIdx.y, b = blockIdx.z;
+  const long co = (long)h * hd;
+  const T* Kb = K + b * sbk + co;
+  const T* Vb = V + b * sbv + co;
+  for (int idx = tid; idx < Nk * hd; idx += 256) {
+    const int j = idx / hd, d = idx - j * hd;
+    sK[j * hp + d] = to_f(Kb[(long)j * ldk + d]);
+    sV[j * hp + d] = to_f(Vb[(long)j * ldv + d]);
+  }
+  for (int idx = tid; idx < QB * hd; idx += 256) {
+    const int q = idx / hd, d = idx - q * hd;
+    const bool ok = q0 + q < Nq;
+    sQ[q * hp + d] = ok ? to_f(Q[b * sbq + (long)(q0 + q) * ldq + co + d]) : 0.f;
+    sdO[q * hp + d] = ok ? to_f(dO[b * sbdo + (long)(q0 + q) * lddo + co + d]) : 0.f;
+  }
+  if (tid < QB) {
+    float acc = 0.f;
+    if (q0 + tid < Nq) {
+      const T* o = O + b * sbo + (long)(q0 + tid) * ldo + co;
+      const T* g = dO + b * sbdo + (long)(q0 + tid) * lddo + co;
+      for (int d = 0; d < hd; ++d) acc += to_f(o[d]) * to_f(g[d]);
+    }
+    sD[tid] = acc;
+  }
+  __syncthreads();
+  for (int idx = tid; idx < QB * Nk; idx += 256) {
+    const int q = idx / Nk, j = idx - q * Nk;
+    float s = 0.f;
+    for (int d = 0; d < hd; ++d) s += sQ[q * hp + d] * sK[j * hp + d];
+    sP[q * kp + j] = s * scale;
+  }
+  __syncthreads();
+  // row softmax: 4 lanes per row
+  {
+    const int q = tid >> 2, sub = tid & 3;
+    if (q < QB) {
+      float m = -INFINITY;
+      for (int j = sub; j < Nk; j += 4) m = fmaxf(m, sP[q * kp + j]);
+      m = fmaxf(m, __shfl_xor(m, 1, 64));
+      m = fmaxf(m, __shfl_xor(m, 2, 64));
+      float l = 0.f;
+      for (int j = sub; j < Nk; j += 4) l += __expf(sP[q * kp + j] - m);
+      l += __shfl_xor(l, 1, 64);
+      l += __shfl_xor(l, 2, 64);
+      const float inv = (q0 + q < Nq) ? 1.f / l : 0.f;
+      for (int j = sub; j < Nk; j += 4) sP[q * kp + j] = __expf(sP[q * kp + j] - m) * inv;
+    }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < QB * Nk; idx += 256) {
+    const int q = idx / Nk, j = idx - q * Nk;
+    float dp = 0.f;
+    for (int d = 0; d < hd; ++d) dp += sdO[q * hp + d] * sV[j * hp + d];
+    sdS[q * kp + j] = sP[q * kp + j] * (dp - sD[q]);
+  }
+  __syncthreads();
+  for (int idx = tid; idx < QB * hd; idx += 256) {
+    const int q = idx / hd, d = idx - q * hd;
+    if (q0 + q >= Nq) continue;
+    float a = 0.f;
+    for (int j = 0; j < Nk; ++j) a += sdS[q * kp + j] * sK[j * hp + d];
+    dQ[b * sbdq + (long)(q0 + q) * lddq + co + d] = from_f<T>(a * scale);
+  }
+  const int qn = min(QB, Nq - q0);
+  for (int idx = tid; idx < Nk * hd; idx += 256) {
+    const int j = idx / hd, d = idx - j * hd;
+    float ak = 0.f, av = 0.f;
+    for (int q = 0; q < qn; ++q) {
+      ak += sdS[q * kp + j] * sQ[q * hp + d];
+      av += sP[q * kp + j] * sdO[q * hp + d];
+    }
+    atomicAdd(dK + b * sbdk + (long)j * lddk + co + d, ak * scale);
+    atomicAdd(dV + b * sbdk + (long)j * lddk + co + d, av);
+  }
+}
+}  // namespace svk
+
+extern "C" int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, const void* K, long ldk, long sbk,
+                                 const void* V, long ldv, long sbv, const void* O, long ldo, long sbo,
+                                 const void* dO, long lddo, long sbdo, void* dQ, long lddq, long sbdq, float* dK,
+                                 float* dV, long lddk, long sbdk, int B, int Nq, int Nk, int heads, int hd,
+                                 float scale, void* stream) {
+  if (B < 0 || Nq < 0 || Nk <= 0 || heads <= 0 || hd <= 0 || hd > 64 || !Q || !K || !V || !O || !dO || !dQ || !dK ||
+      !dV) {
+    set_error("svk_attention_bwd: bad args"); return SVK_EINVAL;
+  }
+  if (B == 0 || Nq == 0) return SVK_OK;
+  auto lds = [&](int qb) { return (size_t)(2 * Nk * (hd + 1) + 2 * qb * (hd + 1) + 2 * qb * (Nk + 1) + qb) * 4; };
+  int QB = 32;
+  while (QB > 8 && lds(QB) > 160 * 1024) QB >>= 1;
+  if (lds(QB) > 160 * 1024) { set_error("svk_attention_bwd: Nk=%d hd=%d exceeds LDS", Nk, hd); return SVK_EUNSUPPORTED; }
+  if (B > 65535 || heads > 65535) { set_error("svk_attention_bwd: grid too large"); return SVK_EUNSUPPORTED; }
+  const size_t sm = lds(QB);
+  dim3 grid((Nq + QB - 1) / QB, heads, B);
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    if (sm > 65536)
+      (void)hipFuncSetAttribute((const void*)attention_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    hipLaunchKernelGGL((attention_bwd_kernel<T>), grid, dim3(256), sm, st, (const T*)Q, ldq, sbq, (const T*)K, ldk, sbk,
+                       (const T*)V, ldv, sbv, (const T*)O, ldo, sbo, (const T*)dO, lddo, sbdo, (T*)dQ, lddq, sbdq, dK,
+                       dV, lddk, sbdk, Nq, Nk, hd, QB, scale);
+    return check_launch("attention_bwd");
+  });
+}

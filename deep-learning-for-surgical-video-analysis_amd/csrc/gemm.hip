@@ -42,8 +42,13 @@ struct GemmArgs {
   void* C; long ldc;
   int M, N, K, act;
   int vec_out;          // C (and R) rows 16-byte aligned with whole chunks -> vector epilogue
-  // implicit-GEMM conv geometry (ASRC == 1)
+  // implicit-GEMM conv geometry.  ASRC == 1 (forward im2col): source map H x Wd x Cin, GEMM rows
+  // are the OH x OW output pixels.  ASRC == 2 (data gradient, transposed-conv gather): source map
+  // is dY (H x Wd x Cin = OHy x OWy x Cout), GEMM rows are the OH x OW input pixels of the conv.
   int H, Wd, Cin, OH, OW, kw, stride, pad;
+  int sshift;           // log2(stride) (ASRC == 2)
+  const float* rscale;  // optional per-row scale of act(A W^T + bias) before the residual add
+  int rdiv;             //   rscale index = m / rdiv (stochastic depth: rdiv = tokens per frame)
 };
 
 template <typename T> struct Chunk { T v[8]; };
@@ -149,6 +154,40 @@ __device__ __forceinline__ unsigned load_im2col(const T* X, const GemmArgs& p, c
   return m;
 }
 
+// Transposed-conv gather for the data gradient of a strided conv: A[m = (b, iy, ix)][k = (i, j, co)]
+// = dY[b, (iy + pad - i) / s, (ix + pad - j) / s, co] when both divisions are exact and in range.
+// r.iy0 / r.ix0 hold iy + pad / ix + pad.  Stride must be a power of two (sshift).
+template <typename T, bool VEC>
+__device__ __forceinline__ unsigned load_col2im(const T* X, const GemmArgs& p, const ConvRow& r, int k, Chunk<T>& c) {
+  const int smask = (1 << p.sshift) - 1;
+  if (VEC) {
+    const int kc = k < p.K ? k : p.K - 8;
+    const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+    const int i = tap / p.kw, j = tap - i * p.kw;
+    const int ny = r.iy0 - i, nx = r.ix0 - j;
+    const int oy = max(ny, 0) >> p.sshift, ox = max(nx, 0) >> p.sshift;
+    const bool ok = r.valid && k < p.K && ny >= 0 && nx >= 0 && !(ny & smask) && !(nx & smask) && oy < p.H && ox < p.Wd;
+    const int oyc = min(oy, p.H - 1), oxc = min(ox, p.Wd - 1);
+    load_vec8(X + r.base + ((long)oyc * p.Wd + oxc) * p.Cin + ci, c);
+    return ok ? 0xFFu : 0u;
+  }
+  unsigned m = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int kk = k + e;
+    const int kc = kk < p.K ? kk : p.K - 1;
+    const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+    const int i = tap / p.kw, j = tap - i * p.kw;
+    const int ny = r.iy0 - i, nx = r.ix0 - j;
+    const int oy = max(ny, 0) >> p.sshift, ox = max(nx, 0) >> p.sshift;
+    const bool ok = r.valid && kk < p.K && ny >= 0 && nx >= 0 && !(ny & smask) && !(nx & smask) && oy < p.H && ox < p.Wd;
+    const int oyc = min(oy, p.H - 1), oxc = min(ox, p.Wd - 1);
+    c.v[e] = X[r.base + ((long)oyc * p.Wd + oxc) * p.Cin + ci];
+    m |= ok ? (1u << e) : 0u;
+  }
+  return m;
+}
+
 template <typename T>
 __device__ __forceinline__ void mfma_step(const Chunk<T>& a, const Chunk<T>& b, f32x4& acc) {
   if constexpr (sizeof(T) == 2) {
@@ -206,7 +245,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
 
   const int lrow = tid / CPR, lk = (tid % CPR) * 8;
   ConvRow crow[ACH];
-  if constexpr (ASRC == 1) {
+  if constexpr (ASRC != 0) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       int m = m0 + lrow + RPP * i;
@@ -216,8 +255,13 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
       int b = mm / hw, rem = mm - b * hw;
       int oy = rem / p.OW, ox = rem - oy * p.OW;
       crow[i].base = (long)b * p.H * p.Wd * p.Cin;
-      crow[i].iy0 = oy * p.stride - p.pad;
-      crow[i].ix0 = ox * p.stride - p.pad;
+      if constexpr (ASRC == 1) {
+        crow[i].iy0 = oy * p.stride - p.pad;
+        crow[i].ix0 = ox * p.stride - p.pad;
+      } else {
+        crow[i].iy0 = oy + p.pad;
+        crow[i].ix0 = ox + p.pad;
+      }
     }
   }
 
@@ -227,6 +271,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       if constexpr (ASRC == 1) ma[i] = load_im2col<T, VEC>(A, p, crow[i], k0 + lk, ra[i]);
+      else if constexpr (ASRC == 2) ma[i] = load_col2im<T, VEC>(A, p, crow[i], k0 + lk, ra[i]);
       else ma[i] = load_dense<T, VEC>(A, p.lda, m0 + lrow + RPP * i, p.M, k0 + lk, p.K, ra[i]);
     }
 #pragma unroll
@@ -301,6 +346,11 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
     float v[8];
     *reinterpret_cast<float4*>(&v[0]) = *reinterpret_cast<const float4*>(&sC[row][c8]);
     *reinterpret_cast<float4*>(&v[4]) = *reinterpret_cast<const float4*>(&sC[row][c8 + 4]);
+    if (p.rscale) {
+      const float sc = p.rscale[m / p.rdiv];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= sc;
+    }
     if (p.vec_out && n + 8 <= p.N) {
       if (R) {
         Chunk<T> rr;
@@ -349,24 +399,159 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
   return check_launch("gemm");
 }
 
+
+// ---- weight gradient: dW[n][k] += sum_m dY[m][n] * X[m][k] ------------------------------------
+// Both operands arrive m-major (token rows), but the MFMA wants the reduction index m contiguous
+// per lane, so each 32-row slab of dY and X is staged TRANSPOSED in LDS ([n][m] / [k][m]); the
+// fragment reads are then the same 16-byte reads as the forward GEMM.  Loader mapping: thread ->
+// (m = tid & 31, 8-column chunk = tid >> 5), which makes the transposed 2/4-byte LDS writes
+// conflict-free (32 consecutive m per column).  Tile 64 (n) x 64 (k); the M range is split over
+// gridDim.y workgroups whose partial tiles are f32-atomically added into dW.
+// BSRC = 1: X is an NHWC map read through the conv im2col gather (conv weight gradient, dW packed
+// [Cout][kh][kw][Cin] like the forward weights).
+struct WgradArgs {
+  const void* dY; long ldy;
+  const void* X; long ldx;
+  float* dW; long lddw;
+  int M, N, K, mchunk;
+  int H, Wd, Cin, OH, OW, kw, stride, pad;
+};
+
+template <typename T, bool VECA, bool VECB, int BSRC>
+__global__ __launch_bounds__(NTHREADS) void wgrad_kernel(WgradArgs p) {
+  constexpr int LDT = 32 + 16 / (int)sizeof(T);   // 40 bf16 (80 B rows) / 36 f32 (144 B rows)
+  __shared__ __attribute__((aligned(16))) T sA[2][64][LDT];
+  __shared__ __attribute__((aligned(16))) T sB[2][64][LDT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int ntk = (p.K + 63) / 64;
+  const int n0 = (blockIdx.x / ntk) * 64, k0 = (blockIdx.x % ntk) * 64;
+  const int mbeg = blockIdx.y * p.mchunk;
+  const int mend = min(mbeg + p.mchunk, p.M);
+  const T* dY = static_cast<const T*>(p.dY);
+  const T* X = static_cast<const T*>(p.X);
+  const int lm = tid & 31, lc = (tid >> 5) * 8;
+
+  Chunk<T> ra, rb;
+  unsigned ma, mb;
+  GemmArgs ga{};   // geometry for the im2col loader
+  if constexpr (BSRC == 1) {
+    ga.K = p.K; ga.H = p.H; ga.Wd = p.Wd; ga.Cin = p.Cin; ga.OH = p.OH; ga.OW = p.OW; ga.kw = p.kw;
+    ga.stride = p.stride; ga.pad = p.pad;
+  }
+  auto fetch = [&](int m0) {
+    const int m = m0 + lm;
+    const bool mv = m < mend;
+    ma = load_dense<T, VECA>(dY, p.ldy, mv ? m : p.M, p.M, n0 + lc, p.N, ra);   // rows >= M are masked
+    if constexpr (BSRC == 1) {
+      ConvRow r;
+      r.valid = mv;
+      const int mm = mv ? m : 0;
+      const int hw = p.OH * p.OW;
+      const int b = mm / hw, rem = mm - b * hw;
+      const int oy = rem / p.OW, ox = rem - oy * p.OW;
+      r.base = (long)b * p.H * p.Wd * p.Cin;
+      r.iy0 = oy * p.stride - p.pad;
+      r.ix0 = ox * p.stride - p.pad;
+      mb = load_im2col<T, VECB>(X, ga, r, k0 + lc, rb);
+    } else {
+      mb = load_dense<T, VECB>(X, p.ldx, mv ? m : p.M, p.M, k0 + lc, p.K, rb);
+    }
+  };
+  auto stash = [&](int buf) {
+    apply_mask8<T, VECA>(ra, ma);
+    apply_mask8<T, VECB>(rb, mb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      sA[buf][lc + e][lm] = ra.v[e];
+      sB[buf][lc + e][lm] = rb.v[e];
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fk = (lane >> 4) * 8;
+  fetch(mbeg);
+  stash(0);
+  __syncthreads();
+  int buf = 0;
+  for (int m0 = mbeg; m0 < mend; m0 += 32) {
+    fetch(m0 + 32);
+    __builtin_amdgcn_sched_barrier(0);
+    Chunk<T> fa[2], fb[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) fa[i] = *reinterpret_cast<const Chunk<T>*>(&sA[buf][wn * 32 + i * 16 + fr][fk]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[j] = *reinterpret_cast<const Chunk<T>*>(&sB[buf][wk * 32 + j * 16 + fr][fk]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) mfma_step<T>(fa[i], fb[j], acc[i][j]);
+    stash(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  // C map: col (k) = lane & 15, row (n) = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int k = k0 + wk * 32 + j * 16 + fr;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 32 + i * 16 + (lane >> 4) * 4 + r;
+        if (n < p.N && k < p.K) atomicAdd(p.dW + (long)n * p.lddw + k, acc[i][j][r]);
+      }
+    }
+}
+
+template <typename T, int BSRC>
+static int launch_wgrad(WgradArgs a, bool veca, bool vecb, hipStream_t st) {
+  const long tiles = (long)((a.N + 63) / 64) * ((a.K + 63) / 64);
+  // split M so that the grid holds ~2048 workgroups, each with >= 256 rows
+  long splits = std::max<long>(1, std::min<long>((2048 + tiles - 1) / tiles, (a.M + 255) / 256));
+  long chunk = (a.M + splits - 1) / splits;
+  chunk = (chunk + 31) / 32 * 32;
+  splits = (a.M + chunk - 1) / chunk;
+  a.mchunk = (int)chunk;
+  dim3 grid((unsigned)tiles, (unsigned)splits);
+  if (veca && vecb) hipLaunchKernelGGL((wgrad_kernel<T, true, true, BSRC>), grid, dim3(NTHREADS), 0, st, a);
+  else if (veca) hipLaunchKernelGGL((wgrad_kernel<T, true, false, BSRC>), grid, dim3(NTHREADS), 0, st, a);
+  else if (vecb) hipLaunchKernelGGL((wgrad_kernel<T, false, true, BSRC>), grid, dim3(NTHREADS), 0, st, a);
+  else hipLaunchKernelGGL((wgrad_kernel<T, false, false, BSRC>), grid, dim3(NTHREADS), 0, st, a);
+  return check_launch("wgrad");
+}
+
 }  // namespace svk
 
 using namespace svk;
 
-extern "C" int svk_gemm(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
-                        const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act, void* stream) {
-  if (M < 0 || N <= 0 || K <= 0 || !A || !W || !C) { set_error("svk_gemm: bad args M=%d N=%d K=%d", M, N, K); return SVK_EINVAL; }
+extern "C" int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
+                           const float* row_scale, int rows_per_scale, const void* R, long ldr, void* C, long ldc,
+                           int M, int N, int K, int act, void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !A || !W || !C || (row_scale && rows_per_scale <= 0)) {
+    set_error("svk_gemm: bad args M=%d N=%d K=%d", M, N, K); return SVK_EINVAL;
+  }
   if (M == 0) return SVK_OK;
   if (lda < K || ldw < K || ldc < N || (R && ldr < N)) { set_error("svk_gemm: leading dims too small"); return SVK_EINVAL; }
   GemmArgs a{};
   a.A = A; a.lda = lda; a.W = W; a.ldw = ldw; a.bias = bias; a.R = R; a.ldr = ldr; a.C = C; a.ldc = ldc;
-  a.M = M; a.N = N; a.K = K; a.act = act;
+  a.M = M; a.N = N; a.K = K; a.act = act; a.rscale = row_scale; a.rdiv = rows_per_scale;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
     const long vecw = 16 / (long)sizeof(T);
     bool vec = aligned16(A) && aligned16(W) && (lda % vecw == 0) && (ldw % vecw == 0) && (K % 8 == 0);
     return launch_gemm<T, 0>(a, vec, st);
   });
+}
+
+extern "C" int svk_gemm(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
+                        const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act, void* stream) {
+  return svk_gemm_ex(dtype, A, lda, W, ldw, bias, nullptr, 1, R, ldr, C, ldc, M, N, K, act, stream);
 }
 
 extern "C" int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* Wt,
@@ -388,5 +573,69 @@ extern "C" int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, in
   SVK_DISPATCH_DTYPE(dtype, T, {
     bool vec = aligned16(X) && aligned16(Wt) && (Cin % 8 == 0);
     return launch_gemm<T, 1>(a, vec, st);
+  });
+}
+
+extern "C" int svk_conv2d_dgrad_nhwc(int dtype, const void* dY, int B, int OH, int OW, int Cout, const void* Wd,
+                                     const void* R, void* dX, int H, int W, int Cin, int k, int stride, int pad,
+                                     void* stream) {
+  if (B < 0 || OH <= 0 || OW <= 0 || Cout <= 0 || H <= 0 || W <= 0 || Cin <= 0 || k <= 0 || pad < 0 || !dY || !Wd ||
+      !dX || stride <= 0 || (stride & (stride - 1))) {
+    set_error("svk_conv2d_dgrad_nhwc: bad args (stride must be a power of two)"); return SVK_EINVAL;
+  }
+  if ((H + 2 * pad - k) / stride + 1 != OH || (W + 2 * pad - k) / stride + 1 != OW) {
+    set_error("svk_conv2d_dgrad_nhwc: geometry mismatch"); return SVK_EINVAL;
+  }
+  if (B == 0) return SVK_OK;
+  const long M = (long)B * H * W;
+  if (M > 0x7fffffffL) { set_error("svk_conv2d_dgrad_nhwc: too many pixels"); return SVK_EUNSUPPORTED; }
+  GemmArgs a{};
+  a.A = dY; a.lda = 0; a.W = Wd; a.ldw = (long)k * k * Cout; a.R = R; a.ldr = Cin; a.C = dX; a.ldc = Cin;
+  a.M = (int)M; a.N = Cin; a.K = k * k * Cout; a.act = 0; a.rdiv = 1;
+  a.H = OH; a.Wd = OW; a.Cin = Cout; a.OH = H; a.OW = W; a.kw = k; a.stride = stride; a.pad = pad;
+  a.sshift = __builtin_ctz(stride);
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    bool vec = aligned16(dY) && aligned16(Wd) && (Cout % 8 == 0);
+    return launch_gemm<T, 2>(a, vec, st);
+  });
+}
+
+extern "C" int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw,
+                              int M, int N, int K, void* stream) {
+  if (M < 0 || N <= 0 || K <= 0 || !dY || !X || !dW || ldy < N || ldx < K || lddw < K) {
+    set_error("svk_gemm_wgrad: bad args"); return SVK_EINVAL;
+  }
+  if (M == 0) return SVK_OK;
+  WgradArgs a{};
+  a.dY = dY; a.ldy = ldy; a.X = X; a.ldx = ldx; a.dW = dW; a.lddw = lddw; a.M = M; a.N = N; a.K = K;
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    const long vw = 16 / (long)sizeof(T);
+    const bool va = aligned16(dY) && ldy % vw == 0 && N % 8 == 0;
+    const bool vb = aligned16(X) && ldx % vw == 0 && K % 8 == 0;
+    return launch_wgrad<T, 0>(a, va, vb, st);
+  });
+}
+
+extern "C" int svk_conv2d_wgrad_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* dY,
+                                     int Cout, int k, int stride, int pad, float* dW, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || k <= 0 || stride <= 0 || pad < 0 || !X || !dY || !dW) {
+    set_error("svk_conv2d_wgrad_nhwc: bad args"); return SVK_EINVAL;
+  }
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  if (OH <= 0 || OW <= 0) { set_error("svk_conv2d_wgrad_nhwc: empty output"); return SVK_EINVAL; }
+  if (B == 0) return SVK_OK;
+  const long M = (long)B * OH * OW;
+  if (M > 0x7fffffffL) { set_error("svk_conv2d_wgrad_nhwc: too many pixels"); return SVK_EUNSUPPORTED; }
+  WgradArgs a{};
+  a.dY = dY; a.ldy = Cout; a.X = X; a.ldx = 0; a.dW = dW; a.lddw = (long)k * k * Cin;
+  a.M = (int)M; a.N = Cout; a.K = k * k * Cin;
+  a.H = H; a.Wd = W; a.Cin = Cin; a.OH = OH; a.OW = OW; a.kw = k; a.stride = stride; a.pad = pad;
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    const bool va = aligned16(dY) && Cout % 8 == 0;
+    const bool vb = aligned16(X) && Cin % 8 == 0;
+    return launch_wgrad<T, 1>(a, va, vb, st);
   });
 }

@@ -9,7 +9,7 @@ namespace svk {
 template <typename T>
 __global__ __launch_bounds__(256) void dwconv3x3_vec8(const T* __restrict__ X, const float* __restrict__ w,
                                                       const float* __restrict__ bias, T* __restrict__ Y,
-                                                      int B, int H, int W, int C, int act) {
+                                                      T* __restrict__ Ypre, int B, int H, int W, int C, int act) {
   const int CG = C >> 3;
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)B * H * W * CG;
@@ -46,6 +46,17 @@ __global__ __launch_bounds__(256) void dwconv3x3_vec8(const T* __restrict__ X, c
     }
   }
   T o[8];
+  if (Ypre) {   // pre-activation copy (training: the GELU backward needs it)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = from_f<T>(acc[j]);
+    T* dp = Ypre + pix * C + c0;
+    if constexpr (sizeof(T) == 2) {
+      *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(o);
+    } else {
+      reinterpret_cast<uint4*>(dp)[0] = reinterpret_cast<const uint4*>(o)[0];
+      reinterpret_cast<uint4*>(dp)[1] = reinterpret_cast<const uint4*>(o)[1];
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) o[j] = from_f<T>(apply_act(acc[j], act));
   T* dst = Y + pix * C + c0;
@@ -59,7 +70,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_vec8(const T* __restrict__ X, c
 
 template <typename T>
 __global__ void dwconv3x3_scalar(const T* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias,
-                                 T* __restrict__ Y, int B, int H, int W, int C, int act) {
+                                 T* __restrict__ Y, T* __restrict__ Ypre, int B, int H, int W, int C, int act) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)B * H * W * C;
   if (idx >= total) return;
@@ -76,6 +87,7 @@ __global__ void dwconv3x3_scalar(const T* __restrict__ X, const float* __restric
       if (yy < 0 || yy >= H || xx < 0 || xx >= W) continue;
       acc += to_f(X[(((long)b * H + yy) * W + xx) * C + c]) * w[((dy + 1) * 3 + (dx + 1)) * C + c];
     }
+  if (Ypre) Ypre[idx] = from_f<T>(acc);
   Y[idx] = from_f<T>(apply_act(acc, act));
 }
 
@@ -199,22 +211,29 @@ inline dim3 grid1d(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) /
 
 using namespace svk;
 
-extern "C" int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B, int H,
-                             int W, int C, int act, void* stream) {
+extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const float* bias, void* Y, void* Ypre,
+                                int B, int H, int W, int C, int act, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || C <= 0 || !X || !w || !bias || !Y) { set_error("svk_dwconv3x3: bad args"); return SVK_EINVAL; }
   if (B == 0) return SVK_OK;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
-    const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y) & 15) == 0;
+    const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 15) == 0;
     if (vec) {
       const long n = (long)B * H * W * (C / 8);
-      hipLaunchKernelGGL((dwconv3x3_vec8<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, B, H, W, C, act);
+      hipLaunchKernelGGL((dwconv3x3_vec8<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B, H,
+                         W, C, act);
     } else {
       const long n = (long)B * H * W * C;
-      hipLaunchKernelGGL((dwconv3x3_scalar<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, B, H, W, C, act);
+      hipLaunchKernelGGL((dwconv3x3_scalar<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B,
+                         H, W, C, act);
     }
     return check_launch("dwconv3x3");
   });
+}
+
+extern "C" int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B, int H,
+                             int W, int C, int act, void* stream) {
+  return svk_dwconv3x3_ex(dtype, X, w, bias, Y, nullptr, B, H, W, C, act, stream);
 }
 
 extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,

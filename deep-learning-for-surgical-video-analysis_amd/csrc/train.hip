@@ -1,0 +1,537 @@
+// Training-step kernels (train_evp.py:473-515): normalisation / activation backward, batch-norm in
+// train mode, bilinear-resize adjoint, phase losses, stochastic-depth / Dropout2d masks, SGD.
+// Activations and their gradients are T (bf16 or f32); statistics, parameter grads and optimizer
+// state are f32.
+#include "svk_common.h"
+
+namespace svk {
+
+// ---- LayerNorm backward ---------------------------------------------------------------------
+// dX = rstd * (g*dY - mean(g*dY) - xhat * mean(g*dY*xhat)) (+ dR);  dgamma += sum dY*xhat,
+// dbeta += sum dY (f32 atomics, one partial per lane per block).  One wave per row, lanes over C.
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ X, long ldx, const T* __restrict__ dY,
+                                                            long ldy, const float* __restrict__ g, const T* __restrict__ dR,
+                                                            long ldr, T* __restrict__ dX, long lddx,
+                                                            float* __restrict__ dg, float* __restrict__ db, int M, int C,
+                                                            float eps) {
+  constexpr int PER = 8;     // C <= 512
+  const int lane = threadIdx.x & 63;
+  float pg[PER], pb[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) { pg[i] = 0.f; pb[i] = 0.f; }
+  for (long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); row < M; row += (long)gridDim.x * 4) {
+    const T* x = X + row * ldx;
+    const T* dy = dY + row * ldy;
+    float xv[PER], gy[PER], dyv[PER];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      xv[i] = c < C ? to_f(x[c]) : 0.f;
+      dyv[i] = c < C ? to_f(dy[c]) : 0.f;
+      gy[i] = c < C ? dyv[i] * g[c] : 0.f;
+      s += xv[i];
+    }
+    const float mean = wave_sum(s) / C;
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) { const int c = lane + 64 * i; const float d = c < C ? xv[i] - mean : 0.f; q += d * d; }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / C + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const float xh = (xv[i] - mean) * rstd;
+      xv[i] = xh;
+      s1 += gy[i];
+      s2 += gy[i] * xh;
+    }
+    s1 = wave_sum(s1) / C;
+    s2 = wave_sum(s2) / C;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c >= C) continue;
+      float v = rstd * (gy[i] - s1 - xv[i] * s2);
+      if (dR) v += to_f(dR[row * ldr + c]);
+      dX[row * lddx + c] = from_f<T>(v);
+      pg[i] += dyv[i] * xv[i];
+      pb[i] += dyv[i];
+    }
+  }
+  if (dg) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = lane + 64 * i;
+      if (c < C) { atomicAdd(dg + c, pg[i]); atomicAdd(db + c, pb[i]); }
+    }
+  }
+}
+
+// ---- activation backward: dX = dY * act'(U) (+ dR) --------------------------------------------
+template <typename T>
+__global__ void act_bwd_kernel(const T* __restrict__ U, const T* __restrict__ dY, const T* __restrict__ dR,
+                               T* __restrict__ dX, long n, int act) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float u = to_f(U[i]);
+  float d;
+  if (act == SVK_ACT_GELU) {
+    const float cdf = 0.5f * (1.0f + erff(u * 0.70710678118654752f));
+    const float pdf = 0.3989422804014327f * expf(-0.5f * u * u);
+    d = cdf + u * pdf;
+  } else if (act == SVK_ACT_RELU) {
+    d = u > 0.f ? 1.f : 0.f;
+  } else if (act == SVK_ACT_TANH) {
+    const float t = tanhf(u);
+    d = 1.f - t * t;
+  } else {
+    d = 1.f;
+  }
+  float v = to_f(dY[i]) * d;
+  if (dR) v += to_f(dR[i]);
+  dX[i] = from_f<T>(v);
+}
+
+// ---- column statistics: sum and sum of squares over M rows (BN batch statistics) --------------
+template <typename T>
+__global__ __launch_bounds__(256) void colstats_kernel(const T* __restrict__ X, long ldx, int M, int C,
+                                                       float* __restrict__ sum, float* __restrict__ sq) {
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  float s = 0.f, q = 0.f;
+  if (c < C)
+    for (long r = (long)blockIdx.x * 4 + rl; r < M; r += (long)gridDim.x * 4) {
+      const float v = to_f(X[r * ldx + c]);
+      s += v;
+      q += v * v;
+    }
+  __shared__ float ss[4][64], sqq[4][64];
+  ss[rl][threadIdx.x & 63] = s;
+  sqq[rl][threadIdx.x & 63] = q;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const int t = threadIdx.x & 63;
+    atomicAdd(sum + c, ss[0][t] + ss[1][t] + ss[2][t] + ss[3][t]);
+    if (sq) atomicAdd(sq + c, sqq[0][t] + sqq[1][t] + sqq[2][t] + sqq[3][t]);
+  }
+}
+
+// ---- BN train-mode apply: Y = act((X - mean) * rstd * g + b), mean/var from the sums -------------
+template <typename T>
+__global__ void bn_apply_kernel(const T* __restrict__ X, const float* __restrict__ sum, const float* __restrict__ sq,
+                                const float* __restrict__ g, const float* __restrict__ b, T* __restrict__ Y, long n,
+                                int C, int M, float eps, int act) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const float mean = sum[c] / M;
+  const float var = fmaxf(sq[c] / M - mean * mean, 0.f);
+  const float v = (to_f(X[i]) - mean) * rsqrtf(var + eps) * g[c] + b[c];
+  Y[i] = from_f<T>(apply_act(v, act));
+}
+
+// BN train-mode backward (with an optional ReLU after the BN, recomputed from X):
+// dxhat = dy' * g, dx = rstd/M * (M*dxhat - sum(dxhat) - xhat*sum(dxhat*xhat)).
+// sdy = sum dy', sdyx = sum dy'*xhat must be precomputed (bn_bwd_reduce_kernel).
+template <typename T>
+__global__ void bn_bwd_reduce_kernel(const T* __restrict__ X, const T* __restrict__ dY, const float* __restrict__ sum,
+                                     const float* __restrict__ sq, const float* __restrict__ g,
+                                     const float* __restrict__ b, int M, int C, float eps, int relu,
+                                     float* __restrict__ sdy, float* __restrict__ sdyx) {
+  const int c = blockIdx.y * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  float a1 = 0.f, a2 = 0.f;
+  if (c < C) {
+    const float mean = sum[c] / M;
+    const float rstd = rsqrtf(fmaxf(sq[c] / M - mean * mean, 0.f) + eps);
+    for (long r = (long)blockIdx.x * 4 + rl; r < M; r += (long)gridDim.x * 4) {
+      const float xh = (to_f(X[r * C + c]) - mean) * rstd;
+      float d = to_f(dY[r * C + c]);
+      if (relu && xh * g[c] + b[c] <= 0.f) d = 0.f;
+      a1 += d;
+      a2 += d * xh;
+    }
+  }
+  __shared__ float s1[4][64], s2[4][64];
+  s1[rl][threadIdx.x & 63] = a1;
+  s2[rl][threadIdx.x & 63] = a2;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const int t = threadIdx.x & 63;
+    atomicAdd(sdy + c, s1[0][t] + s1[1][t] + s1[2][t] + s1[3][t]);
+    atomicAdd(sdyx + c, s2[0][t] + s2[1][t] + s2[2][t] + s2[3][t]);
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ X, const T* __restrict__ dY, const float* __restrict__ sum,
+                                    const float* __restrict__ sq, const float* __restrict__ g,
+                                    const float* __restrict__ b, const float* __restrict__ sdy,
+                                    const float* __restrict__ sdyx, T* __restrict__ dX, long n, int C, int M,
+                                    float eps, int relu) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  const float mean = sum[c] / M;
+  const float rstd = rsqrtf(fmaxf(sq[c] / M - mean * mean, 0.f) + eps);
+  const float xh = (to_f(X[i]) - mean) * rstd;
+  float d = to_f(dY[i]);
+  if (relu && xh * g[c] + b[c] <= 0.f) d = 0.f;
+  const float v = g[c] * rstd / M * (M * d - sdy[c] - xh * sdyx[c]);
+  dX[i] = from_f<T>(v);
+}
+
+// ---- bilinear resize adjoint (align_corners=False): dX[b, src, c] += w * dY[b, dst, c] (f32 atomics)
+__device__ __forceinline__ void src_index_b(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  const float scale = (float)in / (float)out;
+  float s = scale * (dst + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = s - i0;
+  l0 = 1.f - l1;
+}
+
+template <typename T>
+__global__ void resize_bwd_kernel(const T* __restrict__ dY, long ldy, float* __restrict__ dX, int B, int H, int W,
+                                  int C, int OH, int OW) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * OH * OW * C) return;
+  const int c = (int)(idx % C);
+  const long pix = idx / C;
+  const int ox = (int)(pix % OW);
+  const long t = pix / OW;
+  const int oy = (int)(t % OH);
+  const int b = (int)(t / OH);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  src_index_b(oy, H, OH, y0, y1, ly0, ly1);
+  src_index_b(ox, W, OW, x0, x1, lx0, lx1);
+  const float g = to_f(dY[((long)b * OH * OW + (long)oy * OW + ox) * ldy + c]);
+  float* base = dX + (long)b * H * W * C + c;
+  atomicAdd(base + ((long)y0 * W + x0) * C, g * ly0 * lx0);
+  atomicAdd(base + ((long)y0 * W + x1) * C, g * ly0 * lx1);
+  atomicAdd(base + ((long)y1 * W + x0) * C, g * ly1 * lx0);
+  atomicAdd(base + ((long)y1 * W + x1) * C, g * ly1 * lx1);
+}
+
+// ---- broadcast row-mean adjoint: dY[b*R + r, c] = dF[b, c] * scale ---------------------------
+template <typename T>
+__global__ void bcast_rows_kernel(const float* __restrict__ dF, const float* __restrict__ mask, float scale,
+                                  T* __restrict__ dY, int B, int R, int C) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * R * C) return;
+  const int c = (int)(i % C);
+  const long b = i / ((long)R * C);
+  float v = dF[b * C + c] * scale;
+  if (mask) v *= mask[b * C + c];
+  dY[i] = from_f<T>(v);
+}
+
+__global__ void mul_f32_kernel(const float* __restrict__ a, const float* __restrict__ b, float* __restrict__ y, long n) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = a[i] * b[i];
+}
+
+// running_mean = (1 - mom) * running_mean + mom * mean; running_var likewise with the unbiased variance
+// (torch.nn.BatchNorm2d train-mode buffer update).
+__global__ void bn_running_kernel(const float* __restrict__ sum, const float* __restrict__ sq, int M, int C,
+                                  float mom, float* __restrict__ rm, float* __restrict__ rv) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mean = sum[c] / M;
+  const float var = fmaxf(sq[c] / M - mean * mean, 0.f);
+  rm[c] = (1.f - mom) * rm[c] + mom * mean;
+  rv[c] = (1.f - mom) * rv[c] + mom * var * ((float)M / (float)max(M - 1, 1));
+}
+
+// Batched parameter packing: every descriptor is a 4-D strided gather from the f32 master copy into
+// a packed (compute-dtype) layout; source indices at or past `lim` read as zero (channel padding).
+// One launch refreshes every packed view of the trainable weights after an optimizer step.
+struct PackDesc {
+  long src, dst;     // element offsets
+  int n[4];          // packed shape
+  long s[4];         // source stride of each packed dim
+  int lim[4];        // source extent of each packed dim
+  long start;        // first packed element of this descriptor in the launch's linear index space
+};
+
+template <typename T>
+__global__ void pack_params_kernel(const PackDesc* __restrict__ d, int nd, long total, const float* __restrict__ src,
+                                   T* __restrict__ dst) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int lo = 0, hi = nd - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].start <= i) lo = mid; else hi = mid - 1;
+  }
+  const PackDesc& e = d[lo];
+  long r = i - e.start;
+  if (r >= (long)e.n[0] * e.n[1] * e.n[2] * e.n[3]) return;   // alignment gap between descriptors
+  long off = e.src;
+  bool ok = true;
+#pragma unroll
+  for (int k = 3; k >= 0; --k) {
+    const int idx = (int)(r % e.n[k]);
+    r /= e.n[k];
+    ok = ok && idx < e.lim[k];
+    off += (long)idx * e.s[k];
+  }
+  dst[e.dst + (i - e.start)] = from_f<T>(ok ? src[off] : 0.f);
+}
+
+// ---- per-row scale (stochastic depth / Dropout2d masks): Y[r, c] = X[r, c] * s[r / rows_per] ---
+template <typename T>
+__global__ void row_scale_kernel(const T* __restrict__ X, const float* __restrict__ s, T* __restrict__ Y, long n,
+                                 int C, int rows_per) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Y[i] = from_f<T>(to_f(X[i]) * s[(i / C) / rows_per]);
+}
+
+// Counter-based Bernoulli keep-mask scaled by 1/keep (mask values 0 or 1/keep), seeded per call.
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+__global__ void keep_mask_kernel(float* __restrict__ out, long n, float keep, uint32_t seed) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float u = (hash32((uint32_t)i * 0x9E3779B9U ^ hash32(seed)) >> 8) * (1.0f / 16777216.0f);
+  out[i] = u < keep ? 1.0f / keep : 0.f;
+}
+
+// ---- phase losses: CrossEntropy(sum) + SmoothL1(sum) and their gradients (train_evp.py:390-391, 500-509)
+__global__ void phase_loss_kernel(const float* __restrict__ logits, const float* __restrict__ ant,
+                                  const long* __restrict__ labels, const float* __restrict__ ant_t, int B, int K,
+                                  float* __restrict__ loss, float* __restrict__ dlogits, float* __restrict__ dant) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const float* z = logits + (long)b * K;
+  float m = -INFINITY;
+  for (int k = 0; k < K; ++k) m = fmaxf(m, z[k]);
+  float s = 0.f;
+  for (int k = 0; k < K; ++k) s += expf(z[k] - m);
+  const long y = labels[b];
+  atomicAdd(loss, logf(s) + m - z[y]);
+  for (int k = 0; k < K; ++k) dlogits[(long)b * K + k] = expf(z[k] - m) / s - (k == y ? 1.f : 0.f);
+  float l1 = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float d = ant[(long)b * K + k] - ant_t[(long)b * K + k];
+    const float ad = fabsf(d);
+    l1 += ad < 1.f ? 0.5f * d * d : ad - 0.5f;
+    dant[(long)b * K + k] = ad < 1.f ? d : (d > 0.f ? 1.f : -1.f);
+  }
+  atomicAdd(loss + 1, l1);
+}
+
+// ---- SGD with momentum / dampening / weight decay / nesterov (torch.optim.SGD semantics) -------
+__global__ void sgd_kernel(float* __restrict__ p, const float* __restrict__ gr, float* __restrict__ buf, long n,
+                           float lr, float momentum, float dampening, float wd, int nesterov, int first) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float d = gr[i] + wd * p[i];
+  if (momentum != 0.f) {
+    const float bv = first ? d : momentum * buf[i] + (1.f - dampening) * d;
+    buf[i] = bv;
+    d = nesterov ? d + momentum * bv : bv;
+  }
+  p[i] -= lr * d;
+}
+
+// ---- unpatchify: [B*PH*PW, s*s*C] patch rows -> NHWC [B, PH*s, PW*s, C] (+ optional accumulate) ---
+template <typename T>
+__global__ void unpatchify_kernel(const T* __restrict__ P, T* __restrict__ Y, int B, int PH, int PW, int s, int C,
+                                  int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long n = (long)B * PH * PW * s * s * C;
+  if (i >= n) return;
+  const int c = (int)(i % C);
+  long t = i / C;
+  const int j = (int)(t % s); t /= s;
+  const int ii = (int)(t % s); t /= s;
+  const int px = (int)(t % PW); t /= PW;
+  const int py = (int)(t % PH);
+  const long b = t / PH;
+  const long dst = ((b * PH * s + (long)py * s + ii) * ((long)PW * s) + (long)px * s + j) * C + c;
+  const float v = to_f(P[i]);
+  Y[dst] = from_f<T>(accumulate ? to_f(Y[dst]) + v : v);
+}
+
+inline dim3 g1(long n) { return dim3((unsigned)((n + 255) / 256)); }
+
+}  // namespace svk
+
+using namespace svk;
+
+extern "C" int svk_layernorm_bwd(int dtype, const void* X, long ldx, const void* dY, long ldy, const float* gamma,
+                                 const void* dR, long ldr, void* dX, long lddx, float* dgamma, float* dbeta, int M,
+                                 int C, float eps, void* stream) {
+  if (M < 0 || C <= 0 || C > 512 || !X || !dY || !gamma || !dX || ((dgamma == nullptr) != (dbeta == nullptr))) {
+    set_error("svk_layernorm_bwd: bad args (C <= 512)"); return SVK_EINVAL;
+  }
+  if (M == 0) return SVK_OK;
+  const int blocks = (int)std::min<long>((M + 3) / 4, 2048);
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((layernorm_bwd_kernel<T>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const T*)X, ldx,
+                       (const T*)dY, ldy, gamma, (const T*)dR, ldr, (T*)dX, lddx, dgamma, dbeta, M, C, eps);
+    return check_launch("layernorm_bwd");
+  });
+}
+
+extern "C" int svk_act_bwd(int dtype, const void* U, const void* dY, const void* dR, void* dX, long n, int act,
+                           void* stream) {
+  if (n < 0 || !U || !dY || !dX) { set_error("svk_act_bwd: bad args"); return SVK_EINVAL; }
+  if (n == 0) return SVK_OK;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((act_bwd_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, (const T*)U, (const T*)dY,
+                       (const T*)dR, (T*)dX, n, act);
+    return check_launch("act_bwd");
+  });
+}
+
+extern "C" int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, void* stream) {
+  if (M < 0 || C <= 0 || !X || !sum) { set_error("svk_colstats: bad args"); return SVK_EINVAL; }
+  if (M == 0) return SVK_OK;
+  const int bx = (int)std::min<long>((M + 63) / 64, 1024);
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((colstats_kernel<T>), dim3(bx, (C + 63) / 64), dim3(256), 0, (hipStream_t)stream, (const T*)X,
+                       ldx, M, C, sum, sumsq);
+    return check_launch("colstats");
+  });
+}
+
+extern "C" int svk_bn_apply(int dtype, const void* X, const float* sum, const float* sumsq, const float* gamma,
+                            const float* beta, void* Y, int M, int C, float eps, int act, void* stream) {
+  if (M < 0 || C <= 0 || !X || !sum || !sumsq || !gamma || !beta || !Y) { set_error("svk_bn_apply: bad args"); return SVK_EINVAL; }
+  if (M == 0) return SVK_OK;
+  const long n = (long)M * C;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((bn_apply_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, (const T*)X, sum, sumsq, gamma,
+                       beta, (T*)Y, n, C, M, eps, act);
+    return check_launch("bn_apply");
+  });
+}
+
+extern "C" int svk_bn_bwd(int dtype, const void* X, const void* dY, const float* sum, const float* sumsq,
+                          const float* gamma, const float* beta, void* dX, float* dgamma, float* dbeta, int M, int C,
+                          float eps, int relu, void* stream) {
+  if (M <= 0 || C <= 0 || !X || !dY || !sum || !sumsq || !gamma || !beta || !dX || !dgamma || !dbeta) {
+    set_error("svk_bn_bwd: bad args"); return SVK_EINVAL;
+  }
+  const long n = (long)M * C;
+  const int bx = (int)std::min<long>((M + 63) / 64, 1024);
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    // dgamma/dbeta accumulate sum(dy'*xhat) / sum(dy') directly (they are exactly those sums)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3(bx, (C + 63) / 64), dim3(256), 0, st, (const T*)X, (const T*)dY,
+                       sum, sumsq, gamma, beta, M, C, eps, relu, dbeta, dgamma);
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), g1(n), dim3(256), 0, st, (const T*)X, (const T*)dY, sum, sumsq, gamma,
+                       beta, dbeta, dgamma, (T*)dX, n, C, M, eps, relu);
+    return check_launch("bn_bwd");
+  });
+}
+
+extern "C" int svk_resize_bilinear_bwd(int dtype, const void* dY, long ldy, float* dX, int B, int H, int W, int C,
+                                       int OH, int OW, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || C <= 0 || OH <= 0 || OW <= 0 || !dY || !dX) { set_error("svk_resize_bilinear_bwd: bad args"); return SVK_EINVAL; }
+  if (B == 0) return SVK_OK;
+  const long n = (long)B * OH * OW * C;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((resize_bwd_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, (const T*)dY, ldy, dX, B, H, W,
+                       C, OH, OW);
+    return check_launch("resize_bilinear_bwd");
+  });
+}
+
+extern "C" int svk_bcast_rows(int dtype, const float* dF, const float* mask, float scale, void* dY, int B, int R, int C,
+                              void* stream) {
+  if (B < 0 || R <= 0 || C <= 0 || !dF || !dY) { set_error("svk_bcast_rows: bad args"); return SVK_EINVAL; }
+  if (B == 0) return SVK_OK;
+  const long n = (long)B * R * C;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((bcast_rows_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, dF, mask, scale, (T*)dY, B, R,
+                       C);
+    return check_launch("bcast_rows");
+  });
+}
+
+extern "C" int svk_row_scale(int dtype, const void* X, const float* s, void* Y, long M, int C, int rows_per,
+                             void* stream) {
+  if (M < 0 || C <= 0 || rows_per <= 0 || !X || !s || !Y) { set_error("svk_row_scale: bad args"); return SVK_EINVAL; }
+  if (M == 0) return SVK_OK;
+  const long n = M * C;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((row_scale_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, (const T*)X, s, (T*)Y, n, C,
+                       rows_per);
+    return check_launch("row_scale");
+  });
+}
+
+extern "C" int svk_keep_mask(float* out, long n, float keep, unsigned seed, void* stream) {
+  if (n < 0 || !out || !(keep > 0.f) || keep > 1.f) { set_error("svk_keep_mask: bad args"); return SVK_EINVAL; }
+  if (n == 0) return SVK_OK;
+  hipLaunchKernelGGL(keep_mask_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, out, n, keep, (uint32_t)seed);
+  return check_launch("keep_mask");
+}
+
+extern "C" int svk_phase_loss(const float* logits, const float* ant, const long* labels, const float* ant_t, int B,
+                              int K, float* loss, float* dlogits, float* dant, void* stream) {
+  if (B <= 0 || K <= 0 || !logits || !ant || !labels || !ant_t || !loss || !dlogits || !dant) {
+    set_error("svk_phase_loss: bad args"); return SVK_EINVAL;
+  }
+  hipLaunchKernelGGL(phase_loss_kernel, dim3((B + 63) / 64), dim3(64), 0, (hipStream_t)stream, logits, ant, labels,
+                     ant_t, B, K, loss, dlogits, dant);
+  return check_launch("phase_loss");
+}
+
+extern "C" int svk_sgd(float* p, const float* grad, float* buf, long n, float lr, float momentum, float dampening,
+                       float wd, int nesterov, int first, void* stream) {
+  if (n < 0 || !p || !grad || (momentum != 0.f && !buf)) { set_error("svk_sgd: bad args"); return SVK_EINVAL; }
+  if (n == 0) return SVK_OK;
+  hipLaunchKernelGGL(sgd_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, p, grad, buf, n, lr, momentum, dampening,
+                     wd, nesterov, first);
+  return check_launch("sgd");
+}
+
+extern "C" int svk_unpatchify(int dtype, const void* P, void* Y, int B, int PH, int PW, int s, int C, int accumulate,
+                              void* stream) {
+  if (B < 0 || PH <= 0 || PW <= 0 || s <= 0 || C <= 0 || !P || !Y) { set_error("svk_unpatchify: bad args"); return SVK_EINVAL; }
+  if (B == 0) return SVK_OK;
+  const long n = (long)B * PH * PW * s * s * C;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((unpatchify_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, (const T*)P, (T*)Y, B, PH, PW,
+                       s, C, accumulate);
+    return check_launch("unpatchify");
+  });
+}
+
+extern "C" int svk_mul_f32(const float* a, const float* b, float* y, long n, void* stream) {
+  if (n < 0 || !a || !b || !y) { set_error("svk_mul_f32: bad args"); return SVK_EINVAL; }
+  if (n == 0) return SVK_OK;
+  hipLaunchKernelGGL(mul_f32_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, a, b, y, n);
+  return check_launch("mul_f32");
+}
+
+extern "C" int svk_bn_update_running(const float* sum, const float* sumsq, int M, int C, float momentum,
+                                     float* running_mean, float* running_var, void* stream) {
+  if (M <= 0 || C <= 0 || !sum || !sumsq || !running_mean || !running_var) {
+    set_error("svk_bn_update_running: bad args"); return SVK_EINVAL;
+  }
+  hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sum, sumsq, M, C,
+                     momentum, running_mean, running_var);
+  return check_launch("bn_update_running");
+}
+
+extern "C" int svk_pack_params(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,
+                               void* stream) {
+  if (ndesc <= 0 || total < 0 || !desc || !src || !dst) { set_error("svk_pack_params: bad args"); return SVK_EINVAL; }
+  if (total == 0) return SVK_OK;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((pack_params_kernel<T>), g1(total), dim3(256), 0, (hipStream_t)stream, (const PackDesc*)desc,
+                       ndesc, total, src, (T*)dst);
+    return check_launch("pack_params");
+  });
+}

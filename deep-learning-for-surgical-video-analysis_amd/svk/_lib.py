@@ -32,6 +32,31 @@ SIGNATURES = {
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
     "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
+    # training step
+    "svk_dwconv3x3_ex": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_gemm_ex": [c_int, P, c_long, P, c_long, P, P, c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, P],
+    "svk_gemm_wgrad": [c_int, P, c_long, P, c_long, P, c_long, c_int, c_int, c_int, P],
+    "svk_conv2d_wgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P],
+    "svk_conv2d_dgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
+                              c_int, P],
+    "svk_unpatchify": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_attention_bwd": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
+                          P, c_long, c_long, P, c_long, c_long, P, P, c_long, c_long, c_int, c_int, c_int, c_int,
+                          c_int, c_float, P],
+    "svk_layernorm_bwd": [c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
+    "svk_act_bwd": [c_int, P, P, P, P, c_long, c_int, P],
+    "svk_colstats": [c_int, P, c_long, c_int, c_int, P, P, P],
+    "svk_bn_apply": [c_int, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P],
+    "svk_bn_bwd": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P],
+    "svk_bn_update_running": [P, P, c_int, c_int, c_float, P, P, P],
+    "svk_resize_bilinear_bwd": [c_int, P, c_long, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_bcast_rows": [c_int, P, P, c_float, P, c_int, c_int, c_int, P],
+    "svk_row_scale": [c_int, P, P, P, c_long, c_int, c_int, P],
+    "svk_mul_f32": [P, P, P, c_long, P],
+    "svk_keep_mask": [P, c_long, c_float, ctypes.c_uint, P],
+    "svk_phase_loss": [P, P, P, P, c_int, c_int, P, P, P, P],
+    "svk_sgd": [P, P, P, c_long, c_float, c_float, c_float, c_float, c_int, c_int, P],
+    "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],
 }
 STRING_FUNCS = ("svk_version", "svk_last_error")
 

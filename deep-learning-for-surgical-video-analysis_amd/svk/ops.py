@@ -94,8 +94,9 @@ def _prof_end(start, name, flops, nbytes, shape=None):
     _PROF.append((name, flops, nbytes, start, e, shape))
 
 
-def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None):
-    """out = act(a @ w[:n].T + bias) + residual; a [..., K], w [N, K] (same dtype as a)."""
+def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=None, rows_per=1):
+    """out = row_scale[m // rows_per] * act(a @ w[:n].T + bias) + residual; a [..., K], w [N, K]
+    (same dtype as a); row_scale (f32) is optional (stochastic depth)."""
     _chk(a, "a"); _chk(w, "w", a.dtype); _chk(bias, "bias", torch.float32); _chk(residual, "residual", a.dtype)
     M, K, lda = _rows(a, "a")
     N = w.shape[0] if n is None else n
@@ -111,8 +112,15 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None):
         if rc != N:
             raise _lib.SvkError("svk.gemm: residual width mismatch")
     t0 = _prof_begin()
-    _lib.call("svk_gemm", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
-              _p(out), ldc, M, N, K, ACT[act], _stream())
+    if row_scale is None:
+        _lib.call("svk_gemm", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
+                  _p(out), ldc, M, N, K, ACT[act], _stream())
+    else:
+        _chk(row_scale, "row_scale", torch.float32)
+        if row_scale.numel() * rows_per < M:
+            raise _lib.SvkError("svk.gemm: row_scale too short")
+        _lib.call("svk_gemm_ex", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(row_scale),
+                  rows_per, _p(residual), ldr, _p(out), ldc, M, N, K, ACT[act], _stream())
     if t0 is not None:
         es = a.element_size()
         vw = 16 // es
@@ -202,12 +210,20 @@ def mixffn_fused(xn, x, w1, b1, taps, dbias, w2, b2):
     return out
 
 
-def dwconv3x3(x, taps, bias, act=None):
-    """x [B, H, W, C] NHWC contiguous; taps [9, C] f32; bias [C] f32."""
-    _chk(x, "x"); _chk(taps, "taps", torch.float32); _chk(bias, "bias", torch.float32)
+def dwconv3x3(x, taps, bias, act=None, pre_out=None):
+    """x [B, H, W, C] NHWC contiguous; taps [9, C] f32; bias [C] f32.  ``pre_out`` (same shape)
+    additionally receives the pre-activation map."""
+    _chk(x, "x"); _chk(taps, "taps", torch.float32); _chk(bias, "bias", torch.float32); _chk(pre_out, "pre_out", x.dtype)
     B, H, W, C = x.shape
     out = torch.empty_like(x)
-    _lib.call("svk_dwconv3x3", dtype_code(x.dtype), _p(x), _p(taps), _p(bias), _p(out), B, H, W, C, ACT[act], _stream())
+    if pre_out is None:
+        _lib.call("svk_dwconv3x3", dtype_code(x.dtype), _p(x), _p(taps), _p(bias), _p(out), B, H, W, C, ACT[act],
+                  _stream())
+    else:
+        if pre_out.shape != x.shape or not pre_out.is_contiguous():
+            raise _lib.SvkError("svk.dwconv3x3: pre_out shape mismatch")
+        _lib.call("svk_dwconv3x3_ex", dtype_code(x.dtype), _p(x), _p(taps), _p(bias), _p(out), _p(pre_out), B, H, W, C,
+                  ACT[act], _stream())
     return out
 
 
@@ -302,3 +318,211 @@ def add_bcast(x, table):
     _lib.call("svk_add_bcast", dtype_code(x.dtype), _p(x), _p(table), _p(out), x.numel() // C, C, table.shape[0],
               _stream())
     return out
+
+
+# ---- training step (train_evp.py:473-515) ----------------------------------------------------------
+
+def _f32_rows(t, name):
+    _chk(t, name, torch.float32)
+    return _rows(t, name)
+
+
+def gemm_wgrad(dy, x, dw):
+    """dw [N, K] f32 (row stride any) += dy[M, N]^T @ x[M, K]."""
+    _chk(dy, "dy"); _chk(x, "x", dy.dtype)
+    M, N, ldy = _rows(dy, "dy")
+    Mx, K, ldx = _rows(x, "x")
+    _, _, lddw = _f32_rows(dw, "dw")
+    if Mx != M or dw.shape[-1] != K or dw.numel() // K != N:
+        raise _lib.SvkError(f"svk.gemm_wgrad: shapes dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)}")
+    t0 = _prof_begin()
+    _lib.call("svk_gemm_wgrad", dtype_code(dy.dtype), _p(dy), ldy, _p(x), ldx, _p(dw), lddw, M, N, K, _stream())
+    _prof_end(t0, "wgrad_kernel", 2.0 * M * N * K, (M * (N + K)) * dy.element_size() + N * K * 4, (M, N, K, "wgrad"))
+    return dw
+
+
+def conv2d_wgrad(x, dy, k, stride, pad, dw):
+    """x [B, H, W, Cin] NHWC, dy [B, OH, OW, Cout]; dw [Cout, k*k*Cin] f32 += (packed like conv_w)."""
+    _chk(x, "x"); _chk(dy, "dy", x.dtype); _chk(dw, "dw", torch.float32)
+    B, H, W, Cin = x.shape
+    Cout = dy.shape[-1]
+    if not (x.is_contiguous() and dy.is_contiguous() and dw.is_contiguous()) or dw.numel() != Cout * k * k * Cin:
+        raise _lib.SvkError("svk.conv2d_wgrad: layout mismatch")
+    t0 = _prof_begin()
+    _lib.call("svk_conv2d_wgrad_nhwc", dtype_code(x.dtype), _p(x), B, H, W, Cin, _p(dy), Cout, k, stride, pad, _p(dw),
+              _stream())
+    M = dy.numel() // Cout
+    _prof_end(t0, "wgrad_kernel", 2.0 * M * Cout * k * k * Cin, (x.numel() + dy.numel()) * x.element_size(),
+              (M, Cout, k * k * Cin, f"convwgrad{k}s{stride}"))
+    return dw
+
+
+def conv2d_dgrad(dy, wd_packed, H, W, Cin, k, stride, pad, residual=None, out=None):
+    """dy [B, OH, OW, Cout]; wd_packed [Cin, k*k*Cout] -> dx [B, H, W, Cin] (+ residual)."""
+    _chk(dy, "dy"); _chk(wd_packed, "wd", dy.dtype)
+    B, OH, OW, Cout = dy.shape
+    if not dy.is_contiguous() or wd_packed.shape != (Cin, k * k * Cout) or not wd_packed.is_contiguous():
+        raise _lib.SvkError("svk.conv2d_dgrad: layout mismatch")
+    if out is None:
+        out = torch.empty(B, H, W, Cin, device=dy.device, dtype=dy.dtype)
+    for t, nm in ((out, "out"), (residual, "residual")):
+        if t is not None and (t.shape != (B, H, W, Cin) or not t.is_contiguous() or t.dtype != dy.dtype):
+            raise _lib.SvkError(f"svk.conv2d_dgrad: {nm} mismatch")
+    t0 = _prof_begin()
+    _lib.call("svk_conv2d_dgrad_nhwc", dtype_code(dy.dtype), _p(dy), B, OH, OW, Cout, _p(wd_packed), _p(residual),
+              _p(out), H, W, Cin, k, stride, pad, _stream())
+    M = B * H * W
+    vec = dy.data_ptr() % 16 == 0 and wd_packed.data_ptr() % 16 == 0 and Cout % 8 == 0
+    _prof_end(t0, _gemm_kernel_name(dtype_code(dy.dtype), M, Cin, vec, 2), 2.0 * M * Cin * k * k * Cout / stride ** 2,
+              (dy.numel() + out.numel()) * dy.element_size(), (M, Cin, k * k * Cout, f"convdgrad{k}s{stride}"))
+    return out
+
+
+def unpatchify(p, B, PH, PW, s, C, out, accumulate=False):
+    """p [B*PH*PW, s*s*C] -> out NHWC [B, PH*s, PW*s, C] (written or accumulated)."""
+    _chk(p, "p"); _chk(out, "out", p.dtype)
+    if not (p.is_contiguous() and out.is_contiguous()) or p.numel() != B * PH * PW * s * s * C or out.numel() != p.numel():
+        raise _lib.SvkError("svk.unpatchify: shape mismatch")
+    _lib.call("svk_unpatchify", dtype_code(p.dtype), _p(p), _p(out), B, PH, PW, s, C, 1 if accumulate else 0, _stream())
+    return out
+
+
+def attention_bwd(q, k, v, o, do, heads, scale, dk, dv, dq=None):
+    """Backward of attention(q, k, v): returns dq (compute dtype, [B, Nq, C]); dk/dv f32 [B, Nk, C]
+    views with equal strides (e.g. the two halves of one [B, Nk, 2C] buffer) are accumulated (zero them first)."""
+    for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
+        _chk(t, nm, q.dtype)
+        if t.dim() != 3 or t.stride(2) != 1:
+            raise _lib.SvkError(f"svk.attention_bwd: {nm} must be [B, N, C] with unit channel stride")
+    B, Nq, C = q.shape
+    Nk = k.shape[1]
+    for t, nm in ((dk, "dk"), (dv, "dv")):
+        _chk(t, nm, torch.float32)
+        if t.shape != (B, Nk, C) or t.stride(2) != 1 or t.stride() != dk.stride():
+            raise _lib.SvkError(f"svk.attention_bwd: {nm} must be f32 [B, Nk, C] (unit channel stride, dk/dv alike)")
+    if dq is None:
+        dq = torch.empty(B, Nq, C, device=q.device, dtype=q.dtype)
+    t0 = _prof_begin()
+    _lib.call("svk_attention_bwd", dtype_code(q.dtype), _p(q), q.stride(1), q.stride(0), _p(k), k.stride(1),
+              k.stride(0), _p(v), v.stride(1), v.stride(0), _p(o), o.stride(1), o.stride(0), _p(do), do.stride(1),
+              do.stride(0), _p(dq), dq.stride(1), dq.stride(0), _p(dk), _p(dv), dk.stride(1), dk.stride(0), B, Nq, Nk,
+              heads, C // heads, float(scale), _stream())
+    _prof_end(t0, "attention_bwd_kernel", 2.0 * B * Nq * Nk * C * 5, 0, (B, Nq, Nk, C, "attn_bwd"))
+    return dq
+
+
+def layernorm_bwd(x, dy, gamma, eps, dres=None, out=None, dgamma=None, dbeta=None):
+    """dx = LN'(x; gamma)^T dy (+ dres); dgamma/dbeta (f32) += when given."""
+    _chk(x, "x"); _chk(dy, "dy", x.dtype); _chk(gamma, "gamma", torch.float32); _chk(dres, "dres", x.dtype)
+    M, C, ldx = _rows(x, "x")
+    _, _, ldy = _rows(dy, "dy")
+    if out is None:
+        out = torch.empty(*x.shape, device=x.device, dtype=x.dtype)
+    _, _, ldo = _rows(out, "out")
+    ldr = _rows(dres, "dres")[2] if dres is not None else 0
+    _lib.call("svk_layernorm_bwd", dtype_code(x.dtype), _p(x), ldx, _p(dy), ldy, _p(gamma), _p(dres), ldr, _p(out),
+              ldo, _p(dgamma), _p(dbeta), M, C, float(eps), _stream())
+    return out
+
+
+def act_bwd(u, dy, act, dres=None, out=None):
+    _chk(u, "u"); _chk(dy, "dy", u.dtype); _chk(dres, "dres", u.dtype)
+    for t in (u, dy, dres):
+        if t is not None and not t.is_contiguous():
+            raise _lib.SvkError("svk.act_bwd: contiguous tensors required")
+    if out is None:
+        out = torch.empty_like(u)
+    _lib.call("svk_act_bwd", dtype_code(u.dtype), _p(u), _p(dy), _p(dres), _p(out), u.numel(), ACT[act], _stream())
+    return out
+
+
+def colstats(x, s, sq=None):
+    """s (+ sq) f32 [C] += column sums (of squares) of x [M, C]."""
+    _chk(x, "x"); _chk(s, "sum", torch.float32); _chk(sq, "sumsq", torch.float32)
+    M, C, ldx = _rows(x, "x")
+    _lib.call("svk_colstats", dtype_code(x.dtype), _p(x), ldx, M, C, _p(s), _p(sq), _stream())
+    return s
+
+
+def bn_apply(x, s, sq, gamma, beta, eps, act=None, out=None):
+    _chk(x, "x")
+    C = x.shape[-1]
+    M = x.numel() // C
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("svk_bn_apply", dtype_code(x.dtype), _p(x), _p(s), _p(sq), _p(gamma), _p(beta), _p(out), M, C,
+              float(eps), ACT[act], _stream())
+    return out
+
+
+def bn_bwd(x, dy, s, sq, gamma, beta, eps, dgamma, dbeta, relu=True, out=None):
+    _chk(x, "x"); _chk(dy, "dy", x.dtype)
+    C = x.shape[-1]
+    M = x.numel() // C
+    if out is None:
+        out = torch.empty_like(x)
+    _lib.call("svk_bn_bwd", dtype_code(x.dtype), _p(x), _p(dy), _p(s), _p(sq), _p(gamma), _p(beta), _p(out),
+              _p(dgamma), _p(dbeta), M, C, float(eps), 1 if relu else 0, _stream())
+    return out
+
+
+def bn_update_running(s, sq, M, running_mean, running_var, momentum):
+    _lib.call("svk_bn_update_running", _p(s), _p(sq), M, s.numel(), float(momentum), _p(running_mean),
+              _p(running_var), _stream())
+
+
+def resize_bilinear_bwd(dy, H, W, OH, OW, dx):
+    """dx f32 [B, H*W, C] += adjoint of resize_bilinear applied to dy [B, OH*OW, C]."""
+    _chk(dy, "dy"); _chk(dx, "dx", torch.float32)
+    B, C = dy.shape[0], dy.shape[-1]
+    if not dx.is_contiguous() or dx.numel() != B * H * W * C:
+        raise _lib.SvkError("svk.resize_bilinear_bwd: dx shape mismatch")
+    _lib.call("svk_resize_bilinear_bwd", dtype_code(dy.dtype), _p(dy), dy.stride(-2), _p(dx), B, H, W, C, OH, OW,
+              _stream())
+    return dx
+
+
+def bcast_rows(df, R, dtype, scale=1.0, mask=None):
+    """df f32 [B, C] -> [B*R, C] (dtype) rows df[b] * mask[b] * scale."""
+    _chk(df, "df", torch.float32); _chk(mask, "mask", torch.float32)
+    B, C = df.shape
+    out = torch.empty(B * R, C, device=df.device, dtype=dtype)
+    _lib.call("svk_bcast_rows", dtype_code(dtype), _p(df.contiguous()), _p(mask), float(scale), _p(out), B, R, C,
+              _stream())
+    return out
+
+
+def mul_f32(a, b):
+    _chk(a, "a", torch.float32); _chk(b, "b", torch.float32)
+    out = torch.empty_like(a)
+    _lib.call("svk_mul_f32", _p(a), _p(b), _p(out), a.numel(), _stream())
+    return out
+
+
+def keep_mask(n, keep, seed, device):
+    out = torch.empty(n, device=device, dtype=torch.float32)
+    _lib.call("svk_keep_mask", _p(out), n, float(keep), int(seed) & 0xFFFFFFFF, _stream())
+    return out
+
+
+def phase_loss(logits, ant, labels, ant_targets):
+    """CE(sum) + SmoothL1(sum) -> (loss f32 [2], dlogits, dant)."""
+    for t, nm in ((logits, "logits"), (ant, "ant"), (ant_targets, "ant_targets")):
+        _chk(t, nm, torch.float32)
+    _chk(labels, "labels", torch.int64)
+    B, K = logits.shape
+    loss = torch.zeros(2, device=logits.device, dtype=torch.float32)
+    dl = torch.empty_like(logits)
+    da = torch.empty_like(ant)
+    _lib.call("svk_phase_loss", _p(logits.contiguous()), _p(ant.contiguous()), _p(labels.contiguous()),
+              _p(ant_targets.contiguous()), B, K, _p(loss), _p(dl), _p(da), _stream())
+    return loss, dl, da
+
+
+def sgd(p, g, buf, lr, momentum, dampening, wd, nesterov, first):
+    _lib.call("svk_sgd", _p(p), _p(g), _p(buf), p.numel(), float(lr), float(momentum), float(dampening), float(wd),
+              1 if nesterov else 0, 1 if first else 0, _stream())
+
+
+def pack_params(desc, ndesc, total, src, dst):
+    _lib.call("svk_pack_params", dtype_code(dst.dtype), _p(desc), ndesc, total, _p(src), _p(dst), _stream())

@@ -1,0 +1,675 @@
+"""Native frozen-backbone training step of MixVisionTransformerEVP — MI355X build.
+
+Replaces the inner loop of ``train_model`` (train_evp.py:473-515): autocast forward, CE(sum) +
+SmoothL1(sum) loss, backward, SGD step.  Every op is an svk kernel with an explicit backward:
+
+* what trains (train_evp.py:379-382): parameters whose names contain ``head``, ``prompt``,
+  ``flow_encoder``, ``cross_attn_s3`` or ``cross_attn_s4`` (24.79 M for mit_b2_evp).  The
+  backbone is frozen but the prompts are injected before every block, so the backward runs the
+  *data* gradient through every backbone block (no weight gradients there);
+* train-mode semantics: timm DropPath per block branch (drop_path_rate 0.1, linear rule,
+  mix_transformer_evp.py:238) fused as a per-frame row scale into the branch GEMM epilogue and its
+  adjoint; Dropout2d(0.1) on the fused head map applied after the (linear) average pool;
+  BatchNorm with batch statistics (head linear_fuse.bn, flow encoder bn1..4) and the running-stat
+  momentum update;
+* the head is NOT folded in training (its BN uses batch statistics): linear_c* run on the 7x7
+  resized maps (exact: resize and the per-token Linear commute) into one [B*49, 8192] buffer,
+  then the 1x1 fuse GEMM, BN, ReLU, pool;
+* parameters live in one flat f32 buffer (the nn.Parameters are views into it, their ``.grad``
+  views into a flat gradient buffer), so SGD is one kernel, the DDP gradient all-reduce is one
+  RCCL call on one buffer, and a single batched gather re-packs every compute-dtype weight
+  view (forward and transposed layouts) after the step;
+* GradScaler (train_evp.py:443, 512-515) is not needed: bf16 has fp32's exponent range.
+
+Frames per step B = 88 at the reference setting (train_evp.py:28).
+"""
+import numpy as np
+import torch
+from torch.autograd.graph import increment_version
+
+from . import ops
+from ._lib import SvkError
+from .pack import pad_channels, conv_w
+
+TRAINABLE = ("head", "prompt", "flow_encoder", "cross_attn_s3", "cross_attn_s4")
+_BN_BUFFERS = ("running_mean", "running_var", "num_batches_tracked")
+DROP_PATH_RATE = 0.1
+HEAD_DROPOUT = 0.1
+BLOCK_EPS, LN_EPS, BN_EPS, BN_MOMENTUM = 1e-6, 1e-5, 1e-5, 0.1
+
+_DESC = np.dtype([("src", "<i8"), ("dst", "<i8"), ("n", "<i4", 4), ("s", "<i8", 4), ("lim", "<i4", 4),
+                  ("start", "<i8")])      # csrc/train.hip PackDesc
+
+
+def is_trainable(name):
+    return any(k in name for k in TRAINABLE) and not name.endswith(_BN_BUFFERS)
+
+
+class _PackTable:
+    """Descriptor table for svk_pack_params: f32 master (flat) -> packed buffer (flat, dtype)."""
+
+    def __init__(self, dtype):
+        self.dtype = dtype
+        self.rows = []
+        self.total = 0
+        self.views = []
+
+    def add(self, src, shape, strides, lims=None):
+        n = [1] * (4 - len(shape)) + list(shape)
+        s = [0] * (4 - len(strides)) + list(strides)
+        lim = [1] * (4 - len(shape)) + list(lims if lims is not None else shape)
+        numel = int(np.prod(shape))
+        off = self.total
+        self.rows.append((src, off, n, s, lim, off))
+        self.total += (numel + 7) // 8 * 8      # keep every packed tensor 16-byte aligned
+        self.views.append((off, tuple(shape)))
+        return len(self.views) - 1
+
+    def finalize(self, device):
+        arr = np.zeros(len(self.rows), dtype=_DESC)
+        for i, (src, dst, n, s, lim, start) in enumerate(self.rows):
+            arr[i] = (src, dst, n, s, lim, start)
+        raw = torch.from_numpy(arr.view(np.uint8).copy())
+        self.desc = raw.to(device)
+        self.buf = torch.zeros(max(self.total, 8), device=device, dtype=self.dtype)
+        self.tensors = [self.buf[o:o + int(np.prod(sh))].view(sh) for o, sh in self.views]
+
+    def run(self, master, dst=None):
+        if self.rows:
+            ops.pack_params(self.desc, len(self.rows), self.total, master, self.buf if dst is None else dst)
+
+
+def _t(w):
+    """Frozen weight -> transposed contiguous copy (one-time packing)."""
+    return w.detach().t().contiguous()
+
+
+class EVPTrainStep:
+    """One optimizer step per call over a batch of frames; owns the flat parameter/gradient/momentum
+    buffers of the trainable parameters.  ``process_group``: torch.distributed group for DDP
+    (gradient all-reduce, BN buffer broadcast from rank 0); None = single process."""
+
+    def __init__(self, model, lr=5e-4, momentum=0.9, dampening=0.0, weight_decay=1e-5, nesterov=False,
+                 dtype=torch.bfloat16, drop=True, seed=0, process_group=None, world_size=1):
+        self.model = model
+        self.dt = dtype
+        self.hp = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)
+        self.drop = drop
+        self.seed = seed
+        self.group = process_group
+        self.world = world_size
+        self.steps = 0
+        dev = next(model.parameters()).device
+        if dev.type != "cuda":
+            raise SvkError("EVPTrainStep: model must be on a GPU (there is no CPU path)")
+        self.dev = dev
+        model.train()
+        self.depths = list(model.depths)
+        self.dims = list(model.embed_dims)
+        self._setup_flat()
+        self._setup_frozen()
+        self._setup_packs()
+
+    # ---- parameter storage ------------------------------------------------------------------
+    def _setup_flat(self):
+        tr = []
+        for n, p in self.model.named_parameters():
+            p.requires_grad_(is_trainable(n))
+            if p.requires_grad:
+                tr.append((n, p))
+        total = sum(p.numel() for _, p in tr)
+        self.flat = torch.empty(total, device=self.dev, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=self.dev, dtype=torch.float32)
+        self.mom = torch.zeros(total, device=self.dev, dtype=torch.float32)
+        self.off = {}
+        o = 0
+        with torch.no_grad():
+            for n, p in tr:
+                k = p.numel()
+                self.flat[o:o + k].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + k].view_as(p)
+                p.grad = self.grad[o:o + k].view_as(p)
+                self.off[n] = o
+                o += k
+        self.params = dict(tr)
+        self.n_trainable = total
+
+    def P(self, name):
+        """f32 master view of a trainable parameter."""
+        return self.params[name]
+
+    def G(self, name):
+        """f32 gradient view of a trainable parameter."""
+        return self.params[name].grad
+
+    # ---- packs --------------------------------------------------------------------------------
+    def _setup_packs(self):
+        dt = self.dt
+        tab, tab32, un = _PackTable(dt), _PackTable(torch.float32), _PackTable(torch.float32)
+        self.pk, self.pk32 = {}, {}
+        conv_scratch = 0
+        self.conv_grad = {}
+
+        def lin(name, transposed=True):
+            N, K = self.params[name].shape[:2]
+            o = self.off[name]
+            self.pk[name] = tab.add(o, (N, K), (K, 1))
+            if transposed:
+                self.pk[name + ".T"] = tab.add(o, (K, N), (1, K))
+
+        def conv(name, dgrad, pad_in=False):
+            nonlocal conv_scratch
+            co, ci, k, _ = self.params[name].shape
+            o = self.off[name]
+            cp = pad_channels(ci) if pad_in else ci
+            self.pk[name] = tab.add(o, (co, k, k, cp), (ci * k * k, k, 1, k * k), (co, k, k, ci))
+            if dgrad:
+                self.pk[name + ".D"] = tab.add(o, (ci, k, k, co), (k * k, k, 1, ci * k * k))
+            # weight-gradient scratch in the packed layout, unpacked into the flat grad after backward
+            n = co * k * k * cp
+            self.conv_grad[name] = (conv_scratch, (co, k * k * cp))
+            un_rows.append((conv_scratch, name, co, ci, k, cp))
+            conv_scratch += (n + 7) // 8 * 8
+
+        un_rows = []
+        pg = "prompt_generator"
+        for s in range(4):
+            conv(f"{pg}.handcrafted_generator{s + 1}.proj.weight", dgrad=s > 0, pad_in=s == 0)
+            lin(f"{pg}.embedding_generator{s + 1}.weight")
+            lin(f"{pg}.shared_mlp{s + 1}.weight")
+            for i in range(self.depths[s]):
+                lin(f"{pg}.lightweight_mlp{s + 1}_{i}.0.weight")
+        for i in range(1, 5):
+            conv(f"flow_encoder.conv{i}.weight", dgrad=i > 1, pad_in=i == 1)
+        for s in (3, 4):
+            nm = f"cross_attn_s{s}.cross_attn.in_proj_weight"
+            E = self.params[nm].shape[1]
+            o = self.off[nm]
+            self.pk[nm] = tab.add(o, (3 * E, E), (E, 1))
+            self.pk[nm + ".qT"] = tab.add(o, (E, E), (1, E))
+            self.pk[nm + ".kvT"] = tab.add(o + E * E, (E, 2 * E), (1, E))
+            lin(f"cross_attn_s{s}.cross_attn.out_proj.weight")
+        for i in range(1, 5):
+            lin(f"head.linear_c{i}.proj.weight")
+        nm = "head.linear_fuse.conv.weight"
+        E, K = self.params[nm].shape[:2]
+        self.pk[nm] = tab.add(self.off[nm], (E, K), (K, 1))
+        self.pk[nm + ".T"] = tab.add(self.off[nm], (K, E), (1, K))
+        for h in ("fc", "fc_ant"):
+            for j in (0, 2):
+                nm = f"head.{h}.{j}.weight"
+                N, K = self.params[nm].shape
+                self.pk32[nm + ".T"] = tab32.add(self.off[nm], (K, N), (1, K))
+        # packed conv grads -> flat grad ([co][k][k][cp] -> [co][ci][k][k])
+        for sc, name, co, ci, k, cp in un_rows:
+            un.add(sc, (co, ci, k, k), (k * k * cp, 1, k * cp, cp))
+        for t in (tab, tab32, un):
+            t.finalize(self.dev)
+        self.tab, self.tab32, self.untab = tab, tab32, un
+        self.conv_scratch = torch.zeros(max(conv_scratch, 8), device=self.dev, dtype=torch.float32)
+        # the unpack table writes into the flat gradient at each conv weight's offset
+        for i, (sc, name, co, ci, k, cp) in enumerate(un_rows):
+            self.untab.rows[i] = (sc, self.off[name], *self.untab.rows[i][2:5], self.untab.rows[i][5])
+        arr = np.zeros(len(self.untab.rows), dtype=_DESC)
+        for i, r in enumerate(self.untab.rows):
+            arr[i] = r
+        self.untab.desc = torch.from_numpy(arr.view(np.uint8).copy()).to(self.dev)
+        self._refresh_packs()
+
+    def _refresh_packs(self):
+        self.tab.run(self.flat)
+        self.tab32.run(self.flat)
+
+    def W(self, key):
+        return self.tab.tensors[self.pk[key]]
+
+    def W32T(self, key):
+        return self.tab32.tensors[self.pk32[key]]
+
+    def CG(self, name):
+        o, shape = self.conv_grad[name]
+        return self.conv_scratch[o:o + shape[0] * shape[1]].view(shape)
+
+    def _setup_frozen(self):
+        """One-time packs of the frozen backbone (forward and adjoint layouts)."""
+        m, dt = self.model, self.dt
+        self.fz = []
+        with torch.no_grad():
+            for s in range(4):
+                pe = getattr(m, f"patch_embed{s + 1}")
+                w = pe.proj.weight.detach()
+                co, ci, k, _ = w.shape
+                st = dict(k=k, stride=pe.stride, pad=k // 2)
+                st["w"] = conv_w(w, dt, pad_channels(ci))
+                st["wd"] = w.permute(1, 2, 3, 0).reshape(ci, k * k * co).to(dt).contiguous() if s > 0 else None
+                st["b"] = pe.proj.bias.detach().float().contiguous()
+                st["g"], st["beta"] = pe.norm.weight.detach().float().contiguous(), pe.norm.bias.detach().float().contiguous()
+                norm = getattr(m, f"norm{s + 1}")
+                st["ng"], st["nb"] = norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous()
+                blocks = []
+                for blk in getattr(m, f"block{s + 1}"):
+                    a, f = blk.attn, blk.mlp
+                    C = a.dim
+                    b = dict(heads=a.num_heads, scale=a.scale, sr=a.sr_ratio,
+                             g1=blk.norm1.weight.detach().float().contiguous(),
+                             b1=blk.norm1.bias.detach().float().contiguous(),
+                             g2=blk.norm2.weight.detach().float().contiguous(),
+                             b2=blk.norm2.bias.detach().float().contiguous(),
+                             wq=a.q.weight.detach().to(dt).contiguous(), bq=a.q.bias.detach().float().contiguous(),
+                             wqT=_t(a.q.weight).to(dt), wkv=a.kv.weight.detach().to(dt).contiguous(),
+                             bkv=a.kv.bias.detach().float().contiguous(), wkvT=_t(a.kv.weight).to(dt),
+                             wp=a.proj.weight.detach().to(dt).contiguous(),
+                             bp=a.proj.bias.detach().float().contiguous(), wpT=_t(a.proj.weight).to(dt),
+                             w1=f.fc1.weight.detach().to(dt).contiguous(), bf1=f.fc1.bias.detach().float().contiguous(),
+                             w1T=_t(f.fc1.weight).to(dt), w2=f.fc2.weight.detach().to(dt).contiguous(),
+                             bf2=f.fc2.bias.detach().float().contiguous(), w2T=_t(f.fc2.weight).to(dt))
+                    dw = f.dwconv.dwconv
+                    hid = dw.weight.shape[0]
+                    taps = dw.weight.detach().float().reshape(hid, 9).t().contiguous()
+                    b["taps"], b["dwb"] = taps, dw.bias.detach().float().contiguous()
+                    b["taps_flip"] = taps.flip(0).contiguous()
+                    b["zero"] = torch.zeros(hid, device=self.dev, dtype=torch.float32)
+                    if a.sr_ratio > 1:
+                        r = a.sr_ratio
+                        wsr = a.sr.weight.detach()
+                        b["wsr"] = conv_w(wsr, dt)
+                        b["bsr"] = a.sr.bias.detach().float().contiguous()
+                        b["wsrD"] = wsr.permute(2, 3, 1, 0).reshape(r * r * C, C).to(dt).contiguous()
+                        b["gn"] = a.norm.weight.detach().float().contiguous()
+                        b["bn"] = a.norm.bias.detach().float().contiguous()
+                    blocks.append(b)
+                st["blocks"] = blocks
+                self.fz.append(st)
+
+    # ---- masks ----------------------------------------------------------------------------------
+    def make_masks(self, B):
+        """Device DropPath / Dropout2d masks for this step (values 0 or 1/keep)."""
+        dpr = torch.linspace(0, DROP_PATH_RATE, sum(self.depths)).tolist()
+        blocks, cur = [], 0
+        base = (self.seed * 1000003 + self.steps * 7919) & 0x7FFFFFFF
+        ones = torch.ones(B, device=self.dev, dtype=torch.float32)
+        for s, d in enumerate(self.depths):
+            st = []
+            for i in range(d):
+                r = dpr[cur + i]
+                if self.drop and r > 0:
+                    st.append(tuple(ops.keep_mask(B, 1.0 - r, base + 2 * (cur + i) + j, self.dev) for j in range(2)))
+                else:
+                    st.append((ones, ones))
+            blocks.append(st)
+            cur += d
+        if self.drop:
+            d2 = ops.keep_mask(B * 2048, 1.0 - HEAD_DROPOUT, base + 99991, self.dev).view(B, 2048)
+        else:
+            d2 = torch.ones(B, 2048, device=self.dev, dtype=torch.float32)
+        return {"blocks": blocks, "dropout2d": d2}
+
+    # ---- forward ----------------------------------------------------------------------------------
+    def _forward(self, x, y, flow, masks):
+        dt, pg = self.dt, "prompt_generator"
+        B = x.numel() // (3 * 224 * 224)
+        sv = {"B": B}
+        # handcrafted prompt cascade (trainable; mix_transformer_evp.py:718-747)
+        prev = ops.gauss5x5_reflect(y.reshape(B, 3, 224, 224).float(), dt, cpad=8)
+        hc = []
+        for s in range(4):
+            nm = f"{pg}.handcrafted_generator{s + 1}"
+            k, st = (7, 4) if s == 0 else (3, 2)
+            z = ops.conv2d_nhwc(prev, self.W(nm + ".proj.weight"), k, st, k // 2, bias=self.P(nm + ".proj.bias"))
+            _, OH, OW, C = z.shape
+            h = ops.layernorm(z.view(B, OH * OW, C), self.P(nm + ".norm.weight"), self.P(nm + ".norm.bias"), LN_EPS)
+            hc.append(dict(inp=prev, z=z, h=h, k=k, st=st, H=OH, W=OW, C=C))
+            prev = h.view(B, OH, OW, C)
+        sv["hc"] = hc
+        # backbone with prompts (frozen weights; mix_transformer_evp.py:352-416)
+        cur = ops.nchw_to_nhwc(x.reshape(B, 3, 224, 224).float(), dt, cpad=8)
+        stages = []
+        for s in range(4):
+            fz = self.fz[s]
+            z = ops.conv2d_nhwc(cur, fz["w"], fz["k"], fz["stride"], fz["pad"], bias=fz["b"])
+            _, H, W, C = z.shape
+            N = H * W
+            t = ops.layernorm(z.view(B, N, C), fz["g"], fz["beta"], LN_EPS)
+            eg = f"{pg}.embedding_generator{s + 1}"
+            summed = ops.gemm(t, self.W(eg + ".weight"), self.P(eg + ".bias"), residual=hc[s]["h"])
+            st = dict(in_hw=(cur.shape[1], cur.shape[2], cur.shape[3]), z=z, t=t, summed=summed, H=H, W=W, C=C, N=N,
+                      blocks=[])
+            x_ = t
+            sh = f"{pg}.shared_mlp{s + 1}"
+            for i, b in enumerate(fz["blocks"]):
+                lw = f"{pg}.lightweight_mlp{s + 1}_{i}.0"
+                fpre = ops.gemm(summed, self.W(lw + ".weight"), self.P(lw + ".bias"))
+                f = ops.gemm(summed, self.W(lw + ".weight"), self.P(lw + ".bias"), act="gelu")
+                xp = ops.gemm(f, self.W(sh + ".weight"), self.P(sh + ".bias"), residual=x_)
+                ma, mm = masks["blocks"][s][i]
+                sb = self._block_fwd(xp, b, B, H, W, C, ma, mm)
+                sb.update(fpre=fpre, f=f, xp=xp, ma=ma, mm=mm)
+                st["blocks"].append(sb)
+                x_ = sb["out"]
+            st["last"] = x_
+            c = ops.layernorm(x_, fz["ng"], fz["nb"], BLOCK_EPS)
+            st["c"] = c
+            stages.append(st)
+            cur = c.view(B, H, W, C)
+        sv["stages"] = stages
+        # flow encoder, BN in train mode
+        fl = []
+        prev = ops.nchw_to_nhwc(flow.reshape(B, 2, 224, 224).float(), dt, cpad=8)
+        for i, (k, st_, pad) in enumerate(((7, 4, 3), (3, 2, 1), (3, 2, 1), (3, 2, 1)), start=1):
+            nm = f"flow_encoder.conv{i}"
+            z = ops.conv2d_nhwc(prev, self.W(nm + ".weight"), k, st_, pad, bias=self.P(nm + ".bias"))
+            Cz = z.shape[-1]
+            s1 = torch.zeros(Cz, device=self.dev, dtype=torch.float32)
+            s2 = torch.zeros(Cz, device=self.dev, dtype=torch.float32)
+            ops.colstats(z.view(-1, Cz), s1, s2)
+            bn = f"flow_encoder.bn{i}"
+            yb = ops.bn_apply(z, s1, s2, self.P(bn + ".weight"), self.P(bn + ".bias"), BN_EPS, act="relu")
+            fl.append(dict(inp=prev, z=z, y=yb, s1=s1, s2=s2, k=k, st=st_, pad=pad))
+            prev = yb
+        sv["flow"] = fl
+        # motion-guided cross attention on c3 / c4
+        ca = {}
+        for s in (3, 4):
+            c = stages[s - 1]["c"]
+            f = fl[s - 1]["y"]
+            f = f.view(B, -1, f.shape[-1])
+            ca[s] = self._cross_fwd(s, c, f)
+        sv["ca"] = ca
+        # head, train mode
+        sv["head"] = hd = self._head_fwd(B, [stages[0]["c"], stages[1]["c"], ca[3]["out"], ca[4]["out"]],
+                                         [(st["H"], st["W"]) for st in stages], masks["dropout2d"])
+        return sv, hd["logits"], hd["ant"]
+
+    def _block_fwd(self, xp, b, B, H, W, C, ma, mm):
+        N = H * W
+        xn1 = ops.layernorm(xp, b["g1"], b["b1"], BLOCK_EPS)
+        q = ops.gemm(xn1, b["wq"], b["bq"])
+        sv = {}
+        if b["sr"] > 1:
+            r = b["sr"]
+            xs_pre = ops.conv2d_nhwc(xn1.view(B, H, W, C), b["wsr"], r, r, 0, bias=b["bsr"]).view(B, -1, C)
+            xs = ops.layernorm(xs_pre, b["gn"], b["bn"], LN_EPS)
+            sv["xs_pre"] = xs_pre
+        else:
+            xs = xn1
+        kv = ops.gemm(xs, b["wkv"], b["bkv"])
+        o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], b["heads"], b["scale"])
+        x1 = ops.gemm(o, b["wp"], b["bp"], residual=xp, row_scale=ma, rows_per=N)
+        xn2 = ops.layernorm(x1, b["g2"], b["b2"], BLOCK_EPS)
+        h = ops.gemm(xn2, b["w1"], b["bf1"])
+        hid = h.shape[-1]
+        u = torch.empty(B, H, W, hid, device=self.dev, dtype=self.dt)
+        g = ops.dwconv3x3(h.view(B, H, W, hid), b["taps"], b["dwb"], act="gelu", pre_out=u)
+        out = ops.gemm(g.view(B, N, hid), b["w2"], b["bf2"], residual=x1, row_scale=mm, rows_per=N)
+        sv.update(q=q, kv=kv, o=o, x1=x1, u=u, out=out)
+        return sv
+
+    def _cross_fwd(self, s, c, f):
+        p = f"cross_attn_s{s}"
+        E = c.shape[-1]
+        wi = self.W(p + ".cross_attn.in_proj_weight")
+        bi = self.P(p + ".cross_attn.in_proj_bias")
+        q = ops.gemm(c, wi[:E], bi[:E])
+        kv = ops.gemm(f, wi[E:], bi[E:])
+        heads = 8
+        o = ops.attention(q, kv[:, :, :E], kv[:, :, E:], heads, (E // heads) ** -0.5)
+        a = ops.gemm(o, self.W(p + ".cross_attn.out_proj.weight"), self.P(p + ".cross_attn.out_proj.bias"), residual=c)
+        out = ops.layernorm(a, self.P(p + ".norm.weight"), self.P(p + ".norm.bias"), LN_EPS)
+        return dict(c=c, f=f, q=q, kv=kv, o=o, a=a, out=out, E=E, heads=heads)
+
+    def _head_fwd(self, B, toks, hw, d2mask):
+        H4, W4 = hw[3]
+        R = H4 * W4
+        Ed = 2048
+        E = torch.empty(B * R, 4 * Ed, device=self.dev, dtype=self.dt)
+        rs = []
+        for j, lvl in enumerate((3, 2, 1, 0)):             # torch.cat([_c4, _c3, _c2, _c1]) (segformer_head.py:158)
+            t = toks[lvl]
+            H, W = hw[lvl]
+            r = t if (H, W) == (H4, W4) else ops.resize_bilinear(t, H, W, H4, W4)
+            r = r.reshape(B * R, -1)
+            nm = f"head.linear_c{lvl + 1}.proj"
+            ops.gemm(r, self.W(nm + ".weight"), self.P(nm + ".bias"), out=E[:, j * Ed:(j + 1) * Ed])
+            rs.append((lvl, r, H, W))
+        Z = ops.gemm(E, self.W("head.linear_fuse.conv.weight"))
+        s1 = torch.zeros(Ed, device=self.dev, dtype=torch.float32)
+        s2 = torch.zeros(Ed, device=self.dev, dtype=torch.float32)
+        ops.colstats(Z, s1, s2)
+        bn = "head.linear_fuse.bn"
+        Yb = ops.bn_apply(Z, s1, s2, self.P(bn + ".weight"), self.P(bn + ".bias"), BN_EPS, act="relu")
+        feat = ops.mul_f32(ops.mean_rows(Yb, R), d2mask)
+        outs, hs = [], []
+        for h in ("fc", "fc_ant"):
+            h1 = ops.gemm(feat, self.P(f"head.{h}.0.weight"), self.P(f"head.{h}.0.bias"), act="relu")
+            outs.append(ops.gemm(h1, self.P(f"head.{h}.2.weight"), self.P(f"head.{h}.2.bias")))
+            hs.append(h1)
+        return dict(E=E, rs=rs, Z=Z, s1=s1, s2=s2, feat=feat, hs=hs, logits=outs[0], ant=outs[1], R=R, d2=d2mask)
+
+    # ---- backward ---------------------------------------------------------------------------------
+    def _wg(self, dy, x, name, bias_name=None):
+        """Linear weight/bias gradients: dW += dy^T x; db += colsum(dy)."""
+        ops.gemm_wgrad(dy.reshape(-1, dy.shape[-1]), x.reshape(-1, x.shape[-1]), self.G(name))
+        if bias_name is not None:
+            ops.colstats(dy.reshape(-1, dy.shape[-1]), self.G(bias_name))
+
+    def _backward(self, sv, dlogits, dant):
+        dt, B, pg = self.dt, sv["B"], "prompt_generator"
+        hd = sv["head"]
+        # fc / fc_ant (f32)
+        dfeat = None
+        for h, dl, h1 in (("fc", dlogits, hd["hs"][0]), ("fc_ant", dant, hd["hs"][1])):
+            self._wg(dl, h1, f"head.{h}.2.weight", f"head.{h}.2.bias")
+            dh = ops.gemm(dl, self.W32T(f"head.{h}.2.weight.T"))
+            dh = ops.act_bwd(h1, dh, "relu")
+            self._wg(dh, hd["feat"], f"head.{h}.0.weight", f"head.{h}.0.bias")
+            dfeat = ops.gemm(dh, self.W32T(f"head.{h}.0.weight.T"), residual=dfeat)
+        # Dropout2d + average pool + BN(train) + ReLU
+        R = hd["R"]
+        dY = ops.bcast_rows(dfeat, R, dt, scale=1.0 / R, mask=hd["d2"])
+        bn = "head.linear_fuse.bn"
+        dZ = ops.bn_bwd(hd["Z"], dY, hd["s1"], hd["s2"], self.P(bn + ".weight"), self.P(bn + ".bias"), BN_EPS,
+                        self.G(bn + ".weight"), self.G(bn + ".bias"), relu=True)
+        ops.gemm_wgrad(dZ, hd["E"], self.G("head.linear_fuse.conv.weight").view(2048, -1))
+        dE = ops.gemm(dZ, self.W("head.linear_fuse.conv.weight.T"))
+        stages = sv["stages"]
+        dtok = [None] * 4
+        for j, (lvl, r, H, W) in enumerate(hd["rs"]):
+            dEj = dE[:, j * 2048:(j + 1) * 2048]
+            nm = f"head.linear_c{lvl + 1}.proj"
+            self._wg(dEj, r, nm + ".weight", nm + ".bias")
+            dr = ops.gemm(dEj, self.W(nm + ".weight.T"))
+            if (H * W) == R:
+                dtok[lvl] = dr.view(B, R, -1)
+            else:
+                acc = torch.zeros(B, H * W, dr.shape[-1], device=self.dev, dtype=torch.float32)
+                ops.resize_bilinear_bwd(dr.view(B, R, -1), H, W, 7, 7, acc)
+                dtok[lvl] = ops.cast(acc, dt)
+        # cross attention (s4, s3) -> grads of backbone c3/c4 and of the flow features
+        dflow = {}
+        for s in (4, 3):
+            dtok[s - 1], dflow[s] = self._cross_bwd(s, sv["ca"][s], dtok[s - 1])
+        self._flow_bwd(sv["flow"], dflow, B)
+        # backbone, stage 4 -> 1
+        dhc = [None] * 4
+        dnext = None
+        for s in range(3, -1, -1):
+            st, fz = stages[s], self.fz[s]
+            dc = dtok[s].reshape(B, st["N"], st["C"])
+            if dnext is not None:
+                dc = dnext
+            d = ops.layernorm_bwd(st["last"], dc, fz["ng"], BLOCK_EPS)
+            dsum = None
+            sh = f"{pg}.shared_mlp{s + 1}"
+            for i in range(len(fz["blocks"]) - 1, -1, -1):
+                b, sb = fz["blocks"][i], st["blocks"][i]
+                d = self._block_bwd(d, b, sb, B, st["H"], st["W"], st["C"])
+                # prompt: xp = x + shared(GELU(lw_i(summed)))
+                lw = f"{pg}.lightweight_mlp{s + 1}_{i}.0"
+                self._wg(d, sb["f"], sh + ".weight", sh + ".bias")
+                df = ops.gemm(d, self.W(sh + ".weight.T"))
+                dfp = ops.act_bwd(sb["fpre"], df, "gelu")
+                self._wg(dfp, st["summed"], lw + ".weight", lw + ".bias")
+                dsum = ops.gemm(dfp, self.W(lw + ".weight.T"), residual=dsum, out=dsum)
+            eg = f"{pg}.embedding_generator{s + 1}"
+            self._wg(dsum, st["t"], eg + ".weight", eg + ".bias")
+            d = ops.gemm(dsum, self.W(eg + ".weight.T"), residual=d, out=d)
+            dhc[s] = dsum
+            if s > 0:
+                # frozen patch embed: LN backward then conv data gradient, added to the previous stage's grad
+                dz = ops.layernorm_bwd(st["z"].view(B, st["N"], st["C"]), d, fz["g"], LN_EPS)
+                Hp, Wp, Cp = st["in_hw"]
+                prev = dtok[s - 1].reshape(B, Hp, Wp, Cp).contiguous()
+                dnext = ops.conv2d_dgrad(dz.view(B, st["H"], st["W"], st["C"]), fz["wd"], Hp, Wp, Cp, fz["k"],
+                                         fz["stride"], fz["pad"], residual=prev).view(B, Hp * Wp, Cp)
+        # handcrafted cascade backward (trainable convs + LNs)
+        dh = dhc[3]
+        for s in range(3, -1, -1):
+            h = sv["hc"][s]
+            nm = f"{pg}.handcrafted_generator{s + 1}"
+            dz = ops.layernorm_bwd(h["z"].view(B, h["H"] * h["W"], h["C"]), dh.view(B, h["H"] * h["W"], h["C"]),
+                                   self.P(nm + ".norm.weight"), LN_EPS, dgamma=self.G(nm + ".norm.weight"),
+                                   dbeta=self.G(nm + ".norm.bias"))
+            dzm = dz.view(B, h["H"], h["W"], h["C"])
+            ops.conv2d_wgrad(h["inp"], dzm, h["k"], h["st"], h["k"] // 2, self.CG(nm + ".proj.weight"))
+            ops.colstats(dz.view(-1, h["C"]), self.G(nm + ".proj.bias"))
+            if s > 0:
+                pin = h["inp"]
+                dh = ops.conv2d_dgrad(dzm, self.W(nm + ".proj.weight.D"), pin.shape[1], pin.shape[2], pin.shape[3],
+                                      h["k"], h["st"], h["k"] // 2,
+                                      residual=dhc[s - 1].view(pin.shape).contiguous())
+
+    def _block_bwd(self, d, b, sb, B, H, W, C):
+        """Data gradient through one frozen block (given d = dL/d out) -> dL/d xp."""
+        N = H * W
+        hid = sb["u"].shape[-1]
+        dg = ops.gemm(d, b["w2T"], row_scale=sb["mm"], rows_per=N)
+        du = ops.act_bwd(sb["u"].view(B, N, hid), dg, "gelu")
+        dh = ops.dwconv3x3(du.view(B, H, W, hid), b["taps_flip"], b["zero"]).view(B, N, hid)
+        dxn2 = ops.gemm(dh, b["w1T"])
+        d1 = ops.layernorm_bwd(sb["x1"], dxn2, b["g2"], BLOCK_EPS, dres=d)
+        do = ops.gemm(d1, b["wpT"], row_scale=sb["ma"], rows_per=N)
+        kv = sb["kv"]
+        Nk = kv.shape[1]
+        dkv32 = torch.zeros(B, Nk, 2 * C, device=self.dev, dtype=torch.float32)
+        dq = ops.attention_bwd(sb["q"], kv[:, :, :C], kv[:, :, C:], sb["o"], do, b["heads"], b["scale"],
+                               dkv32[:, :, :C], dkv32[:, :, C:])
+        dkv = ops.cast(dkv32, self.dt)
+        dxs = ops.gemm(dkv, b["wkvT"])
+        if b["sr"] > 1:
+            r = b["sr"]
+            dxs_pre = ops.layernorm_bwd(sb["xs_pre"], dxs, b["gn"], LN_EPS)
+            dpatch = ops.gemm(dxs_pre, b["wsrD"])
+            dxn1 = torch.empty(B, H, W, C, device=self.dev, dtype=self.dt)
+            ops.unpatchify(dpatch.view(-1, r * r * C), B, H // r, W // r, r, C, dxn1)
+            dxn1 = dxn1.view(B, N, C)
+            ops.gemm(dq, b["wqT"], residual=dxn1, out=dxn1)
+        else:
+            dxn1 = ops.gemm(dq, b["wqT"], residual=dxs)
+        return ops.layernorm_bwd(sb["xp"], dxn1, b["g1"], BLOCK_EPS, dres=d1)
+
+    def _cross_bwd(self, s, ca, dout):
+        p = f"cross_attn_s{s}"
+        E, heads = ca["E"], ca["heads"]
+        B = ca["c"].shape[0]
+        da = ops.layernorm_bwd(ca["a"], dout.reshape(ca["a"].shape), self.P(p + ".norm.weight"), LN_EPS,
+                               dgamma=self.G(p + ".norm.weight"), dbeta=self.G(p + ".norm.bias"))
+        op = p + ".cross_attn.out_proj"
+        self._wg(da, ca["o"], op + ".weight", op + ".bias")
+        do = ops.gemm(da, self.W(op + ".weight.T"))
+        kv = ca["kv"]
+        Nk = kv.shape[1]
+        dkv32 = torch.zeros(B, Nk, 2 * E, device=self.dev, dtype=torch.float32)
+        dq = ops.attention_bwd(ca["q"], kv[:, :, :E], kv[:, :, E:], ca["o"], do, heads, (E // heads) ** -0.5,
+                               dkv32[:, :, :E], dkv32[:, :, E:])
+        dkv = ops.cast(dkv32, self.dt)
+        ip = p + ".cross_attn.in_proj_weight"
+        gW, gb = self.G(ip), self.G(p + ".cross_attn.in_proj_bias")
+        ops.gemm_wgrad(dq.reshape(-1, E), ca["c"].reshape(-1, E), gW[:E])
+        ops.colstats(dq.reshape(-1, E), gb[:E])
+        ops.gemm_wgrad(dkv.reshape(-1, 2 * E), ca["f"].reshape(-1, E), gW[E:])
+        ops.colstats(dkv.reshape(-1, 2 * E), gb[E:])
+        dc = ops.gemm(dq, self.W(ip + ".qT"), residual=da)
+        df = ops.gemm(dkv, self.W(ip + ".kvT"))
+        return dc, df
+
+    def _flow_bwd(self, fl, dflow, B):
+        dy = None
+        for i in range(4, 0, -1):
+            L = fl[i - 1]
+            z = L["z"]
+            if i == 4:
+                dy = dflow[4].reshape(z.shape)
+            bn = f"flow_encoder.bn{i}"
+            dz = ops.bn_bwd(z, dy.reshape(z.shape).contiguous(), L["s1"], L["s2"], self.P(bn + ".weight"),
+                            self.P(bn + ".bias"), BN_EPS, self.G(bn + ".weight"), self.G(bn + ".bias"), relu=True)
+            nm = f"flow_encoder.conv{i}"
+            ops.conv2d_wgrad(L["inp"], dz, L["k"], L["st"], L["pad"], self.CG(nm + ".weight"))
+            ops.colstats(dz.view(-1, dz.shape[-1]), self.G(nm + ".bias"))
+            if i > 1:
+                pin = L["inp"]
+                res = dflow[3].reshape(pin.shape).contiguous() if i == 4 else None
+                dy = ops.conv2d_dgrad(dz, self.W(nm + ".weight.D"), pin.shape[1], pin.shape[2], pin.shape[3], L["k"],
+                                      L["st"], L["pad"], residual=res)
+
+    # ---- the step ---------------------------------------------------------------------------------
+    def forward_backward(self, x, y, flow, labels, ant_targets, masks=None):
+        """Zero grads, forward (train mode), loss, backward.  Returns (loss [2] f32 device tensor
+        = (CE sum, SmoothL1 sum), logits, anticipation)."""
+        B = x.numel() // (3 * 224 * 224)
+        if masks is None:
+            masks = self.make_masks(B)
+        else:
+            masks = {"blocks": [[(a.to(self.dev, torch.float32), b.to(self.dev, torch.float32)) for a, b in st]
+                                for st in masks["blocks"]],
+                     "dropout2d": masks["dropout2d"].to(self.dev, torch.float32).contiguous()}
+        self.grad.zero_()
+        self.conv_scratch.zero_()
+        if self.group is not None and self.world > 1:
+            self._broadcast_buffers()
+        sv, logits, ant = self._forward(x, y, flow, masks)
+        loss, dl, da = ops.phase_loss(logits, ant, labels, ant_targets)
+        self._backward(sv, dl, da)
+        self.untab.run(self.conv_scratch, self.grad)   # packed conv weight grads -> flat grad (f32 gather)
+        self._update_bn_running(sv)
+        return loss, logits, ant
+
+    def _update_bn_running(self, sv):
+        m = self.model
+        mods = [(m.head.linear_fuse.bn, sv["head"]["s1"], sv["head"]["s2"], sv["head"]["Z"].shape[0])]
+        for i, L in enumerate(sv["flow"], start=1):
+            mods.append((getattr(m.flow_encoder, f"bn{i}"), L["s1"], L["s2"], L["z"].numel() // L["z"].shape[-1]))
+        for bn, s1, s2, M in mods:
+            ops.bn_update_running(s1, s2, M, bn.running_mean, bn.running_var, BN_MOMENTUM)
+            bn.num_batches_tracked.add_(1)
+
+    def _broadcast_buffers(self):
+        import torch.distributed as dist
+        m = self.model
+        for bn in [m.head.linear_fuse.bn] + [getattr(m.flow_encoder, f"bn{i}") for i in range(1, 5)]:
+            dist.broadcast(bn.running_mean, 0, group=self.group)
+            dist.broadcast(bn.running_var, 0, group=self.group)
+
+    def allreduce_grads(self):
+        """DDP gradient averaging: one RCCL all-reduce over the flat f32 gradient buffer."""
+        if self.group is not None and self.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.grad, group=self.group)
+            self.grad.mul_(1.0 / self.world)
+
+    def optimizer_step(self):
+        h = self.hp
+        ops.sgd(self.flat, self.grad, self.mom, h["lr"], h["momentum"], h["dampening"], h["weight_decay"],
+                h["nesterov"], first=self.steps == 0)
+        self.steps += 1
+        self._refresh_packs()
+        # the kernel wrote the parameters behind autograd's back: bump their version counters so the
+        # eval-mode modules re-derive their cached packs (svk.pack.PackCache)
+        for p in self.params.values():
+            increment_version(p)
+
+    def step(self, x, y, flow, labels, ant_targets, masks=None):
+        """One train_model iteration (train_evp.py:473-515): returns (loss [2], logits, anticipation)."""
+        loss, logits, ant = self.forward_backward(x, y, flow, labels, ant_targets, masks)
+        self.allreduce_grads()
+        self.optimizer_step()
+        return loss, logits, ant

@@ -122,6 +122,107 @@ int svk_add_bcast(int dtype, const void* X, const float* P, void* Y, long M, int
 /* Elementwise dtype conversion (n elements). */
 int svk_cast(int dtype_in, const void* X, int dtype_out, void* Y, long n, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Training step (train_evp.py:473-515): the frozen-backbone step differentiates through every
+ * backbone block (prompts are injected at each block) and produces f32 gradients for the
+ * trainable modules (head, prompt_generator, flow_encoder, cross_attn_s3/s4, :379-382).
+ * Activation gradients are in the compute dtype; parameter gradients, statistics and optimizer
+ * state are f32.  Gradient outputs marked "+=" accumulate (f32 atomics): the caller zeroes them.
+ * ------------------------------------------------------------------------------------------- */
+
+/* svk_dwconv3x3 that also stores the pre-activation map (Ypre, may be NULL) for the GELU backward. */
+int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const float* bias, void* Y, void* Ypre, int B,
+                     int H, int W, int C, int act, void* stream);
+
+/* svk_gemm plus a per-row scale s[m / rows_per_scale] applied to act(A W^T + bias) before the
+ * residual add: timm DropPath (stochastic depth, mix_transformer_evp.py:168-169 in train mode)
+ * fused into the branch GEMM, and its adjoint in the data-gradient GEMM. */
+int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
+                const float* row_scale, int rows_per_scale, const void* R, long ldr, void* C, long ldc,
+                int M, int N, int K, int act, void* stream);
+
+/* dW[n, k] += sum_m dY[m, n] * X[m, k] (f32, split-M MFMA with atomics): nn.Linear weight gradient. */
+int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw,
+                   int M, int N, int K, void* stream);
+
+/* Conv2d weight gradient: dW[Cout][kh][kw][Cin] (packed like the forward weights) += im2col(X)^T dY. */
+int svk_conv2d_wgrad_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* dY,
+                          int Cout, int k, int stride, int pad, float* dW, void* stream);
+
+/* Conv2d data gradient (transposed-conv gather, power-of-two stride): dX [B,H,W,Cin] = col2im(dY) .
+ * Wd packed [Cin][kh][kw][Cout]; optional R is added (R may alias dX). */
+int svk_conv2d_dgrad_nhwc(int dtype, const void* dY, int B, int OH, int OW, int Cout, const void* Wd,
+                          const void* R, void* dX, int H, int W, int Cin, int k, int stride, int pad,
+                          void* stream);
+
+/* [B*PH*PW, s*s*C] patch rows -> NHWC [B, PH*s, PW*s, C] (adjoint of the k = s patchify conv's im2col;
+ * accumulate != 0 adds into Y). */
+int svk_unpatchify(int dtype, const void* P, void* Y, int B, int PH, int PW, int s, int C, int accumulate,
+                   void* stream);
+
+/* Scaled-dot-product attention backward (recomputes P): dQ written, dK/dV (f32 [B, Nk, heads*hd]
+ * with row stride lddk, batch stride sbdk) accumulated.  hd <= 64, Nk limited by LDS (<= ~200). */
+int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, const void* K, long ldk, long sbk,
+                      const void* V, long ldv, long sbv, const void* O, long ldo, long sbo,
+                      const void* dO, long lddo, long sbdo, void* dQ, long lddq, long sbdq, float* dK,
+                      float* dV, long lddk, long sbdk, int B, int Nq, int Nk, int heads, int hd, float scale,
+                      void* stream);
+
+/* LayerNorm backward (recomputes mean/rstd from X): dX = LN'(dY) (+ dR); dgamma/dbeta += (both or
+ * neither; NULL for frozen norms).  C <= 512. */
+int svk_layernorm_bwd(int dtype, const void* X, long ldx, const void* dY, long ldy, const float* gamma,
+                      const void* dR, long ldr, void* dX, long lddx, float* dgamma, float* dbeta, int M, int C,
+                      float eps, void* stream);
+
+/* dX = dY * act'(U) (+ dR), elementwise over n (GELU erf / ReLU / tanh). */
+int svk_act_bwd(int dtype, const void* U, const void* dY, const void* dR, void* dX, long n, int act, void* stream);
+
+/* Column sums (and sums of squares, optional) over M rows, += into f32 sum/sumsq: batch statistics
+ * and bias gradients. */
+int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, void* stream);
+
+/* BatchNorm2d train mode on [M = B*H*W, C]: Y = act((X - mean) rsqrt(var + eps) g + b) from colstats
+ * sums (biased variance), and its backward with the optional ReLU recomputed from X (dgamma/dbeta +=). */
+int svk_bn_apply(int dtype, const void* X, const float* sum, const float* sumsq, const float* gamma,
+                 const float* beta, void* Y, int M, int C, float eps, int act, void* stream);
+int svk_bn_bwd(int dtype, const void* X, const void* dY, const float* sum, const float* sumsq,
+               const float* gamma, const float* beta, void* dX, float* dgamma, float* dbeta, int M, int C,
+               float eps, int relu, void* stream);
+/* running_mean/var momentum update (unbiased variance), as nn.BatchNorm2d does in train mode. */
+int svk_bn_update_running(const float* sum, const float* sumsq, int M, int C, float momentum,
+                          float* running_mean, float* running_var, void* stream);
+
+/* Adjoint of svk_resize_bilinear: dX (f32 [B, H*W, C], +=) from dY [B, OH*OW, C] (row stride ldy). */
+int svk_resize_bilinear_bwd(int dtype, const void* dY, long ldy, float* dX, int B, int H, int W, int C,
+                            int OH, int OW, void* stream);
+
+/* Adjoint of svk_mean_rows (+ Dropout2d mask): dY[b*R + r, c] = dF[b, c] * mask[b, c] * scale. */
+int svk_bcast_rows(int dtype, const float* dF, const float* mask, float scale, void* dY, int B, int R, int C,
+                   void* stream);
+
+/* Y[r, c] = X[r, c] * s[r / rows_per]; y = a * b (f32). */
+int svk_row_scale(int dtype, const void* X, const float* s, void* Y, long M, int C, int rows_per, void* stream);
+int svk_mul_f32(const float* a, const float* b, float* y, long n, void* stream);
+
+/* Counter-based Bernoulli(keep) mask scaled by 1/keep (values 0 or 1/keep): DropPath / Dropout2d. */
+int svk_keep_mask(float* out, long n, float keep, unsigned seed, void* stream);
+
+/* CrossEntropyLoss(sum) + SmoothL1Loss(sum) (train_evp.py:390-391, 500-509): loss[0] += CE,
+ * loss[1] += SmoothL1; dlogits / dant are the gradients of their sum. */
+int svk_phase_loss(const float* logits, const float* ant, const long* labels, const float* ant_targets, int B,
+                   int K, float* loss, float* dlogits, float* dant, void* stream);
+
+/* torch.optim.SGD step (momentum, dampening, weight decay, nesterov; train_evp.py:405-419) over a
+ * flat f32 parameter buffer; first != 0 initialises the momentum buffer. */
+int svk_sgd(float* p, const float* grad, float* buf, long n, float lr, float momentum, float dampening,
+            float wd, int nesterov, int first, void* stream);
+
+/* Batched strided gather f32 master parameters -> packed compute-dtype views (one launch refreshes
+ * all forward/transposed packs after an optimizer step).  desc: device array of
+ * {long src, dst; int n[4]; long s[4]; int lim[4]; long start} (see csrc/train.hip PackDesc). */
+int svk_pack_params(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

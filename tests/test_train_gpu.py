@@ -1,0 +1,337 @@
+"""Training-step parity on the GPU (§8 a13): each backward kernel against torch autograd (f32 on the
+CPU, same seeded inputs), then the whole frozen-backbone step (svk.train.EVPTrainStep) against the
+oracle's autograd restatement (oracle/train_evp.py) with identical DropPath / Dropout2d masks.
+
+Tolerances: f32 kernels 1e-4..1e-3 relative to the tensor's max magnitude (atomics reorder sums);
+full f32 step: every trainable gradient within 2e-3 of max|g| of the fp64 oracle, losses within
+1e-4 relative; bf16 step: per-tensor cosine similarity >= 0.99 against the oracle (bf16 is the
+throughput dtype; the reference itself trains under fp16 autocast).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import inputs as I, params as P, train_evp as TR
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    scale = max(b.abs().max().item(), 1e-6)
+    err = (a - b).abs().max().item()
+    assert err <= tol * scale, f"max err {err:.3e} > {tol} * {scale:.3e}"
+
+
+def _rand(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g) * scale
+
+
+@pytest.mark.parametrize("M,C", [(300, 64), (77, 320), (49, 512)])
+def test_layernorm_bwd(cuda, M, C):
+    from svk import ops
+    x, dy, r = _rand(M, C, seed=1), _rand(M, C, seed=2), _rand(M, C, seed=3)
+    g, b = 1 + 0.1 * _rand(C, seed=4), 0.1 * _rand(C, seed=5)
+    xr = x.clone().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    F.layer_norm(xr, (C,), gr, br, 1e-6).backward(dy)
+    dg = torch.zeros(C, device=cuda)
+    db = torch.zeros(C, device=cuda)
+    dx = ops.layernorm_bwd(x.to(cuda), dy.to(cuda), g.to(cuda), 1e-6, dres=r.to(cuda), dgamma=dg, dbeta=db)
+    _close(dx, xr.grad + r, 1e-4)
+    _close(dg, gr.grad, 1e-4)
+    _close(db, br.grad, 1e-4)
+
+
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+def test_act_bwd(cuda, act):
+    from svk import ops
+    u, dy = _rand(1000, seed=1), _rand(1000, seed=2)
+    ur = u.clone().requires_grad_(True)
+    (F.gelu(ur) if act == "gelu" else F.relu(ur)).backward(dy)
+    _close(ops.act_bwd(u.to(cuda), dy.to(cuda), act), ur.grad, 1e-5)
+
+
+@pytest.mark.parametrize("M,C", [(88 * 49, 2048), (1000, 64)])
+def test_batchnorm_train_fwd_bwd(cuda, M, C):
+    from svk import ops
+    x, dy = _rand(M, C, seed=1), _rand(M, C, seed=2)
+    g, b = 1 + 0.1 * _rand(C, seed=3), 0.1 * _rand(C, seed=4)
+    xr = x.clone().requires_grad_(True)
+    gr, br = g.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    y = F.relu(F.batch_norm(xr, None, None, gr, br, True, 0.1, 1e-5))
+    y.backward(dy)
+    xc = x.to(cuda)
+    s1, s2 = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    ops.colstats(xc, s1, s2)
+    yc = ops.bn_apply(xc, s1, s2, g.to(cuda), b.to(cuda), 1e-5, act="relu")
+    _close(yc, y, 1e-4)
+    dg, db = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    dx = ops.bn_bwd(xc, dy.to(cuda), s1, s2, g.to(cuda), b.to(cuda), 1e-5, dg, db, relu=True)
+    _close(dx, xr.grad, 1e-3)
+    _close(dg, gr.grad, 1e-3)
+    _close(db, br.grad, 1e-3)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    ops.bn_update_running(s1, s2, M, rm, rv, 0.1)
+    _close(rm, 0.1 * x.mean(0), 1e-4)
+    _close(rv, 0.9 + 0.1 * x.var(0, unbiased=True), 1e-4)
+
+
+@pytest.mark.parametrize("H,W", [(56, 56), (28, 28), (14, 14)])
+def test_resize_bilinear_bwd(cuda, H, W):
+    from svk import ops
+    B, C = 2, 24
+    x = _rand(B, C, H, W, seed=1).requires_grad_(True)
+    dy = _rand(B, C, 7, 7, seed=2)
+    F.interpolate(x, (7, 7), mode="bilinear", align_corners=False).backward(dy)
+    dyt = dy.permute(0, 2, 3, 1).reshape(B, 49, C).contiguous().to(cuda)
+    dx = torch.zeros(B, H * W, C, device=cuda)
+    ops.resize_bilinear_bwd(dyt, H, W, 7, 7, dx)
+    _close(dx, x.grad.permute(0, 2, 3, 1).reshape(B, H * W, C), 1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(1000, 64, 256), (4312, 2048, 512), (37, 7, 512), (500, 48, 40)])
+def test_gemm_wgrad(cuda, dt, M, N, K):
+    from svk import ops
+    dy, x = _rand(M, N, seed=1), _rand(M, K, seed=2)
+    dw = torch.full((N, K), 0.5, device=cuda)
+    ops.gemm_wgrad(dy.to(cuda, dt), x.to(cuda, dt), dw)
+    ref = dy.to(dt).double().t() @ x.to(dt).double() + 0.5
+    _close(dw, ref, 1e-5 if dt == torch.float32 else 1e-2)
+
+
+def _conv_case(B, Cin, H, Cout, k, s, seed):
+    x = _rand(B, Cin, H, H, seed=seed)
+    w = _rand(Cout, Cin, k, k, seed=seed + 1, scale=0.1)
+    return x, w
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,Cin,H,Cout,k,s", [(2, 16, 56, 32, 3, 2), (2, 64, 56, 128, 3, 2), (2, 3, 224, 16, 7, 4),
+                                              (3, 128, 28, 320, 3, 2)])
+def test_conv_wgrad_dgrad(cuda, dt, B, Cin, H, Cout, k, s):
+    from svk import ops
+    from svk.pack import pad_channels
+    x, w = _conv_case(B, Cin, H, Cout, k, s, 3)
+    xr, wr = x.to(dt).double().requires_grad_(True), w.to(dt).double().requires_grad_(True)
+    y = F.conv2d(xr, wr, stride=s, padding=k // 2)
+    dy = _rand(*y.shape, seed=9).to(dt).double()
+    y.backward(dy)
+    cp = pad_channels(Cin)
+    xn = ops.nchw_to_nhwc(x.to(cuda), dt, cpad=cp)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    dwp = torch.zeros(Cout, k * k * cp, device=cuda)
+    ops.conv2d_wgrad(xn, dyn, k, s, k // 2, dwp)
+    dw = dwp.view(Cout, k, k, cp)[..., :Cin].permute(0, 3, 1, 2)
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    _close(dw, wr.grad, tol)
+    if Cin >= 8:
+        wd = w.permute(1, 2, 3, 0).reshape(Cin, k * k * Cout).to(cuda, dt).contiguous()
+        res = _rand(B, H, H, Cin, seed=11).to(cuda, dt)
+        dx = ops.conv2d_dgrad(dyn, wd, H, H, Cin, k, s, k // 2, residual=res)
+        _close(dx, xr.grad.permute(0, 2, 3, 1) + res.double().cpu(), tol)
+
+
+def test_patchify_adjoint(cuda):
+    """sr-conv data gradient: GEMM with the (i, j, ci) x co packed weight + unpatchify."""
+    from svk import ops
+    B, C, H, r = 2, 64, 56, 8
+    x = _rand(B, C, H, H, seed=1).double().requires_grad_(True)
+    w = _rand(C, C, r, r, seed=2, scale=0.05).double()
+    y = F.conv2d(x, w, stride=r)
+    dy = _rand(*y.shape, seed=3).double()
+    y.backward(dy)
+    wd = w.permute(2, 3, 1, 0).reshape(r * r * C, C).float().to(cuda)
+    dp = ops.gemm(dy.permute(0, 2, 3, 1).reshape(-1, C).float().to(cuda), wd)
+    dx = torch.empty(B, H, H, C, device=cuda)
+    ops.unpatchify(dp, B, H // r, H // r, r, C, dx)
+    _close(dx, x.grad.permute(0, 2, 3, 1), 1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("Nq,Nk,heads,hd", [(3136, 49, 1, 64), (196, 196, 8, 40), (49, 49, 8, 64), (100, 30, 2, 16)])
+def test_attention_bwd(cuda, dt, Nq, Nk, heads, hd):
+    from svk import ops
+    B, C = 2, heads * hd
+    q, k, v = _rand(B, Nq, C, seed=1), _rand(B, Nk, C, seed=2), _rand(B, Nk, C, seed=3)
+    do = _rand(B, Nq, C, seed=4)
+    scale = hd ** -0.5
+    qr, kr, vr = (t.to(dt).double().requires_grad_(True) for t in (q, k, v))
+    sp = lambda t, n: t.reshape(B, n, heads, hd).transpose(1, 2)
+    a = (sp(qr, Nq) @ sp(kr, Nk).transpose(-1, -2) * scale).softmax(-1)
+    o = (a @ sp(vr, Nk)).transpose(1, 2).reshape(B, Nq, C)
+    o.backward(do.to(dt).double())
+    qc, kc, vc = (t.to(cuda, dt) for t in (q, k, v))
+    oc = ops.attention(qc, kc, vc, heads, scale)
+    dkv = torch.zeros(B, Nk, 2 * C, device=cuda)
+    dq = ops.attention_bwd(qc, kc, vc, oc, do.to(cuda, dt), heads, scale, dkv[:, :, :C], dkv[:, :, C:])
+    tol = 1e-4 if dt == torch.float32 else 3e-2
+    _close(dq, qr.grad, tol)
+    _close(dkv[:, :, :C], kr.grad, tol)
+    _close(dkv[:, :, C:], vr.grad, tol)
+
+
+def test_phase_loss_and_sgd(cuda):
+    from svk import ops
+    B = 88
+    z, a = _rand(B, 7, seed=1, scale=3), _rand(B, 7, seed=2, scale=2)
+    lab = torch.randint(0, 7, (B,), generator=torch.Generator().manual_seed(3))
+    at = torch.rand(B, 7, generator=torch.Generator().manual_seed(4))
+    zr, ar = z.clone().requires_grad_(True), a.clone().requires_grad_(True)
+    lp = F.cross_entropy(zr, lab, reduction="sum")
+    la = F.smooth_l1_loss(ar, at, reduction="sum")
+    (lp + la).backward()
+    loss, dl, da = ops.phase_loss(z.to(cuda), a.to(cuda), lab.to(cuda), at.to(cuda))
+    _close(loss, torch.stack([lp, la]), 1e-5)
+    _close(dl, zr.grad, 1e-5)
+    _close(da, ar.grad, 1e-5)
+    # SGD: two steps against torch.optim.SGD
+    p0, g1, g2 = _rand(1000, seed=5), _rand(1000, seed=6), _rand(1000, seed=7)
+    pt = p0.clone().requires_grad_(True)
+    opt = torch.optim.SGD([pt], lr=5e-4, momentum=0.9, dampening=0.0, weight_decay=1e-5, nesterov=False)
+    pc, buf = p0.to(cuda), torch.zeros(1000, device=cuda)
+    for i, g in enumerate((g1, g2)):
+        pt.grad = g.clone()
+        opt.step()
+        ops.sgd(pc, g.to(cuda), buf, 5e-4, 0.9, 0.0, 1e-5, False, first=i == 0)
+    _close(pc, pt.detach(), 1e-6)
+
+
+def test_gemm_row_scale_and_dwconv_pre(cuda):
+    from svk import ops
+    B, N, K, C = 4, 49, 64, 32
+    a, w, r = _rand(B * N, K, seed=1), _rand(C, K, seed=2, scale=0.1), _rand(B * N, C, seed=3)
+    s = torch.tensor([0.0, 1.25, 1.25, 0.0])
+    out = ops.gemm(a.to(cuda), w.to(cuda), residual=r.to(cuda), row_scale=s.to(cuda), rows_per=N)
+    ref = (a @ w.t()) * s.repeat_interleave(N)[:, None] + r
+    _close(out, ref, 1e-5)
+    x = _rand(2, 7, 7, 64, seed=4).to(cuda)
+    taps, bias = _rand(9, 64, seed=5).to(cuda), _rand(64, seed=6).to(cuda)
+    pre = torch.empty_like(x)
+    y = ops.dwconv3x3(x, taps, bias, act="gelu", pre_out=pre)
+    _close(pre, ops.dwconv3x3(x, taps, bias), 1e-6)
+    _close(y, F.gelu(pre), 1e-5)
+
+
+def test_pack_params_gather(cuda):
+    """Batched gather: transposes and conv repacks with channel padding."""
+    import numpy as np
+    from svk.train import _PackTable
+    w1 = _rand(5, 3, seed=1)
+    w2 = _rand(16, 3, 7, 7, seed=2)
+    flat = torch.cat([w1.reshape(-1), w2.reshape(-1)]).to(cuda)
+    t = _PackTable(torch.float32)
+    i1 = t.add(0, (3, 5), (1, 3))
+    i2 = t.add(15, (16, 7, 7, 8), (3 * 49, 7, 1, 49), (16, 7, 7, 3))
+    t.finalize(cuda)
+    t.run(flat)
+    _close(t.tensors[i1], w1.t(), 0)
+    ref = F.pad(w2.permute(0, 2, 3, 1), (0, 5))
+    _close(t.tensors[i2], ref, 0)
+
+
+# ---- the full step --------------------------------------------------------------------------------
+
+def _train_inputs(B, seed):
+    g = torch.Generator().manual_seed(seed + 100)
+    return (I.frames(B, seed), I.segmaps(B, seed), I.flow(B, seed), torch.randint(0, 7, (B,), generator=g),
+            torch.rand(B, 7, generator=g))
+
+
+def _build(variant, cuda, dtype, seed=0):
+    from models import mix_transformer_evp as mte
+    from svk.train import EVPTrainStep
+    m = getattr(mte, variant)()
+    sd = P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, seed)
+    m.load_state_dict(sd)
+    m = m.to(cuda)
+    return m, sd, EVPTrainStep(m, dtype=dtype)
+
+
+@pytest.mark.parametrize("variant", ["mit_b0_evp", "mit_b2_evp"])
+def test_train_step_grads_fp32_vs_oracle(cuda, variant):
+    B = 3
+    m, sd, tr = _build(variant, cuda, torch.float32)
+    x, y, fl, lab, at = _train_inputs(B, 1)
+    masks = TR.make_masks(B, variant, seed=5)
+    # make sure the draw actually drops something (stochastic depth and Dropout2d both exercised)
+    assert any((a == 0).any() or (b == 0).any() for st in masks["blocks"] for a, b in st)
+    lp, la, grads, stats = TR.loss_and_grads(x, y, fl, lab, at, sd, variant, masks)
+    loss, logits, ant = tr.forward_backward(x.to(cuda), y.to(cuda), fl.to(cuda), lab.to(cuda), at.to(cuda),
+                                            masks=masks)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss.cpu().numpy(), [lp.item(), la.item()], rtol=1e-4)
+    names = sorted(grads)
+    assert set(names) == set(tr.params), "trainable set differs from train_evp.py:379-382"
+    for n in names:
+        _close(tr.params[n].grad, grads[n], 2e-3)
+    for prefix, (mean, var) in stats.items():
+        bn = m.get_submodule(prefix)
+        _close(bn.running_mean, 0.9 * sd[prefix + ".running_mean"] + 0.1 * mean, 1e-4)
+        _close(bn.running_var, 0.9 * sd[prefix + ".running_var"] + 0.1 * var, 1e-4)
+
+
+def test_train_step_sgd_update_and_eval_repack(cuda):
+    """step() = forward_backward + SGD: parameters move exactly as torch.optim.SGD would move them
+    with the same gradients, and the eval-mode forward sees the updated weights."""
+    variant = "mit_b0_evp"
+    B = 2
+    m, sd, tr = _build(variant, cuda, torch.float32)
+    x, y, fl, lab, at = _train_inputs(B, 2)
+    masks = TR.make_masks(B, variant, seed=1, enabled=False)
+    before = {n: p.detach().double().cpu().clone() for n, p in tr.params.items()}
+    tr.step(x.to(cuda), y.to(cuda), fl.to(cuda), lab.to(cuda), at.to(cuda), masks=masks)
+    torch.cuda.synchronize()
+    grads = {n: p.grad.detach().double().cpu() for n, p in tr.params.items()}
+    expect, _ = TR.sgd_step(before, grads)
+    for n, p in tr.params.items():
+        _close(p.detach(), expect[n], 1e-6)
+    # eval forward after the step uses the new weights (pack caches invalidated)
+    m.eval()
+    with torch.no_grad():
+        out = m(x.to(cuda), y.to(cuda), fl.to(cuda), return_features=True)
+    from oracle import mit_evp as M
+    sd2 = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+    ref = M.forward(x, y, sd2, variant, fl, return_features=True)
+    _close(out, ref, 1e-3)
+
+
+def test_train_step_bf16_b2_cosine(cuda):
+    variant = "mit_b2_evp"
+    B = 4
+    m, sd, tr = _build(variant, cuda, torch.bfloat16)
+    x, y, fl, lab, at = _train_inputs(B, 3)
+    masks = TR.make_masks(B, variant, seed=7)
+    lp, la, grads, _ = TR.loss_and_grads(x, y, fl, lab, at, sd, variant, masks)
+    loss, _, _ = tr.forward_backward(x.to(cuda), y.to(cuda), fl.to(cuda), lab.to(cuda), at.to(cuda), masks=masks)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss.cpu().numpy(), [lp.item(), la.item()], rtol=3e-2)
+    worst = 1.0
+    for n, g in grads.items():
+        a = tr.params[n].grad.detach().double().cpu().reshape(-1)
+        b = g.reshape(-1)
+        if b.norm() < 1e-12:
+            continue
+        cos = (a @ b / (a.norm() * b.norm() + 1e-30)).item()
+        worst = min(worst, cos)
+        assert cos >= 0.99, f"{n}: cosine {cos:.4f}"
+    assert worst >= 0.99
+
+
+def test_train_loss_decreases(cuda):
+    """Several SGD steps on one fixed batch (device masks, stochastic depth on) reduce the loss."""
+    variant = "mit_b0_evp"
+    B = 8
+    m, sd, tr = _build(variant, cuda, torch.bfloat16)
+    tr.hp["lr"] = 2e-3
+    x, y, fl, lab, at = (t.to(cuda) for t in _train_inputs(B, 4))
+    losses = []
+    for _ in range(6):
+        loss, _, _ = tr.step(x, y, fl, lab, at)
+        losses.append(loss.sum().item())
+    assert all(np.isfinite(losses))
+    assert losses[-1] < losses[0], losses
