@@ -54,7 +54,7 @@ class _PackTable:
         self.total = 0
         self.views = []
 
-    def add(self, src, shape, strides, lims=None):
+    def add(self, src, shape, strides, lims=None, view=None):
         n = [1] * (4 - len(shape)) + list(shape)
         s = [0] * (4 - len(strides)) + list(strides)
         lim = [1] * (4 - len(shape)) + list(lims if lims is not None else shape)
@@ -62,7 +62,7 @@ class _PackTable:
         off = self.total
         self.rows.append((src, off, n, s, lim, off))
         self.total += (numel + 7) // 8 * 8      # keep every packed tensor 16-byte aligned
-        self.views.append((off, tuple(shape)))
+        self.views.append((off, tuple(view or shape)))
         return len(self.views) - 1
 
     def finalize(self, device):
@@ -162,9 +162,9 @@ class EVPTrainStep:
             co, ci, k, _ = self.params[name].shape
             o = self.off[name]
             cp = pad_channels(ci) if pad_in else ci
-            self.pk[name] = tab.add(o, (co, k, k, cp), (ci * k * k, k, 1, k * k), (co, k, k, ci))
+            self.pk[name] = tab.add(o, (co, k, k, cp), (ci * k * k, k, 1, k * k), (co, k, k, ci), view=(co, k * k * cp))
             if dgrad:
-                self.pk[name + ".D"] = tab.add(o, (ci, k, k, co), (k * k, k, 1, ci * k * k))
+                self.pk[name + ".D"] = tab.add(o, (ci, k, k, co), (k * k, k, 1, ci * k * k), view=(ci, k * k * co))
             # weight-gradient scratch in the packed layout, unpacked into the flat grad after backward
             n = co * k * k * cp
             self.conv_grad[name] = (conv_scratch, (co, k * k * cp))
