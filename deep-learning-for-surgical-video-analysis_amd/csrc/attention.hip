@@ -380,30 +380,268 @@ __global__ __launch_bounds__(256) void attention_bwd_kernel(const T* __restrict_
 }
 }  // namespace svk
 
+
+// ---- MFMA attention backward (bf16): dQ, and P / dS for the key/value reductions ----------------
+// One workgroup per (frame, head, 64 queries); wave w owns queries q0 + 16w .. +15.  Keys are padded
+// to NKC x 64 (masked).  Per wave, with 16x16x32 bf16 MFMAs (C layout: col = key (lane & 15),
+// row = query 4 (lane >> 4) + r):
+//   S = Q K^T, dP = dO V^T (K, V staged in LDS [key][d]); row max / sum over keys by 16-lane
+//   xor-shuffles; P = softmax(scale S); dS' = scale P (dP - D), D = rowsum(dO * O);
+//   dQ = dS' K  (dS' goes through LDS once to become an A operand; K^T staged in LDS).
+// P and dS' are written (bf16, rows padded to NKC x 64 with zeros) to the workspace; dK = dS'^T Q
+// and dV = P^T dO are then batched MFMA reductions over the queries (wgrad_batched).
+namespace svk {
+template <int HDP, int NKC>
+__global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16* __restrict__ Q, long ldq, long sbq,
+                                                        const bf16* __restrict__ K, long ldk, long sbk,
+                                                        const bf16* __restrict__ V, long ldv, long sbv,
+                                                        const bf16* __restrict__ O, long ldo, long sbo,
+                                                        const bf16* __restrict__ dO, long lddo, long sbdo,
+                                                        bf16* __restrict__ dQ, long lddq, long sbdq,
+                                                        bf16* __restrict__ Pws, bf16* __restrict__ dSws, int Nq,
+                                                        int Nk, int hd, float scale) {
+  constexpr int NKP = NKC * 64;
+  constexpr int LDK = HDP + 8;
+  constexpr int LDT = NKP + 8;
+  __shared__ __attribute__((aligned(16))) bf16 sK[NKP][LDK];
+  __shared__ __attribute__((aligned(16))) bf16 sV[NKP][LDK];
+  __shared__ __attribute__((aligned(16))) bf16 sKt[HDP][LDT];
+  __shared__ __attribute__((aligned(16))) bf16 sdS[4][16][LDT];
+  __shared__ float sD[64];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int q0 = blockIdx.x * 64, h = blockIdx.y, b = blockIdx.z, heads = gridDim.y;
+  const long co = (long)h * hd;
+  const bf16 zero = (bf16)0.f;
+  // stage K, V, K^T (zero past Nk / hd)
+  constexpr int CPR = HDP / 8;
+  for (int idx = tid; idx < NKP * CPR; idx += 256) {
+    const int key = idx / CPR, c8 = (idx - key * CPR) * 8;
+    bf16x8 kv, vv;
+    if (key < Nk && c8 < hd) {
+      kv = *reinterpret_cast<const bf16x8*>(K + b * sbk + (long)key * ldk + co + c8);
+      vv = *reinterpret_cast<const bf16x8*>(V + b * sbv + (long)key * ldv + co + c8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { kv[e] = zero; vv[e] = zero; }
+    }
+    *reinterpret_cast<bf16x8*>(&sK[key][c8]) = kv;
+    *reinterpret_cast<bf16x8*>(&sV[key][c8]) = vv;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sKt[c8 + e][key] = kv[e];
+  }
+  if (tid < 64) {
+    const int q = q0 + tid;
+    float acc = 0.f;
+    if (q < Nq) {
+      const bf16* o = O + b * sbo + (long)q * ldo + co;
+      const bf16* g = dO + b * sbdo + (long)q * lddo + co;
+      for (int d = 0; d < hd; d += 8) {
+        const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + d);
+        const bf16x8 gv = *reinterpret_cast<const bf16x8*>(g + d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc += (float)ov[e] * (float)gv[e];
+      }
+    }
+    sD[tid] = acc;
+  }
+  // A operands: Q and dO rows of this wave (row = lane & 15, k = 8 (lane >> 4) + j per 32-wide step)
+  const int fr = lane & 15, fg = lane >> 4;
+  const int qa = q0 + w * 16 + fr;
+  bf16x8 aq[HDP / 32], ag[HDP / 32];
+#pragma unroll
+  for (int ks = 0; ks < HDP / 32; ++ks) {
+    const int c = ks * 32 + fg * 8;
+    if (qa < Nq && c < hd) {
+      aq[ks] = *reinterpret_cast<const bf16x8*>(Q + b * sbq + (long)qa * ldq + co + c);
+      ag[ks] = *reinterpret_cast<const bf16x8*>(dO + b * sbdo + (long)qa * lddo + co + c);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { aq[ks][e] = zero; ag[ks][e] = zero; }
+    }
+  }
+  __syncthreads();
+  f32x4 S[NKC * 4], dP[NKC * 4];
+#pragma unroll
+  for (int t = 0; t < NKC * 4; ++t) {
+    S[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dP[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < HDP / 32; ++ks) {
+      const bf16x8 bk = *reinterpret_cast<const bf16x8*>(&sK[t * 16 + fr][ks * 32 + fg * 8]);
+      const bf16x8 bv = *reinterpret_cast<const bf16x8*>(&sV[t * 16 + fr][ks * 32 + fg * 8]);
+      S[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aq[ks], bk, S[t], 0, 0, 0);
+      dP[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ag[ks], bv, dP[t], 0, 0, 0);
+    }
+  }
+  // softmax over keys for the 4 query rows this lane holds
+  const float sl2 = scale * 1.4426950408889634f;
+  float mx[4], inv[4], Dq[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < NKC * 4; ++t) {
+      const int key = t * 16 + fr;
+      if (key < Nk) m = fmaxf(m, S[t][r]);
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int t = 0; t < NKC * 4; ++t) {
+      const int key = t * 16 + fr;
+      const float p = key < Nk ? exp2f((S[t][r] - m) * sl2) : 0.f;
+      S[t][r] = p;
+      l += p;
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) l += __shfl_xor(l, o, 64);
+    mx[r] = m;
+    inv[r] = 1.f / l;
+    Dq[r] = sD[w * 16 + fg * 4 + r];
+  }
+  (void)mx;
+  // P, dS' -> workspace (rows of this wave) and dS' -> LDS
+  const long zrow = ((long)b * heads + h) * Nq;
+#pragma unroll
+  for (int t = 0; t < NKC * 4; ++t) {
+    const int key = t * 16 + fr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qr = w * 16 + fg * 4 + r;
+      const float p = S[t][r] * inv[r];
+      const float ds = scale * p * (dP[t][r] - Dq[r]);
+      const bf16 dsb = (bf16)ds;
+      sdS[w][fg * 4 + r][key] = dsb;
+      if (q0 + qr < Nq) {
+        const long off = (zrow + q0 + qr) * NKP + key;
+        Pws[off] = (bf16)p;
+        dSws[off] = dsb;
+      }
+    }
+  }
+  __syncthreads();
+  // dQ = dS' K: A = dS' rows (LDS), B = K (k = keys, n = d) from sKt
+#pragma unroll
+  for (int nt = 0; nt < HDP / 16; ++nt) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < NKP / 32; ++kk) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sdS[w][fr][kk * 32 + fg * 8]);
+      const bf16x8 bb = *reinterpret_cast<const bf16x8*>(&sKt[nt * 16 + fr][kk * 32 + fg * 8]);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bb, acc, 0, 0, 0);
+    }
+    const int d = nt * 16 + fr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + w * 16 + fg * 4 + r;
+      if (q < Nq && d < hd) dQ[b * sbdq + (long)q * lddq + co + d] = (bf16)acc[r];
+    }
+  }
+}
+
+template <typename T>
+__global__ void store_kv_kernel(const float* __restrict__ acc, T* __restrict__ dK, T* __restrict__ dV, long lddk,
+                                long sbdk, int B, int Nk, int C) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * Nk * C) return;
+  const int c = (int)(i % C);
+  const long t = i / C;
+  const int j = (int)(t % Nk);
+  const int b = (int)(t / Nk);
+  const long n = (long)B * Nk * C;
+  dK[b * sbdk + (long)j * lddk + c] = from_f<T>(acc[i]);
+  dV[b * sbdk + (long)j * lddk + c] = from_f<T>(acc[n + i]);
+}
+}  // namespace svk
+
+static bool attn_bwd_mfma_ok(int dtype, int Nk, int hd) {
+  return dtype == SVK_BF16 && hd % 8 == 0 && hd <= 64 && Nk <= 256;
+}
+
+static bool al16(const void* p, long ld, long sb) { return ((uintptr_t)p & 15) == 0 && ld % 8 == 0 && sb % 8 == 0; }
+
+extern "C" long svk_attention_bwd_workspace(int dtype, int B, int Nq, int Nk, int heads, int hd) {
+  const long acc = 2L * B * Nk * heads * hd * 4;
+  if (!attn_bwd_mfma_ok(dtype, Nk, hd)) return acc;
+  const long nkp = (Nk + 63) / 64 * 64;
+  return acc + 2L * B * heads * Nq * nkp * 2;
+}
+
 extern "C" int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, const void* K, long ldk, long sbk,
                                  const void* V, long ldv, long sbv, const void* O, long ldo, long sbo,
-                                 const void* dO, long lddo, long sbdo, void* dQ, long lddq, long sbdq, float* dK,
-                                 float* dV, long lddk, long sbdk, int B, int Nq, int Nk, int heads, int hd,
-                                 float scale, void* stream) {
+                                 const void* dO, long lddo, long sbdo, void* dQ, long lddq, long sbdq, void* dK,
+                                 void* dV, long lddk, long sbdk, void* ws, long ws_bytes, int B, int Nq, int Nk,
+                                 int heads, int hd, float scale, void* stream) {
   if (B < 0 || Nq < 0 || Nk <= 0 || heads <= 0 || hd <= 0 || hd > 64 || !Q || !K || !V || !O || !dO || !dQ || !dK ||
-      !dV) {
+      !dV || !ws) {
     set_error("svk_attention_bwd: bad args"); return SVK_EINVAL;
   }
   if (B == 0 || Nq == 0) return SVK_OK;
-  auto lds = [&](int qb) { return (size_t)(2 * Nk * (hd + 1) + 2 * qb * (hd + 1) + 2 * qb * (Nk + 1) + qb) * 4; };
-  int QB = 32;
-  while (QB > 8 && lds(QB) > 160 * 1024) QB >>= 1;
-  if (lds(QB) > 160 * 1024) { set_error("svk_attention_bwd: Nk=%d hd=%d exceeds LDS", Nk, hd); return SVK_EUNSUPPORTED; }
+  if (ws_bytes < svk_attention_bwd_workspace(dtype, B, Nq, Nk, heads, hd)) {
+    set_error("svk_attention_bwd: workspace too small"); return SVK_EINVAL;
+  }
   if (B > 65535 || heads > 65535) { set_error("svk_attention_bwd: grid too large"); return SVK_EUNSUPPORTED; }
-  const size_t sm = lds(QB);
-  dim3 grid((Nq + QB - 1) / QB, heads, B);
   hipStream_t st = (hipStream_t)stream;
+  const int C = heads * hd;
+  float* acc = static_cast<float*>(ws);                 // [2][B][Nk][C] f32: dK | dV accumulators
+  const long nacc = (long)B * Nk * C;
+  if (hipMemsetAsync(acc, 0, 2 * nacc * sizeof(float), st) != hipSuccess) { set_error("svk_attention_bwd: memset"); return SVK_ELAUNCH; }
+  const bool vec_ok = al16(Q, ldq, sbq) && al16(K, ldk, sbk) && al16(V, ldv, sbv) && al16(O, ldo, sbo) &&
+                      al16(dO, lddo, sbdo) && al16(dQ, lddq, sbdq);
+  if (attn_bwd_mfma_ok(dtype, Nk, hd) && vec_ok) {
+    const int nkc = (Nk + 63) / 64;
+    const long nkp = nkc * 64L;
+    bf16* Pws = reinterpret_cast<bf16*>(acc + 2 * nacc);
+    bf16* dSws = Pws + (long)B * heads * Nq * nkp;
+    dim3 grid((Nq + 63) / 64, heads, B);
+    auto go = [&](auto hdp_c, auto nkc_c) {
+      constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
+      hipLaunchKernelGGL((attn_bwd_dq_mfma<HDP, NKC>), grid, dim3(256), 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K,
+                         ldk, sbk, (const bf16*)V, ldv, sbv, (const bf16*)O, ldo, sbo, (const bf16*)dO, lddo, sbdo,
+                         (bf16*)dQ, lddq, sbdq, Pws, dSws, Nq, Nk, hd, scale);
+    };
+    using H32 = std::integral_constant<int, 32>;
+    using H64 = std::integral_constant<int, 64>;
+    using N1 = std::integral_constant<int, 1>;
+    using N2 = std::integral_constant<int, 2>;
+    using N3 = std::integral_constant<int, 3>;
+    using N4 = std::integral_constant<int, 4>;
+    auto by_nkc = [&](auto hdp) {
+      switch (nkc) { case 1: go(hdp, N1{}); break; case 2: go(hdp, N2{}); break;
+                     case 3: go(hdp, N3{}); break; default: go(hdp, N4{}); break; }
+    };
+    if (hd <= 32) by_nkc(H32{}); else by_nkc(H64{});
+    int rc = check_launch("attn_bwd_dq_mfma");
+    if (rc) return rc;
+    // dK[b, :, h] += dS'[z]^T Q[b, :, h];  dV[b, :, h] += P[z]^T dO[b, :, h]   (z = b * heads + h)
+    const long zs = (long)Nq * nkp;
+    rc = wgrad_batched(SVK_BF16, dSws, nkp, heads * zs, zs, Q, ldq, sbq, hd, acc, C, (long)Nk * C, hd, B * heads, heads,
+                       Nq, Nk, hd, st);
+    if (rc) return rc;
+    rc = wgrad_batched(SVK_BF16, Pws, nkp, heads * zs, zs, dO, lddo, sbdo, hd, acc + nacc, C, (long)Nk * C, hd,
+                       B * heads, heads, Nq, Nk, hd, st);
+    if (rc) return rc;
+  } else {
+    auto lds = [&](int qb) { return (size_t)(2 * Nk * (hd + 1) + 2 * qb * (hd + 1) + 2 * qb * (Nk + 1) + qb) * 4; };
+    int QB = 32;
+    while (QB > 8 && lds(QB) > 160 * 1024) QB >>= 1;
+    if (lds(QB) > 160 * 1024) { set_error("svk_attention_bwd: Nk=%d hd=%d exceeds LDS", Nk, hd); return SVK_EUNSUPPORTED; }
+    const size_t sm = lds(QB);
+    dim3 grid((Nq + QB - 1) / QB, heads, B);
+    SVK_DISPATCH_DTYPE(dtype, T, {
+      if (sm > 65536)
+        (void)hipFuncSetAttribute((const void*)attention_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+      hipLaunchKernelGGL((attention_bwd_kernel<T>), grid, dim3(256), sm, st, (const T*)Q, ldq, sbq, (const T*)K, ldk,
+                         sbk, (const T*)V, ldv, sbv, (const T*)O, ldo, sbo, (const T*)dO, lddo, sbdo, (T*)dQ, lddq,
+                         sbdq, acc, acc + nacc, (long)C, (long)Nk * C, Nq, Nk, hd, QB, scale);
+      int rc = check_launch("attention_bwd");
+      if (rc) return rc;
+    });
+  }
   SVK_DISPATCH_DTYPE(dtype, T, {
-    if (sm > 65536)
-      (void)hipFuncSetAttribute((const void*)attention_bwd_kernel<T>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
-    hipLaunchKernelGGL((attention_bwd_kernel<T>), grid, dim3(256), sm, st, (const T*)Q, ldq, sbq, (const T*)K, ldk, sbk,
-                       (const T*)V, ldv, sbv, (const T*)O, ldo, sbo, (const T*)dO, lddo, sbdo, (T*)dQ, lddq, sbdq, dK,
-                       dV, lddk, sbdk, Nq, Nk, hd, QB, scale);
-    return check_launch("attention_bwd");
+    hipLaunchKernelGGL((store_kv_kernel<T>), dim3((unsigned)((nacc + 255) / 256)), dim3(256), 0, st, acc, (T*)dK,
+                       (T*)dV, lddk, sbdk, B, Nk, C);
+    return check_launch("attention_bwd store");
   });
 }

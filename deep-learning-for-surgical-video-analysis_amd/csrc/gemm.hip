@@ -49,6 +49,10 @@ struct GemmArgs {
   int sshift;           // log2(stride) (ASRC == 2)
   const float* rscale;  // optional per-row scale of act(A W^T + bias) before the residual add
   int rdiv;             //   rscale index = m / rdiv (stochastic depth: rdiv = tokens per frame)
+  const void* U; long ldu; int uact;   // optional activation backward: v *= act'(U[m, n]) (same dtype as C)
+  // out_mode 1: C (and R) are an NHWC map [B, uH, uW, uC] and GEMM row m = (b, py, px) of the
+  // (uH/us) x (uW/us) patch grid, column n = (i, j, ci): the adjoint of a k = s patchify conv.
+  int out_mode, uH, uW, us, uC;
 };
 
 template <typename T> struct Chunk { T v[8]; };
@@ -109,7 +113,7 @@ template <typename T, bool VEC>
 __device__ __forceinline__ unsigned load_dense(const T* base, long ld, int row, int rows, int k, int K, Chunk<T>& c) {
   const int rc = row < rows ? row : rows - 1;
   if (VEC) {
-    const int kc = k < K ? k : K - 8;
+    const int kc = k < K ? k : ((K - 1) & ~7);   // aligned clamp (rows may be zero-padded past K)
     load_vec8(base + (long)rc * ld + kc, c);
     return (row < rows && k < K) ? 0xFFu : 0u;
   }
@@ -216,7 +220,7 @@ constexpr int smem_bytes() {
   return main_b > epi_b ? main_b : epi_b;
 }
 
-template <typename T, int BM, int BN, bool VEC, int ASRC>
+template <typename T, int BM, int BN, bool VEC, int ASRC, bool EXT>
 __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
   constexpr int BK = bk_of<T>();
   constexpr int LDK = BK + 16 / sizeof(T);
@@ -318,7 +322,73 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
     __syncthreads();
   }
 
-  // Epilogue part 1: bias + activation in registers, f32 tile -> LDS.
+  if constexpr (!EXT) {
+    // Plain epilogue (bias + act + residual).  Part 1: bias + activation in registers, f32 tile -> LDS.
+    // C/D map of the 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + r.
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int cl = wn * WN + j * 16 + fr;
+      const int n = n0 + cl;
+      const float bn = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          sC[wm * WM + i * 16 + (lane >> 4) * 4 + r][cl] = apply_act(acc[i][j][r] + bn, p.act);
+    }
+    __syncthreads();
+    // Part 2: 8-column row chunks, residual added in f32, 16-byte stores.
+    T* C = static_cast<T*>(p.C);
+    const T* R = static_cast<const T*>(p.R);
+    constexpr int CH = BN / 8;
+#pragma unroll
+    for (int it = 0; it < (BM * CH) / NTHREADS; ++it) {
+      const int cidx = tid + it * NTHREADS;
+      const int row = cidx / CH, c8 = (cidx % CH) * 8;
+      const int m = m0 + row, n = n0 + c8;
+      if (m >= p.M || n >= p.N) continue;
+      float v[8];
+      *reinterpret_cast<float4*>(&v[0]) = *reinterpret_cast<const float4*>(&sC[row][c8]);
+      *reinterpret_cast<float4*>(&v[4]) = *reinterpret_cast<const float4*>(&sC[row][c8 + 4]);
+      if (p.vec_out && n + 8 <= p.N) {
+        if (R) {
+          Chunk<T> rr;
+          load_vec8(R + (long)m * p.ldr + n, rr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += to_f(rr.v[e]);
+        }
+        Chunk<T> o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o.v[e] = from_f<T>(v[e]);
+        store8(C + (long)m * p.ldc + n, o);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          if (n + e >= p.N) break;
+          float x = v[e];
+          if (R) x += to_f(R[(long)m * p.ldr + n + e]);
+          C[(long)m * p.ldc + n + e] = from_f<T>(x);
+        }
+      }
+    }
+  } else {
+    // Extended epilogue: + row scale (stochastic depth), activation backward (U), unpatchify store.
+  // Epilogue.
+  T* C = static_cast<T*>(p.C);
+  const T* R = static_cast<const T*>(p.R);
+  const T* U = static_cast<const T*>(p.U);
+  constexpr int CH = BN / 8;
+  constexpr int EPI = (BM * CH) / NTHREADS;
+  auto out_off = [&](int m, int n) -> long {
+    if (p.out_mode == 1) {
+      const int PW = p.uW / p.us, PH = p.uH / p.us;
+      const int px = m % PW, t = m / PW, py = t % PH, b = t / PH;
+      const int ci = n % p.uC, ij = n / p.uC, j = ij % p.us, i = ij / p.us;
+      return (((long)b * p.uH + py * p.us + i) * p.uW + px * p.us + j) * p.uC + ci;
+    }
+    return -1;
+  };
+  // Part 1: bias + activation in registers, f32 tile -> LDS.
   // C/D map of the 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + r.
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -331,14 +401,27 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
       for (int r = 0; r < 4; ++r)
         sC[wm * WM + i * 16 + (lane >> 4) * 4 + r][cl] = apply_act(acc[i][j][r] + bn, p.act);
   }
+  // Prefetch (after the accumulators are dead, so the register peak does not grow): the global loads
+  // of the residual R and the activation-backward source U overlap the barrier and the LDS reads.
+  Chunk<T> pu[EPI], pr[EPI];
+  if (p.vec_out && p.N >= 8) {
+#pragma unroll
+    for (int it = 0; it < EPI; ++it) {
+      const int cidx = tid + it * NTHREADS;
+      const int mc = min(m0 + cidx / CH, p.M - 1), nc = min(n0 + (cidx % CH) * 8, p.N - 8);
+      if (U) load_vec8(U + (long)mc * p.ldu + nc, pu[it]);
+      if (R) {
+        const long o = out_off(mc, nc);
+        load_vec8(R + (o >= 0 ? o : (long)mc * p.ldr + nc), pr[it]);
+      }
+    }
+  }
+
   __syncthreads();
 
-  // Epilogue part 2: 8-column row chunks, residual added in f32, 16-byte stores.
-  T* C = static_cast<T*>(p.C);
-  const T* R = static_cast<const T*>(p.R);
-  constexpr int CH = BN / 8;
+  // Part 2: 8-column row chunks, row scale / activation backward / residual in f32, 16-byte stores.
 #pragma unroll
-  for (int it = 0; it < (BM * CH) / NTHREADS; ++it) {
+  for (int it = 0; it < EPI; ++it) {
     const int cidx = tid + it * NTHREADS;
     const int row = cidx / CH, c8 = (cidx % CH) * 8;
     const int m = m0 + row, n = n0 + c8;
@@ -351,26 +434,32 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= sc;
     }
+    const long om = out_off(m, n);
+    const long coff = om >= 0 ? om : (long)m * p.ldc + n, roff = om >= 0 ? om : (long)m * p.ldr + n;
     if (p.vec_out && n + 8 <= p.N) {
-      if (R) {
-        Chunk<T> rr;
-        load_vec8(R + (long)m * p.ldr + n, rr);
+      if (U) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += to_f(rr.v[e]);
+        for (int e = 0; e < 8; ++e) v[e] *= act_grad(to_f(pu[it].v[e]), p.uact);
+      }
+      if (R) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += to_f(pr[it].v[e]);
       }
       Chunk<T> o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) o.v[e] = from_f<T>(v[e]);
-      store8(C + (long)m * p.ldc + n, o);
+      store8(C + coff, o);
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         if (n + e >= p.N) break;
         float x = v[e];
-        if (R) x += to_f(R[(long)m * p.ldr + n + e]);
-        C[(long)m * p.ldc + n + e] = from_f<T>(x);
+        if (U) x *= act_grad(to_f(U[(long)m * p.ldu + n + e]), p.uact);
+        if (R) x += to_f(R[roff + e]);
+        C[coff + e] = from_f<T>(x);
       }
     }
+  }
   }
 }
 
@@ -380,13 +469,20 @@ template <typename T, int ASRC>
 static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
   const int M = a.M, N = a.N;
   const long vw = 16 / (long)sizeof(T);
-  a.vec_out = aligned16(a.C) && (a.ldc % vw == 0) && (!a.R || (aligned16(a.R) && a.ldr % vw == 0));
+  a.vec_out = aligned16(a.C) && (a.ldc % vw == 0) && (!a.R || (aligned16(a.R) && a.ldr % vw == 0)) &&
+              (!a.U || (aligned16(a.U) && a.ldu % vw == 0)) && (a.out_mode == 0 || a.uC % 8 == 0);
+  const bool ext = a.rscale || a.U || a.out_mode;
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;
     const long nwg = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     dim3 grid((unsigned)nwg);
-    if (vec) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, ASRC>), grid, dim3(NTHREADS), 0, st, a);
-    else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, ASRC>), grid, dim3(NTHREADS), 0, st, a);
+    if (ext) {
+      if (vec) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, ASRC, true>), grid, dim3(NTHREADS), 0, st, a);
+      else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, ASRC, true>), grid, dim3(NTHREADS), 0, st, a);
+    } else {
+      if (vec) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, ASRC, false>), grid, dim3(NTHREADS), 0, st, a);
+      else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, ASRC, false>), grid, dim3(NTHREADS), 0, st, a);
+    }
   };
   using I64 = std::integral_constant<int, 64>;
   using I128 = std::integral_constant<int, 128>;
@@ -415,6 +511,10 @@ struct WgradArgs {
   float* dW; long lddw;
   int M, N, K, mchunk;
   int H, Wd, Cin, OH, OW, kw, stride, pad;
+  // batching over gridDim.z: z -> (z / nzi, z % nzi) outer/inner offsets (elements)
+  int nzi;
+  long sa_o, sa_i, sx_o, sx_i, sw_o, sw_i;
+  float* db;            // optional bias gradient db[n] += sum_m dY[m, n] (first K-tile column only)
 };
 
 template <typename T, bool VECA, bool VECB, int BSRC>
@@ -428,8 +528,10 @@ __global__ __launch_bounds__(NTHREADS) void wgrad_kernel(WgradArgs p) {
   const int n0 = (blockIdx.x / ntk) * 64, k0 = (blockIdx.x % ntk) * 64;
   const int mbeg = blockIdx.y * p.mchunk;
   const int mend = min(mbeg + p.mchunk, p.M);
-  const T* dY = static_cast<const T*>(p.dY);
-  const T* X = static_cast<const T*>(p.X);
+  const int zo = blockIdx.z / p.nzi, zi = blockIdx.z - (blockIdx.z / p.nzi) * p.nzi;
+  const T* dY = static_cast<const T*>(p.dY) + zo * p.sa_o + zi * p.sa_i;
+  const T* X = static_cast<const T*>(p.X) + zo * p.sx_o + zi * p.sx_i;
+  float* dWz = p.dW + zo * p.sw_o + zi * p.sw_i;
   const int lm = tid & 31, lc = (tid >> 5) * 8;
 
   Chunk<T> ra, rb;
@@ -458,9 +560,17 @@ __global__ __launch_bounds__(NTHREADS) void wgrad_kernel(WgradArgs p) {
       mb = load_dense<T, VECB>(X, p.ldx, mv ? m : p.M, p.M, k0 + lc, p.K, rb);
     }
   };
+  const bool do_db = p.db != nullptr && (blockIdx.x % ntk) == 0;
+  float dsum[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) dsum[e] = 0.f;
   auto stash = [&](int buf) {
     apply_mask8<T, VECA>(ra, ma);
     apply_mask8<T, VECB>(rb, mb);
+    if (do_db) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dsum[e] += to_f(ra.v[e]);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       sA[buf][lc + e][lm] = ra.v[e];
@@ -495,6 +605,21 @@ __global__ __launch_bounds__(NTHREADS) void wgrad_kernel(WgradArgs p) {
     __syncthreads();
     buf ^= 1;
   }
+  if (do_db) {
+    // the stash after the last step loaded a fully masked slab, so dsum holds exactly this WG's rows
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = dsum[e];
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+      dsum[e] = v;
+    }
+    if ((tid & 31) == 0) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n0 + lc + e < p.N) atomicAdd(p.db + n0 + lc + e, dsum[e]);
+    }
+  }
   // C map: col (k) = lane & 15, row (n) = (lane >> 4) * 4 + r
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -504,21 +629,23 @@ __global__ __launch_bounds__(NTHREADS) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn * 32 + i * 16 + (lane >> 4) * 4 + r;
-        if (n < p.N && k < p.K) atomicAdd(p.dW + (long)n * p.lddw + k, acc[i][j][r]);
+        if (n < p.N && k < p.K) atomicAdd(dWz + (long)n * p.lddw + k, acc[i][j][r]);
       }
     }
 }
 
 template <typename T, int BSRC>
-static int launch_wgrad(WgradArgs a, bool veca, bool vecb, hipStream_t st) {
+static int launch_wgrad(WgradArgs a, bool veca, bool vecb, hipStream_t st, int Z = 1) {
+  if (a.nzi <= 0) a.nzi = 1;
   const long tiles = (long)((a.N + 63) / 64) * ((a.K + 63) / 64);
-  // split M so that the grid holds ~2048 workgroups, each with >= 256 rows
-  long splits = std::max<long>(1, std::min<long>((2048 + tiles - 1) / tiles, (a.M + 255) / 256));
+  // split M so that the grid holds ~1024 workgroups, each with >= 1024 rows (fewer, longer
+  // workgroups: the partial tiles and bias sums are f32 atomics on few addresses)
+  long splits = std::max<long>(1, std::min<long>((1024 + tiles * Z - 1) / (tiles * Z), (a.M + 1023) / 1024));
   long chunk = (a.M + splits - 1) / splits;
   chunk = (chunk + 31) / 32 * 32;
   splits = (a.M + chunk - 1) / chunk;
   a.mchunk = (int)chunk;
-  dim3 grid((unsigned)tiles, (unsigned)splits);
+  dim3 grid((unsigned)tiles, (unsigned)splits, (unsigned)Z);
   if (veca && vecb) hipLaunchKernelGGL((wgrad_kernel<T, true, true, BSRC>), grid, dim3(NTHREADS), 0, st, a);
   else if (veca) hipLaunchKernelGGL((wgrad_kernel<T, true, false, BSRC>), grid, dim3(NTHREADS), 0, st, a);
   else if (vecb) hipLaunchKernelGGL((wgrad_kernel<T, false, true, BSRC>), grid, dim3(NTHREADS), 0, st, a);
@@ -531,8 +658,8 @@ static int launch_wgrad(WgradArgs a, bool veca, bool vecb, hipStream_t st) {
 using namespace svk;
 
 extern "C" int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
-                           const float* row_scale, int rows_per_scale, const void* R, long ldr, void* C, long ldc,
-                           int M, int N, int K, int act, void* stream) {
+                           const float* row_scale, int rows_per_scale, const void* U, long ldu, int uact,
+                           const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act, void* stream) {
   if (M < 0 || N <= 0 || K <= 0 || !A || !W || !C || (row_scale && rows_per_scale <= 0)) {
     set_error("svk_gemm: bad args M=%d N=%d K=%d", M, N, K); return SVK_EINVAL;
   }
@@ -541,6 +668,8 @@ extern "C" int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, lo
   GemmArgs a{};
   a.A = A; a.lda = lda; a.W = W; a.ldw = ldw; a.bias = bias; a.R = R; a.ldr = ldr; a.C = C; a.ldc = ldc;
   a.M = M; a.N = N; a.K = K; a.act = act; a.rscale = row_scale; a.rdiv = rows_per_scale;
+  if (U && ldu < N) { set_error("svk_gemm: ldu too small"); return SVK_EINVAL; }
+  a.U = U; a.ldu = ldu; a.uact = uact;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
     const long vecw = 16 / (long)sizeof(T);
@@ -551,7 +680,26 @@ extern "C" int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, lo
 
 extern "C" int svk_gemm(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
                         const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act, void* stream) {
-  return svk_gemm_ex(dtype, A, lda, W, ldw, bias, nullptr, 1, R, ldr, C, ldc, M, N, K, act, stream);
+  return svk_gemm_ex(dtype, A, lda, W, ldw, bias, nullptr, 1, nullptr, 0, 0, R, ldr, C, ldc, M, N, K, act, stream);
+}
+
+extern "C" int svk_gemm_unpatchify(int dtype, const void* A, long lda, const void* W, long ldw, const void* R,
+                                   void* Y, int B, int H, int Wd, int s, int C, int K, void* stream) {
+  if (B < 0 || H <= 0 || Wd <= 0 || s <= 0 || C <= 0 || K <= 0 || H % s || Wd % s || !A || !W || !Y || lda < K ||
+      ldw < K) {
+    set_error("svk_gemm_unpatchify: bad args"); return SVK_EINVAL;
+  }
+  if (B == 0) return SVK_OK;
+  GemmArgs a{};
+  a.A = A; a.lda = lda; a.W = W; a.ldw = ldw; a.R = R; a.ldr = 0; a.C = Y; a.ldc = 0;
+  a.M = B * (H / s) * (Wd / s); a.N = s * s * C; a.K = K; a.rdiv = 1;
+  a.out_mode = 1; a.uH = H; a.uW = Wd; a.us = s; a.uC = C;
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    const long vecw = 16 / (long)sizeof(T);
+    bool vec = aligned16(A) && aligned16(W) && (lda % vecw == 0) && (ldw % vecw == 0) && (K % 8 == 0);
+    return launch_gemm<T, 0>(a, vec, st);
+  });
 }
 
 extern "C" int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* Wt,
@@ -601,14 +749,31 @@ extern "C" int svk_conv2d_dgrad_nhwc(int dtype, const void* dY, int B, int OH, i
   });
 }
 
+// Batched weight-gradient reduction used by the attention backward (dK = dS^T Q, dV = P^T dO per
+// frame and head).  dY rows may be padded past N (ldy >= N rounded up to 8, zero-filled) which
+// allows the vector loader whenever the alignment holds.
+int svk::wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o,
+                  long sx_i, float* dW, long lddw, long sw_o, long sw_i, int Z, int nzi, int M, int N, int K,
+                  hipStream_t st) {
+  WgradArgs a{};
+  a.dY = dY; a.ldy = ldy; a.X = X; a.ldx = ldx; a.dW = dW; a.lddw = lddw; a.M = M; a.N = N; a.K = K;
+  a.nzi = nzi; a.sa_o = sa_o; a.sa_i = sa_i; a.sx_o = sx_o; a.sx_i = sx_i; a.sw_o = sw_o; a.sw_i = sw_i;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    const long vw = 16 / (long)sizeof(T);
+    const bool va = aligned16(dY) && ldy % vw == 0 && sa_o % vw == 0 && sa_i % vw == 0 && ldy >= (N + 7) / 8 * 8;
+    const bool vb = aligned16(X) && ldx % vw == 0 && sx_o % vw == 0 && sx_i % vw == 0 && K % 8 == 0;
+    return launch_wgrad<T, 0>(a, va, vb, st, Z);
+  });
+}
+
 extern "C" int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw,
-                              int M, int N, int K, void* stream) {
+                              float* db, int M, int N, int K, void* stream) {
   if (M < 0 || N <= 0 || K <= 0 || !dY || !X || !dW || ldy < N || ldx < K || lddw < K) {
     set_error("svk_gemm_wgrad: bad args"); return SVK_EINVAL;
   }
   if (M == 0) return SVK_OK;
   WgradArgs a{};
-  a.dY = dY; a.ldy = ldy; a.X = X; a.ldx = ldx; a.dW = dW; a.lddw = lddw; a.M = M; a.N = N; a.K = K;
+  a.dY = dY; a.ldy = ldy; a.X = X; a.ldx = ldx; a.dW = dW; a.lddw = lddw; a.M = M; a.N = N; a.K = K; a.db = db;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
     const long vw = 16 / (long)sizeof(T);
@@ -619,7 +784,7 @@ extern "C" int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X
 }
 
 extern "C" int svk_conv2d_wgrad_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* dY,
-                                     int Cout, int k, int stride, int pad, float* dW, void* stream) {
+                                     int Cout, int k, int stride, int pad, float* dW, float* db, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || k <= 0 || stride <= 0 || pad < 0 || !X || !dY || !dW) {
     set_error("svk_conv2d_wgrad_nhwc: bad args"); return SVK_EINVAL;
   }
@@ -630,7 +795,7 @@ extern "C" int svk_conv2d_wgrad_nhwc(int dtype, const void* X, int B, int H, int
   if (M > 0x7fffffffL) { set_error("svk_conv2d_wgrad_nhwc: too many pixels"); return SVK_EUNSUPPORTED; }
   WgradArgs a{};
   a.dY = dY; a.ldy = Cout; a.X = X; a.ldx = 0; a.dW = dW; a.lddw = (long)k * k * Cin;
-  a.M = (int)M; a.N = Cout; a.K = k * k * Cin;
+  a.M = (int)M; a.N = Cout; a.K = k * k * Cin; a.db = db;
   a.H = H; a.Wd = W; a.Cin = Cin; a.OH = OH; a.OW = OW; a.kw = k; a.stride = stride; a.pad = pad;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {

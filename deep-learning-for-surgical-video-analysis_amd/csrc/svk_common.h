@@ -15,6 +15,10 @@ namespace svk {
 // Thread-local last-error string (svk_last_error); set by the host wrappers only.
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// gemm.hip: batched split-M weight-gradient reduction dW[z] += dY[z]^T X[z] (f32 atomics)
+int wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o,
+                  long sx_i, float* dW, long lddw, long sw_o, long sw_i, int Z, int nzi, int M, int N, int K,
+                  hipStream_t st);
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
@@ -45,6 +49,27 @@ __device__ __forceinline__ float apply_act(float v, int act) {
     case SVK_ACT_RELU: return v > 0.f ? v : 0.f;
     case SVK_ACT_TANH: return tanhf(v);
     default: return v;
+  }
+}
+
+// d act(u) / du (activation backward): GELU (erf form), ReLU, tanh.  The GELU derivative uses the
+// branch-free erf (|err| <= 1.5e-7, below bf16 resolution and f32-parity tolerance).
+__device__ __forceinline__ float act_grad(float u, int act) {
+  switch (act) {
+    case SVK_ACT_GELU: {
+      const float e = __expf(-0.5f * u * u);
+      const float x = u * 0.70710678118654752f, ax = fabsf(x);
+      const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+      float p = fmaf(1.061405429f, t, -1.453152027f);
+      p = fmaf(p, t, 1.421413741f);
+      p = fmaf(p, t, -0.284496736f);
+      p = fmaf(p, t, 0.254829592f);
+      const float erf_ = copysignf(1.0f - p * t * e, x);      // exp(-x^2) == exp(-u^2 / 2) = e
+      return 0.5f * (1.0f + erf_) + u * 0.3989422804014327f * e;
+    }
+    case SVK_ACT_RELU: return u > 0.f ? 1.f : 0.f;
+    case SVK_ACT_TANH: { const float t = tanhf(u); return 1.f - t * t; }
+    default: return 1.f;
   }
 }
 

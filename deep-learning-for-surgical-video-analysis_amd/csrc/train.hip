@@ -68,6 +68,120 @@ __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict_
   }
 }
 
+// Vectorized LayerNorm backward: LPR lanes per row, 16-byte chunks (C % 8 == 0, C <= 512), grid-stride
+// over rows; the affine gradients are reduced in registers over the rows a lane group visits, then
+// across the wave's row groups by shuffles, then one f32 atomic per channel per wave.
+template <typename T>
+__device__ __forceinline__ void ld8(const T* p, float* v) {
+  T t[8];
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(t) = *reinterpret_cast<const uint4*>(p);
+  } else {
+    reinterpret_cast<uint4*>(t)[0] = reinterpret_cast<const uint4*>(p)[0];
+    reinterpret_cast<uint4*>(t)[1] = reinterpret_cast<const uint4*>(p)[1];
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = to_f(t[e]);
+}
+template <typename T>
+__device__ __forceinline__ void st8(T* p, const float* v) {
+  T t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = from_f<T>(v[e]);
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(p) = *reinterpret_cast<const uint4*>(t);
+  } else {
+    reinterpret_cast<uint4*>(p)[0] = reinterpret_cast<const uint4*>(t)[0];
+    reinterpret_cast<uint4*>(p)[1] = reinterpret_cast<const uint4*>(t)[1];
+  }
+}
+
+template <typename T, int LPR, bool AFFINE>
+__global__ __launch_bounds__(256) void layernorm_bwd_vec(const T* __restrict__ X, long ldx, const T* __restrict__ dY,
+                                                         long ldy, const float* __restrict__ g,
+                                                         const T* __restrict__ dR, long ldr, T* __restrict__ dX,
+                                                         long lddx, float* __restrict__ dg, float* __restrict__ db,
+                                                         int M, int C, float eps) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR, rg = lane / LPR;
+  const int nch = C >> 3;
+  const bool has = sub < nch;
+  const int c0 = sub * 8;
+  float gv[8], pg[8], pb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { gv[e] = has ? g[c0 + e] : 0.f; pg[e] = 0.f; pb[e] = 0.f; }
+  const long stride = (long)gridDim.x * 4 * RPW;
+  for (long r0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW; r0 < M; r0 += stride) {
+    const long row = r0 + rg;
+    const bool ok = has && row < M;
+    float x[8], dy[8];
+    if (ok) { ld8(X + row * ldx + c0, x); ld8(dY + row * ldy + c0, dy); }
+    else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { x[e] = 0.f; dy[e] = 0.f; }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += x[e];
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s / C;
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { const float d = ok ? x[e] - mean : 0.f; q += d * d; }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q / C + eps);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      x[e] = (x[e] - mean) * rstd;
+      const float gy = dy[e] * gv[e];
+      s1 += gy;
+      s2 += gy * x[e];
+    }
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) { s1 += __shfl_xor(s1, o, 64); s2 += __shfl_xor(s2, o, 64); }
+    s1 /= C;
+    s2 /= C;
+    if (ok) {
+      float out[8];
+      if (dR) ld8(dR + row * ldr + c0, out);
+      else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) out[e] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) out[e] += rstd * (dy[e] * gv[e] - s1 - x[e] * s2);
+      st8(dX + row * lddx + c0, out);
+      if constexpr (AFFINE) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { pg[e] += dy[e] * x[e]; pb[e] += dy[e]; }
+      }
+    }
+  }
+  if constexpr (AFFINE) {
+    // reduce over the wave's row groups, then over the block's 4 waves in LDS: one atomic per channel
+    // per block (the grid is capped at 256 blocks for the affine variant)
+    __shared__ float red[2][4][512];
+    const int w = threadIdx.x >> 6;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int o = LPR; o < 64; o <<= 1) { pg[e] += __shfl_xor(pg[e], o, 64); pb[e] += __shfl_xor(pb[e], o, 64); }
+    }
+    if (rg == 0 && has) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { red[0][w][c0 + e] = pg[e]; red[1][w][c0 + e] = pb[e]; }
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      atomicAdd(dg + c, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+      atomicAdd(db + c, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+    }
+  }
+}
+
 // ---- activation backward: dX = dY * act'(U) (+ dR) --------------------------------------------
 template <typename T>
 __global__ void act_bwd_kernel(const T* __restrict__ U, const T* __restrict__ dY, const T* __restrict__ dR,
@@ -296,9 +410,13 @@ __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
   return x;
 }
-__global__ void keep_mask_kernel(float* __restrict__ out, long n, float keep, uint32_t seed) {
+__global__ void keep_mask_kernel(float* __restrict__ out, long n, float keep, uint32_t seed,
+                                 const long long* __restrict__ counter) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  // the optional device counter (the trainer's step count) makes replays of a captured graph draw
+  // fresh masks
+  if (counter) seed = hash32(seed ^ hash32((uint32_t)*counter * 0x85EBCA6BU));
   const float u = (hash32((uint32_t)i * 0x9E3779B9U ^ hash32(seed)) >> 8) * (1.0f / 16777216.0f);
   out[i] = u < keep ? 1.0f / keep : 0.f;
 }
@@ -366,6 +484,19 @@ inline dim3 g1(long n) { return dim3((unsigned)((n + 255) / 256)); }
 
 using namespace svk;
 
+template <typename T, int LPR>
+static void launch_ln_bwd_vec(const T* X, long ldx, const T* dY, long ldy, const float* g, const T* dR, long ldr, T* dX,
+                              long lddx, float* dg, float* db, int M, int C, float eps, hipStream_t st) {
+  constexpr int RPB = 4 * (64 / LPR);
+  const int blocks = (int)std::min<long>((M + RPB - 1) / RPB, dg ? 256 : 1L << 30);
+  if (dg)
+    hipLaunchKernelGGL((layernorm_bwd_vec<T, LPR, true>), dim3(blocks), dim3(256), 0, st, X, ldx, dY, ldy, g, dR, ldr,
+                       dX, lddx, dg, db, M, C, eps);
+  else
+    hipLaunchKernelGGL((layernorm_bwd_vec<T, LPR, false>), dim3(blocks), dim3(256), 0, st, X, ldx, dY, ldy, g, dR, ldr,
+                       dX, lddx, dg, db, M, C, eps);
+}
+
 extern "C" int svk_layernorm_bwd(int dtype, const void* X, long ldx, const void* dY, long ldy, const float* gamma,
                                  const void* dR, long ldr, void* dX, long lddx, float* dgamma, float* dbeta, int M,
                                  int C, float eps, void* stream) {
@@ -373,6 +504,29 @@ extern "C" int svk_layernorm_bwd(int dtype, const void* X, long ldx, const void*
     set_error("svk_layernorm_bwd: bad args (C <= 512)"); return SVK_EINVAL;
   }
   if (M == 0) return SVK_OK;
+  {
+    const uintptr_t al = (uintptr_t)X | (uintptr_t)dY | (uintptr_t)dX | (uintptr_t)dR;
+    const long vw = dtype == SVK_BF16 ? 8 : 4;
+    if (C % 8 == 0 && (al & 15) == 0 && ldx % vw == 0 && ldy % vw == 0 && lddx % vw == 0 && (!dR || ldr % vw == 0)) {
+      hipStream_t st = (hipStream_t)stream;
+      const int nch = C / 8;
+      SVK_DISPATCH_DTYPE(dtype, T, {
+        auto go = [&](auto lpr) {
+          constexpr int L = decltype(lpr)::value;
+          launch_ln_bwd_vec<T, L>((const T*)X, ldx, (const T*)dY, ldy, gamma, (const T*)dR, ldr, (T*)dX, lddx, dgamma,
+                                  dbeta, M, C, eps, st);
+        };
+        if (nch <= 1) go(std::integral_constant<int, 1>{});
+        else if (nch <= 2) go(std::integral_constant<int, 2>{});
+        else if (nch <= 4) go(std::integral_constant<int, 4>{});
+        else if (nch <= 8) go(std::integral_constant<int, 8>{});
+        else if (nch <= 16) go(std::integral_constant<int, 16>{});
+        else if (nch <= 32) go(std::integral_constant<int, 32>{});
+        else go(std::integral_constant<int, 64>{});
+        return check_launch("layernorm_bwd_vec");
+      });
+    }
+  }
   const int blocks = (int)std::min<long>((M + 3) / 4, 2048);
   SVK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((layernorm_bwd_kernel<T>), dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const T*)X, ldx,
@@ -470,10 +624,10 @@ extern "C" int svk_row_scale(int dtype, const void* X, const float* s, void* Y, 
   });
 }
 
-extern "C" int svk_keep_mask(float* out, long n, float keep, unsigned seed, void* stream) {
+extern "C" int svk_keep_mask(float* out, long n, float keep, unsigned seed, const long long* counter, void* stream) {
   if (n < 0 || !out || !(keep > 0.f) || keep > 1.f) { set_error("svk_keep_mask: bad args"); return SVK_EINVAL; }
   if (n == 0) return SVK_OK;
-  hipLaunchKernelGGL(keep_mask_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, out, n, keep, (uint32_t)seed);
+  hipLaunchKernelGGL(keep_mask_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, out, n, keep, (uint32_t)seed, counter);
   return check_launch("keep_mask");
 }
 

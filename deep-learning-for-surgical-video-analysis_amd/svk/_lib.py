@@ -34,15 +34,17 @@ SIGNATURES = {
     "svk_cast": [c_int, P, c_int, P, c_long, P],
     # training step
     "svk_dwconv3x3_ex": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
-    "svk_gemm_ex": [c_int, P, c_long, P, c_long, P, P, c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, P],
-    "svk_gemm_wgrad": [c_int, P, c_long, P, c_long, P, c_long, c_int, c_int, c_int, P],
-    "svk_conv2d_wgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P],
+    "svk_gemm_ex": [c_int, P, c_long, P, c_long, P, P, c_int, P, c_long, c_int, P, c_long, P, c_long, c_int, c_int,
+                    c_int, c_int, P],
+    "svk_gemm_unpatchify": [c_int, P, c_long, P, c_long, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_gemm_wgrad": [c_int, P, c_long, P, c_long, P, c_long, P, c_int, c_int, c_int, P],
+    "svk_conv2d_wgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, P],
     "svk_conv2d_dgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
                               c_int, P],
     "svk_unpatchify": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_attention_bwd": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
-                          P, c_long, c_long, P, c_long, c_long, P, P, c_long, c_long, c_int, c_int, c_int, c_int,
-                          c_int, c_float, P],
+                          P, c_long, c_long, P, c_long, c_long, P, P, c_long, c_long, P, c_long, c_int, c_int, c_int,
+                          c_int, c_int, c_float, P],
     "svk_layernorm_bwd": [c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
     "svk_act_bwd": [c_int, P, P, P, P, c_long, c_int, P],
     "svk_colstats": [c_int, P, c_long, c_int, c_int, P, P, P],
@@ -53,12 +55,13 @@ SIGNATURES = {
     "svk_bcast_rows": [c_int, P, P, c_float, P, c_int, c_int, c_int, P],
     "svk_row_scale": [c_int, P, P, P, c_long, c_int, c_int, P],
     "svk_mul_f32": [P, P, P, c_long, P],
-    "svk_keep_mask": [P, c_long, c_float, ctypes.c_uint, P],
+    "svk_keep_mask": [P, c_long, c_float, ctypes.c_uint, P, P],
     "svk_phase_loss": [P, P, P, P, c_int, c_int, P, P, P, P],
     "svk_sgd": [P, P, P, c_long, c_float, c_float, c_float, c_float, c_int, c_int, P],
     "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],
 }
 STRING_FUNCS = ("svk_version", "svk_last_error")
+LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int]}
 
 _lib = None
 
@@ -77,13 +80,21 @@ def load():
                        f"`python -c 'import __graft_entry__ as g; g.build()'` (make -C csrc)")
     lib = ctypes.CDLL(LIB_PATH)
     for name, argtypes in SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:          # an older library build (SVK_LIB): the symbol fails when called
+            continue
         fn.argtypes = argtypes
         fn.restype = c_int
     for name in STRING_FUNCS:
         fn = getattr(lib, name)
         fn.argtypes = []
         fn.restype = c_char_p
+    for name, argtypes in LONG_FUNCS.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = c_long
     _lib = lib
     return lib
 

@@ -68,14 +68,14 @@ def set_profiler(records):
     _PROF = records
 
 
-def _gemm_kernel_name(dt, M, N, vec, asrc):
+def _gemm_kernel_name(dt, M, N, vec, asrc, ext=False):
     """Mirror of launch_gemm's tile choice (csrc/gemm.hip) -> the kernel symbol rocprof reports."""
     if N <= 64:
         bm, bn = (128, 64) if (M + 127) // 128 >= 512 else (64, 64)
     else:
         bm, bn = (128, 128) if ((M + 127) // 128) * ((N + 127) // 128) >= 512 else (64, 64)
     t = "float" if dt == F32 else "__bf16"
-    return f"gemm_kernel<{t}, {bm}, {bn}, {'true' if vec else 'false'}, {asrc}>"
+    return f"gemm_kernel<{t}, {bm}, {bn}, {'true' if vec else 'false'}, {asrc}, {'true' if ext else 'false'}>"
 
 
 def _prof_begin():
@@ -94,9 +94,11 @@ def _prof_end(start, name, flops, nbytes, shape=None):
     _PROF.append((name, flops, nbytes, start, e, shape))
 
 
-def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=None, rows_per=1):
-    """out = row_scale[m // rows_per] * act(a @ w[:n].T + bias) + residual; a [..., K], w [N, K]
-    (same dtype as a); row_scale (f32) is optional (stochastic depth)."""
+def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=None, rows_per=1, dact=None,
+         dact_src=None):
+    """out = row_scale[m // rows_per] * act(a @ w[:n].T + bias) * dact'(dact_src) + residual; a [..., K],
+    w [N, K] (same dtype as a); row_scale (f32, stochastic depth) and the activation-backward factor
+    (dact in {"gelu", "relu", "tanh"} evaluated at dact_src [M, N]) are optional."""
     _chk(a, "a"); _chk(w, "w", a.dtype); _chk(bias, "bias", torch.float32); _chk(residual, "residual", a.dtype)
     M, K, lda = _rows(a, "a")
     N = w.shape[0] if n is None else n
@@ -112,21 +114,29 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
         if rc != N:
             raise _lib.SvkError("svk.gemm: residual width mismatch")
     t0 = _prof_begin()
-    if row_scale is None:
+    if row_scale is None and dact is None:
         _lib.call("svk_gemm", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
                   _p(out), ldc, M, N, K, ACT[act], _stream())
     else:
         _chk(row_scale, "row_scale", torch.float32)
-        if row_scale.numel() * rows_per < M:
+        if row_scale is not None and row_scale.numel() * rows_per < M:
             raise _lib.SvkError("svk.gemm: row_scale too short")
+        ldu = 0
+        if dact is not None:
+            _chk(dact_src, "dact_src", a.dtype)
+            mu, nu, ldu = _rows(dact_src, "dact_src")
+            if mu != M or nu != N:
+                raise _lib.SvkError("svk.gemm: dact_src shape mismatch")
         _lib.call("svk_gemm_ex", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(row_scale),
-                  rows_per, _p(residual), ldr, _p(out), ldc, M, N, K, ACT[act], _stream())
+                  rows_per, _p(dact_src), ldu, ACT[dact], _p(residual), ldr, _p(out), ldc, M, N, K, ACT[act],
+                  _stream())
     if t0 is not None:
         es = a.element_size()
         vw = 16 // es
         vec = a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and lda % vw == 0 and w.stride(0) % vw == 0
         nb = (M * K + N * K + M * N * (2 if residual is not None else 1)) * es
-        _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0), 2.0 * M * N * K, nb, (M, N, K))
+        _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0, row_scale is not None or dact is not None),
+                  2.0 * M * N * K, nb, (M, N, K))
     return out
 
 
@@ -327,30 +337,36 @@ def _f32_rows(t, name):
     return _rows(t, name)
 
 
-def gemm_wgrad(dy, x, dw):
-    """dw [N, K] f32 (row stride any) += dy[M, N]^T @ x[M, K]."""
+def gemm_wgrad(dy, x, dw, db=None):
+    """dw [N, K] f32 (row stride any) += dy[M, N]^T @ x[M, K]; db [N] f32 += column sums of dy."""
     _chk(dy, "dy"); _chk(x, "x", dy.dtype)
     M, N, ldy = _rows(dy, "dy")
     Mx, K, ldx = _rows(x, "x")
     _, _, lddw = _f32_rows(dw, "dw")
     if Mx != M or dw.shape[-1] != K or dw.numel() // K != N:
         raise _lib.SvkError(f"svk.gemm_wgrad: shapes dy {tuple(dy.shape)} x {tuple(x.shape)} dw {tuple(dw.shape)}")
+    _chk(db, "db", torch.float32)
+    if db is not None and (db.numel() != N or not db.is_contiguous()):
+        raise _lib.SvkError("svk.gemm_wgrad: db shape mismatch")
     t0 = _prof_begin()
-    _lib.call("svk_gemm_wgrad", dtype_code(dy.dtype), _p(dy), ldy, _p(x), ldx, _p(dw), lddw, M, N, K, _stream())
+    _lib.call("svk_gemm_wgrad", dtype_code(dy.dtype), _p(dy), ldy, _p(x), ldx, _p(dw), lddw, _p(db), M, N, K,
+              _stream())
     _prof_end(t0, "wgrad_kernel", 2.0 * M * N * K, (M * (N + K)) * dy.element_size() + N * K * 4, (M, N, K, "wgrad"))
     return dw
 
 
-def conv2d_wgrad(x, dy, k, stride, pad, dw):
-    """x [B, H, W, Cin] NHWC, dy [B, OH, OW, Cout]; dw [Cout, k*k*Cin] f32 += (packed like conv_w)."""
+def conv2d_wgrad(x, dy, k, stride, pad, dw, db=None):
+    """x [B, H, W, Cin] NHWC, dy [B, OH, OW, Cout]; dw [Cout, k*k*Cin] f32 += (packed like conv_w);
+    db [Cout] f32 += column sums of dy."""
     _chk(x, "x"); _chk(dy, "dy", x.dtype); _chk(dw, "dw", torch.float32)
     B, H, W, Cin = x.shape
     Cout = dy.shape[-1]
     if not (x.is_contiguous() and dy.is_contiguous() and dw.is_contiguous()) or dw.numel() != Cout * k * k * Cin:
         raise _lib.SvkError("svk.conv2d_wgrad: layout mismatch")
     t0 = _prof_begin()
+    _chk(db, "db", torch.float32)
     _lib.call("svk_conv2d_wgrad_nhwc", dtype_code(x.dtype), _p(x), B, H, W, Cin, _p(dy), Cout, k, stride, pad, _p(dw),
-              _stream())
+              _p(db), _stream())
     M = dy.numel() // Cout
     _prof_end(t0, "wgrad_kernel", 2.0 * M * Cout * k * k * Cin, (x.numel() + dy.numel()) * x.element_size(),
               (M, Cout, k * k * Cin, f"convwgrad{k}s{stride}"))
@@ -378,6 +394,24 @@ def conv2d_dgrad(dy, wd_packed, H, W, Cin, k, stride, pad, residual=None, out=No
     return out
 
 
+def gemm_unpatchify(a, w, out, s, residual=None):
+    """out NHWC [B, H, W, C] = unpatchify(a [B*(H/s)*(W/s), K] @ w.T) + residual (adjoint of the k = s
+    patchify conv; w [(i, j, ci), K]).  residual may alias out."""
+    _chk(a, "a"); _chk(w, "w", a.dtype); _chk(out, "out", a.dtype); _chk(residual, "residual", a.dtype)
+    M, K, lda = _rows(a, "a")
+    B, H, W, C = out.shape
+    if not out.is_contiguous() or w.shape != (s * s * C, K) or M != B * (H // s) * (W // s):
+        raise _lib.SvkError("svk.gemm_unpatchify: shape mismatch")
+    if residual is not None and (residual.shape != out.shape or not residual.is_contiguous()):
+        raise _lib.SvkError("svk.gemm_unpatchify: residual mismatch")
+    t0 = _prof_begin()
+    _lib.call("svk_gemm_unpatchify", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(residual), _p(out), B,
+              H, W, s, C, K, _stream())
+    _prof_end(t0, "gemm_kernel(unpatchify)", 2.0 * M * s * s * C * K, (a.numel() + w.numel() + out.numel()) *
+              a.element_size(), (M, s * s * C, K, "unpatchify"))
+    return out
+
+
 def unpatchify(p, B, PH, PW, s, C, out, accumulate=False):
     """p [B*PH*PW, s*s*C] -> out NHWC [B, PH*s, PW*s, C] (written or accumulated)."""
     _chk(p, "p"); _chk(out, "out", p.dtype)
@@ -387,28 +421,34 @@ def unpatchify(p, B, PH, PW, s, C, out, accumulate=False):
     return out
 
 
-def attention_bwd(q, k, v, o, do, heads, scale, dk, dv, dq=None):
-    """Backward of attention(q, k, v): returns dq (compute dtype, [B, Nq, C]); dk/dv f32 [B, Nk, C]
-    views with equal strides (e.g. the two halves of one [B, Nk, 2C] buffer) are accumulated (zero them first)."""
+def attention_bwd(q, k, v, o, do, heads, scale, dk=None, dv=None, dq=None):
+    """Backward of attention(q, k, v) -> (dq, dk, dv) in the compute dtype.  dk / dv may be given as
+    views with equal strides (e.g. the two halves of one [B, Nk, 2C] buffer)."""
     for t, nm in ((q, "q"), (k, "k"), (v, "v"), (o, "o"), (do, "do")):
         _chk(t, nm, q.dtype)
         if t.dim() != 3 or t.stride(2) != 1:
             raise _lib.SvkError(f"svk.attention_bwd: {nm} must be [B, N, C] with unit channel stride")
     B, Nq, C = q.shape
     Nk = k.shape[1]
+    if dk is None:
+        kv = torch.empty(B, Nk, 2 * C, device=q.device, dtype=q.dtype)
+        dk, dv = kv[:, :, :C], kv[:, :, C:]
     for t, nm in ((dk, "dk"), (dv, "dv")):
-        _chk(t, nm, torch.float32)
+        _chk(t, nm, q.dtype)
         if t.shape != (B, Nk, C) or t.stride(2) != 1 or t.stride() != dk.stride():
-            raise _lib.SvkError(f"svk.attention_bwd: {nm} must be f32 [B, Nk, C] (unit channel stride, dk/dv alike)")
+            raise _lib.SvkError(f"svk.attention_bwd: {nm} must be [B, Nk, C] (unit channel stride, dk/dv alike)")
     if dq is None:
         dq = torch.empty(B, Nq, C, device=q.device, dtype=q.dtype)
+    hd = C // heads
+    nbytes = _lib.load().svk_attention_bwd_workspace(dtype_code(q.dtype), B, Nq, Nk, heads, hd)
+    ws = torch.empty((nbytes + 15) // 16 * 4, device=q.device, dtype=torch.float32)
     t0 = _prof_begin()
     _lib.call("svk_attention_bwd", dtype_code(q.dtype), _p(q), q.stride(1), q.stride(0), _p(k), k.stride(1),
               k.stride(0), _p(v), v.stride(1), v.stride(0), _p(o), o.stride(1), o.stride(0), _p(do), do.stride(1),
-              do.stride(0), _p(dq), dq.stride(1), dq.stride(0), _p(dk), _p(dv), dk.stride(1), dk.stride(0), B, Nq, Nk,
-              heads, C // heads, float(scale), _stream())
-    _prof_end(t0, "attention_bwd_kernel", 2.0 * B * Nq * Nk * C * 5, 0, (B, Nq, Nk, C, "attn_bwd"))
-    return dq
+              do.stride(0), _p(dq), dq.stride(1), dq.stride(0), _p(dk), _p(dv), dk.stride(1), dk.stride(0), _p(ws),
+              ws.numel() * 4, B, Nq, Nk, heads, hd, float(scale), _stream())
+    _prof_end(t0, "attention_bwd", 2.0 * B * Nq * Nk * C * 4, 0, (B, Nq, Nk, C, "attn_bwd"))
+    return dq, dk, dv
 
 
 def layernorm_bwd(x, dy, gamma, eps, dres=None, out=None, dgamma=None, dbeta=None):
@@ -499,9 +539,11 @@ def mul_f32(a, b):
     return out
 
 
-def keep_mask(n, keep, seed, device):
+def keep_mask(n, keep, seed, device, counter=None):
+    """Bernoulli(keep)/keep mask of n floats; ``counter`` (device int64 tensor) is mixed in at run time."""
+    _chk(counter, "counter", torch.int64)
     out = torch.empty(n, device=device, dtype=torch.float32)
-    _lib.call("svk_keep_mask", _p(out), n, float(keep), int(seed) & 0xFFFFFFFF, _stream())
+    _lib.call("svk_keep_mask", _p(out), n, float(keep), int(seed) & 0xFFFFFFFF, _p(counter), _stream())
     return out
 
 

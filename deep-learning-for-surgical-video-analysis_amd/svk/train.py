@@ -109,6 +109,8 @@ class EVPTrainStep:
         self._setup_flat()
         self._setup_frozen()
         self._setup_packs()
+        self.counter = torch.zeros(1, device=self.dev, dtype=torch.int64)   # device step count (mask RNG)
+        self.graph = None
 
     # ---- parameter storage ------------------------------------------------------------------
     def _setup_flat(self):
@@ -286,20 +288,21 @@ class EVPTrainStep:
         """Device DropPath / Dropout2d masks for this step (values 0 or 1/keep)."""
         dpr = torch.linspace(0, DROP_PATH_RATE, sum(self.depths)).tolist()
         blocks, cur = [], 0
-        base = (self.seed * 1000003 + self.steps * 7919) & 0x7FFFFFFF
+        base = (self.seed * 1000003) & 0x7FFFFFFF      # the step enters through the device counter
         ones = torch.ones(B, device=self.dev, dtype=torch.float32)
         for s, d in enumerate(self.depths):
             st = []
             for i in range(d):
                 r = dpr[cur + i]
                 if self.drop and r > 0:
-                    st.append(tuple(ops.keep_mask(B, 1.0 - r, base + 2 * (cur + i) + j, self.dev) for j in range(2)))
+                    st.append(tuple(ops.keep_mask(B, 1.0 - r, base + 2 * (cur + i) + j, self.dev, self.counter)
+                                    for j in range(2)))
                 else:
                     st.append((ones, ones))
             blocks.append(st)
             cur += d
         if self.drop:
-            d2 = ops.keep_mask(B * 2048, 1.0 - HEAD_DROPOUT, base + 99991, self.dev).view(B, 2048)
+            d2 = ops.keep_mask(B * 2048, 1.0 - HEAD_DROPOUT, base + 99991, self.dev, self.counter).view(B, 2048)
         else:
             d2 = torch.ones(B, 2048, device=self.dev, dtype=torch.float32)
         return {"blocks": blocks, "dropout2d": d2}
@@ -447,10 +450,9 @@ class EVPTrainStep:
 
     # ---- backward ---------------------------------------------------------------------------------
     def _wg(self, dy, x, name, bias_name=None):
-        """Linear weight/bias gradients: dW += dy^T x; db += colsum(dy)."""
-        ops.gemm_wgrad(dy.reshape(-1, dy.shape[-1]), x.reshape(-1, x.shape[-1]), self.G(name))
-        if bias_name is not None:
-            ops.colstats(dy.reshape(-1, dy.shape[-1]), self.G(bias_name))
+        """Linear weight/bias gradients: dW += dy^T x; db += colsum(dy) (one fused kernel)."""
+        ops.gemm_wgrad(dy.reshape(-1, dy.shape[-1]), x.reshape(-1, x.shape[-1]), self.G(name),
+                       None if bias_name is None else self.G(bias_name))
 
     def _backward(self, sv, dlogits, dant):
         dt, B, pg = self.dt, sv["B"], "prompt_generator"
@@ -459,8 +461,7 @@ class EVPTrainStep:
         dfeat = None
         for h, dl, h1 in (("fc", dlogits, hd["hs"][0]), ("fc_ant", dant, hd["hs"][1])):
             self._wg(dl, h1, f"head.{h}.2.weight", f"head.{h}.2.bias")
-            dh = ops.gemm(dl, self.W32T(f"head.{h}.2.weight.T"))
-            dh = ops.act_bwd(h1, dh, "relu")
+            dh = ops.gemm(dl, self.W32T(f"head.{h}.2.weight.T"), dact="relu", dact_src=h1)
             self._wg(dh, hd["feat"], f"head.{h}.0.weight", f"head.{h}.0.bias")
             dfeat = ops.gemm(dh, self.W32T(f"head.{h}.0.weight.T"), residual=dfeat)
         # Dropout2d + average pool + BN(train) + ReLU
@@ -506,8 +507,7 @@ class EVPTrainStep:
                 # prompt: xp = x + shared(GELU(lw_i(summed)))
                 lw = f"{pg}.lightweight_mlp{s + 1}_{i}.0"
                 self._wg(d, sb["f"], sh + ".weight", sh + ".bias")
-                df = ops.gemm(d, self.W(sh + ".weight.T"))
-                dfp = ops.act_bwd(sb["fpre"], df, "gelu")
+                dfp = ops.gemm(d, self.W(sh + ".weight.T"), dact="gelu", dact_src=sb["fpre"])
                 self._wg(dfp, st["summed"], lw + ".weight", lw + ".bias")
                 dsum = ops.gemm(dfp, self.W(lw + ".weight.T"), residual=dsum, out=dsum)
             eg = f"{pg}.embedding_generator{s + 1}"
@@ -530,8 +530,8 @@ class EVPTrainStep:
                                    self.P(nm + ".norm.weight"), LN_EPS, dgamma=self.G(nm + ".norm.weight"),
                                    dbeta=self.G(nm + ".norm.bias"))
             dzm = dz.view(B, h["H"], h["W"], h["C"])
-            ops.conv2d_wgrad(h["inp"], dzm, h["k"], h["st"], h["k"] // 2, self.CG(nm + ".proj.weight"))
-            ops.colstats(dz.view(-1, h["C"]), self.G(nm + ".proj.bias"))
+            ops.conv2d_wgrad(h["inp"], dzm, h["k"], h["st"], h["k"] // 2, self.CG(nm + ".proj.weight"),
+                             self.G(nm + ".proj.bias"))
             if s > 0:
                 pin = h["inp"]
                 dh = ops.conv2d_dgrad(dzm, self.W(nm + ".proj.weight.D"), pin.shape[1], pin.shape[2], pin.shape[3],
@@ -542,27 +542,22 @@ class EVPTrainStep:
         """Data gradient through one frozen block (given d = dL/d out) -> dL/d xp."""
         N = H * W
         hid = sb["u"].shape[-1]
-        dg = ops.gemm(d, b["w2T"], row_scale=sb["mm"], rows_per=N)
-        du = ops.act_bwd(sb["u"].view(B, N, hid), dg, "gelu")
+        du = ops.gemm(d, b["w2T"], row_scale=sb["mm"], rows_per=N, dact="gelu", dact_src=sb["u"].view(B, N, hid))
         dh = ops.dwconv3x3(du.view(B, H, W, hid), b["taps_flip"], b["zero"]).view(B, N, hid)
         dxn2 = ops.gemm(dh, b["w1T"])
         d1 = ops.layernorm_bwd(sb["x1"], dxn2, b["g2"], BLOCK_EPS, dres=d)
         do = ops.gemm(d1, b["wpT"], row_scale=sb["ma"], rows_per=N)
         kv = sb["kv"]
         Nk = kv.shape[1]
-        dkv32 = torch.zeros(B, Nk, 2 * C, device=self.dev, dtype=torch.float32)
-        dq = ops.attention_bwd(sb["q"], kv[:, :, :C], kv[:, :, C:], sb["o"], do, b["heads"], b["scale"],
-                               dkv32[:, :, :C], dkv32[:, :, C:])
-        dkv = ops.cast(dkv32, self.dt)
+        dkv = torch.empty(B, Nk, 2 * C, device=self.dev, dtype=self.dt)
+        dq, _, _ = ops.attention_bwd(sb["q"], kv[:, :, :C], kv[:, :, C:], sb["o"], do, b["heads"], b["scale"],
+                                     dkv[:, :, :C], dkv[:, :, C:])
         dxs = ops.gemm(dkv, b["wkvT"])
         if b["sr"] > 1:
             r = b["sr"]
             dxs_pre = ops.layernorm_bwd(sb["xs_pre"], dxs, b["gn"], LN_EPS)
-            dpatch = ops.gemm(dxs_pre, b["wsrD"])
-            dxn1 = torch.empty(B, H, W, C, device=self.dev, dtype=self.dt)
-            ops.unpatchify(dpatch.view(-1, r * r * C), B, H // r, W // r, r, C, dxn1)
-            dxn1 = dxn1.view(B, N, C)
-            ops.gemm(dq, b["wqT"], residual=dxn1, out=dxn1)
+            dxn1 = ops.gemm(dq, b["wqT"])
+            ops.gemm_unpatchify(dxs_pre.view(-1, C), b["wsrD"], dxn1.view(B, H, W, C), r, residual=dxn1.view(B, H, W, C))
         else:
             dxn1 = ops.gemm(dq, b["wqT"], residual=dxs)
         return ops.layernorm_bwd(sb["xp"], dxn1, b["g1"], BLOCK_EPS, dres=d1)
@@ -578,16 +573,13 @@ class EVPTrainStep:
         do = ops.gemm(da, self.W(op + ".weight.T"))
         kv = ca["kv"]
         Nk = kv.shape[1]
-        dkv32 = torch.zeros(B, Nk, 2 * E, device=self.dev, dtype=torch.float32)
-        dq = ops.attention_bwd(ca["q"], kv[:, :, :E], kv[:, :, E:], ca["o"], do, heads, (E // heads) ** -0.5,
-                               dkv32[:, :, :E], dkv32[:, :, E:])
-        dkv = ops.cast(dkv32, self.dt)
+        dkv = torch.empty(B, Nk, 2 * E, device=self.dev, dtype=self.dt)
+        dq, _, _ = ops.attention_bwd(ca["q"], kv[:, :, :E], kv[:, :, E:], ca["o"], do, heads, (E // heads) ** -0.5,
+                                     dkv[:, :, :E], dkv[:, :, E:])
         ip = p + ".cross_attn.in_proj_weight"
         gW, gb = self.G(ip), self.G(p + ".cross_attn.in_proj_bias")
-        ops.gemm_wgrad(dq.reshape(-1, E), ca["c"].reshape(-1, E), gW[:E])
-        ops.colstats(dq.reshape(-1, E), gb[:E])
-        ops.gemm_wgrad(dkv.reshape(-1, 2 * E), ca["f"].reshape(-1, E), gW[E:])
-        ops.colstats(dkv.reshape(-1, 2 * E), gb[E:])
+        ops.gemm_wgrad(dq.reshape(-1, E), ca["c"].reshape(-1, E), gW[:E], gb[:E])
+        ops.gemm_wgrad(dkv.reshape(-1, 2 * E), ca["f"].reshape(-1, E), gW[E:], gb[E:])
         dc = ops.gemm(dq, self.W(ip + ".qT"), residual=da)
         df = ops.gemm(dkv, self.W(ip + ".kvT"))
         return dc, df
@@ -603,8 +595,7 @@ class EVPTrainStep:
             dz = ops.bn_bwd(z, dy.reshape(z.shape).contiguous(), L["s1"], L["s2"], self.P(bn + ".weight"),
                             self.P(bn + ".bias"), BN_EPS, self.G(bn + ".weight"), self.G(bn + ".bias"), relu=True)
             nm = f"flow_encoder.conv{i}"
-            ops.conv2d_wgrad(L["inp"], dz, L["k"], L["st"], L["pad"], self.CG(nm + ".weight"))
-            ops.colstats(dz.view(-1, dz.shape[-1]), self.G(nm + ".bias"))
+            ops.conv2d_wgrad(L["inp"], dz, L["k"], L["st"], L["pad"], self.CG(nm + ".weight"), self.G(nm + ".bias"))
             if i > 1:
                 pin = L["inp"]
                 res = dflow[3].reshape(pin.shape).contiguous() if i == 4 else None
@@ -656,20 +647,73 @@ class EVPTrainStep:
             dist.all_reduce(self.grad, group=self.group)
             self.grad.mul_(1.0 / self.world)
 
-    def optimizer_step(self):
+    def _optimizer_launch(self, first):
         h = self.hp
         ops.sgd(self.flat, self.grad, self.mom, h["lr"], h["momentum"], h["dampening"], h["weight_decay"],
-                h["nesterov"], first=self.steps == 0)
-        self.steps += 1
+                h["nesterov"], first=first)
         self._refresh_packs()
-        # the kernel wrote the parameters behind autograd's back: bump their version counters so the
+        self.counter.add_(1)
+
+    def _after_step(self):
+        self.steps += 1
+        # the kernels wrote the parameters behind autograd's back: bump their version counters so the
         # eval-mode modules re-derive their cached packs (svk.pack.PackCache)
         for p in self.params.values():
             increment_version(p)
 
+    def optimizer_step(self):
+        self._optimizer_launch(first=self.steps == 0)
+        self._after_step()
+
     def step(self, x, y, flow, labels, ant_targets, masks=None):
-        """One train_model iteration (train_evp.py:473-515): returns (loss [2], logits, anticipation)."""
+        """One train_model iteration (train_evp.py:473-515): returns (loss [2], logits, anticipation).
+        After capture() with these same input tensors, the iteration replays as one HIP graph."""
+        if self.graph is not None and masks is None and self._static == (x, y, flow, labels, ant_targets):
+            return self._replay()
         loss, logits, ant = self.forward_backward(x, y, flow, labels, ant_targets, masks)
         self.allreduce_grads()
         self.optimizer_step()
         return loss, logits, ant
+
+    # ---- HIP graph capture ----------------------------------------------------------------------
+    def capture(self, x, y, flow, labels, ant_targets):
+        """Capture one full iteration (forward, backward, SGD, re-pack) over these input tensors as a
+        HIP graph (torch.cuda.CUDAGraph drives hipStreamBeginCapture).  The ~700 kernel launches of a
+        step then cost one graph launch.  With DDP the gradient all-reduce stays outside the graph
+        (two graphs: forward/backward and optimizer).  Needs at least one eager step first (momentum
+        buffer initialised)."""
+        if self.steps == 0:
+            raise SvkError("EVPTrainStep.capture: run one eager step first")
+        self._static = (x, y, flow, labels, ant_targets)
+        ddp = self.group is not None and self.world > 1
+        bns = [self.model.head.linear_fuse.bn] + [getattr(self.model.flow_encoder, f"bn{i}") for i in range(1, 5)]
+        saved = [(bn.running_mean.clone(), bn.running_var.clone(), bn.num_batches_tracked.clone()) for bn in bns]
+        s = torch.cuda.Stream(device=self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.stream(s):        # warm the allocator's private pool outside the capture
+            self.forward_backward(*self._static)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        with torch.no_grad():             # the warm-up pass must not count as a BatchNorm update
+            for bn, (rm, rv, nb) in zip(bns, saved):
+                bn.running_mean.copy_(rm)
+                bn.running_var.copy_(rv)
+                bn.num_batches_tracked.copy_(nb)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self._gout = self.forward_backward(*self._static)
+            if not ddp:
+                self._optimizer_launch(first=False)
+        self.graph_opt = None
+        if ddp:
+            self.graph_opt = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph_opt):
+                self._optimizer_launch(first=False)
+        return self
+
+    def _replay(self):
+        self.graph.replay()
+        if self.graph_opt is not None:
+            self.allreduce_grads()
+            self.graph_opt.replay()
+        self._after_step()
+        return self._gout

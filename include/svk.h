@@ -134,20 +134,29 @@ int svk_cast(int dtype_in, const void* X, int dtype_out, void* Y, long n, void* 
 int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const float* bias, void* Y, void* Ypre, int B,
                      int H, int W, int C, int act, void* stream);
 
-/* svk_gemm plus a per-row scale s[m / rows_per_scale] applied to act(A W^T + bias) before the
- * residual add: timm DropPath (stochastic depth, mix_transformer_evp.py:168-169 in train mode)
- * fused into the branch GEMM, and its adjoint in the data-gradient GEMM. */
+/* svk_gemm plus (a) a per-row scale s[m / rows_per_scale] applied to act(A W^T + bias) before the
+ * residual add: timm DropPath (stochastic depth, mix_transformer_evp.py:168-169 in train mode) fused
+ * into the branch GEMM and its adjoint in the data-gradient GEMM; (b) an activation backward
+ * v *= uact'(U[m, n]) (U may be NULL): GELU/ReLU derivatives fused into the data-gradient GEMM. */
 int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
-                const float* row_scale, int rows_per_scale, const void* R, long ldr, void* C, long ldc,
-                int M, int N, int K, int act, void* stream);
+                const float* row_scale, int rows_per_scale, const void* U, long ldu, int uact,
+                const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act, void* stream);
 
-/* dW[n, k] += sum_m dY[m, n] * X[m, k] (f32, split-M MFMA with atomics): nn.Linear weight gradient. */
+/* Adjoint of a k = s patchify conv (Attention.sr, mix_transformer_evp.py:89, 116): GEMM rows are the
+ * [B, H/s, W/s] patches, columns (i, j, ci), stored straight into the NHWC map Y [B, H, W, C]
+ * (+ R at the same positions; R may alias Y).  K = Cout, W packed [(i, j, ci)][co]. */
+int svk_gemm_unpatchify(int dtype, const void* A, long lda, const void* W, long ldw, const void* R, void* Y,
+                        int B, int H, int Wd, int s, int C, int K, void* stream);
+
+/* dW[n, k] += sum_m dY[m, n] * X[m, k] and db[n] += sum_m dY[m, n] (db may be NULL)
+ * (f32, split-M MFMA with atomics): nn.Linear weight and bias gradients. */
 int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw,
-                   int M, int N, int K, void* stream);
+                   float* db, int M, int N, int K, void* stream);
 
-/* Conv2d weight gradient: dW[Cout][kh][kw][Cin] (packed like the forward weights) += im2col(X)^T dY. */
+/* Conv2d weight gradient: dW[Cout][kh][kw][Cin] (packed like the forward weights) += im2col(X)^T dY,
+ * db[Cout] += column sums of dY (db may be NULL). */
 int svk_conv2d_wgrad_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* dY,
-                          int Cout, int k, int stride, int pad, float* dW, void* stream);
+                          int Cout, int k, int stride, int pad, float* dW, float* db, void* stream);
 
 /* Conv2d data gradient (transposed-conv gather, power-of-two stride): dX [B,H,W,Cin] = col2im(dY) .
  * Wd packed [Cin][kh][kw][Cout]; optional R is added (R may alias dX). */
@@ -160,13 +169,18 @@ int svk_conv2d_dgrad_nhwc(int dtype, const void* dY, int B, int OH, int OW, int 
 int svk_unpatchify(int dtype, const void* P, void* Y, int B, int PH, int PW, int s, int C, int accumulate,
                    void* stream);
 
-/* Scaled-dot-product attention backward (recomputes P): dQ written, dK/dV (f32 [B, Nk, heads*hd]
- * with row stride lddk, batch stride sbdk) accumulated.  hd <= 64, Nk limited by LDS (<= ~200). */
+/* Scaled-dot-product attention backward (recomputes P): dQ, dK, dV written in the compute dtype
+ * (dK/dV [B, Nk, heads*hd] with row stride lddk and batch stride sbdk).  bf16 with hd % 8 == 0,
+ * hd <= 64, Nk <= 256: MFMA path (dQ kernel that also stores P and scale*dS, then batched MFMA
+ * reductions dK = dS^T Q, dV = P^T dO); otherwise an LDS scalar path.  ws: caller-owned scratch of
+ * at least svk_attention_bwd_workspace(...) bytes.  Replaces autograd through
+ * mix_transformer_evp.py:123-127 and nn.MultiheadAttention (:868-883) in train_evp.py:512. */
+long svk_attention_bwd_workspace(int dtype, int B, int Nq, int Nk, int heads, int hd);
 int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, const void* K, long ldk, long sbk,
                       const void* V, long ldv, long sbv, const void* O, long ldo, long sbo,
-                      const void* dO, long lddo, long sbdo, void* dQ, long lddq, long sbdq, float* dK,
-                      float* dV, long lddk, long sbdk, int B, int Nq, int Nk, int heads, int hd, float scale,
-                      void* stream);
+                      const void* dO, long lddo, long sbdo, void* dQ, long lddq, long sbdq, void* dK,
+                      void* dV, long lddk, long sbdk, void* ws, long ws_bytes, int B, int Nq, int Nk, int heads,
+                      int hd, float scale, void* stream);
 
 /* LayerNorm backward (recomputes mean/rstd from X): dX = LN'(dY) (+ dR); dgamma/dbeta += (both or
  * neither; NULL for frozen norms).  C <= 512. */
@@ -204,8 +218,9 @@ int svk_bcast_rows(int dtype, const float* dF, const float* mask, float scale, v
 int svk_row_scale(int dtype, const void* X, const float* s, void* Y, long M, int C, int rows_per, void* stream);
 int svk_mul_f32(const float* a, const float* b, float* y, long n, void* stream);
 
-/* Counter-based Bernoulli(keep) mask scaled by 1/keep (values 0 or 1/keep): DropPath / Dropout2d. */
-int svk_keep_mask(float* out, long n, float keep, unsigned seed, void* stream);
+/* Counter-based Bernoulli(keep) mask scaled by 1/keep (values 0 or 1/keep): DropPath / Dropout2d.
+ * counter (device int64, may be NULL) is mixed into the seed at run time (graph replays). */
+int svk_keep_mask(float* out, long n, float keep, unsigned seed, const long long* counter, void* stream);
 
 /* CrossEntropyLoss(sum) + SmoothL1Loss(sum) (train_evp.py:390-391, 500-509): loss[0] += CE,
  * loss[1] += SmoothL1; dlogits / dant are the gradients of their sum. */

@@ -18,7 +18,7 @@ def _header_functions():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     out = {}
-    for m in re.finditer(r"\b(?:int|const char\*)\s+(svk_\w+)\s*\(([^)]*)\)\s*;", src):
+    for m in re.finditer(r"\b(?:int|long|const char\*)\s+(svk_\w+)\s*\(([^)]*)\)\s*;", src):
         args = [a.strip() for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
         out[m.group(1)] = len(args)
     return out
@@ -33,9 +33,11 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, name), f"{name} declared in svk.h but not exported"
         if name in _lib.SIGNATURES:
             assert len(_lib.SIGNATURES[name]) == nargs, f"{name}: ctypes binding has wrong arity"
+        elif name in _lib.LONG_FUNCS:
+            assert len(_lib.LONG_FUNCS[name]) == nargs, f"{name}: ctypes binding has wrong arity"
         else:
             assert name in _lib.STRING_FUNCS
-    assert set(_lib.SIGNATURES) | set(_lib.STRING_FUNCS) == set(funcs)
+    assert set(_lib.SIGNATURES) | set(_lib.STRING_FUNCS) | set(_lib.LONG_FUNCS) == set(funcs)
 
 
 def test_library_version_and_error_path():

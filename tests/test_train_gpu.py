@@ -99,9 +99,11 @@ def test_gemm_wgrad(cuda, dt, M, N, K):
     from svk import ops
     dy, x = _rand(M, N, seed=1), _rand(M, K, seed=2)
     dw = torch.full((N, K), 0.5, device=cuda)
-    ops.gemm_wgrad(dy.to(cuda, dt), x.to(cuda, dt), dw)
+    db = torch.full((N,), 0.25, device=cuda)
+    ops.gemm_wgrad(dy.to(cuda, dt), x.to(cuda, dt), dw, db)
     ref = dy.to(dt).double().t() @ x.to(dt).double() + 0.5
     _close(dw, ref, 1e-5 if dt == torch.float32 else 1e-2)
+    _close(db, dy.to(dt).double().sum(0) + 0.25, 1e-5 if dt == torch.float32 else 1e-2)
 
 
 def _conv_case(B, Cin, H, Cout, k, s, seed):
@@ -125,10 +127,12 @@ def test_conv_wgrad_dgrad(cuda, dt, B, Cin, H, Cout, k, s):
     xn = ops.nchw_to_nhwc(x.to(cuda), dt, cpad=cp)
     dyn = dy.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
     dwp = torch.zeros(Cout, k * k * cp, device=cuda)
-    ops.conv2d_wgrad(xn, dyn, k, s, k // 2, dwp)
+    dbias = torch.zeros(Cout, device=cuda)
+    ops.conv2d_wgrad(xn, dyn, k, s, k // 2, dwp, dbias)
     dw = dwp.view(Cout, k, k, cp)[..., :Cin].permute(0, 3, 1, 2)
     tol = 1e-4 if dt == torch.float32 else 2e-2
     _close(dw, wr.grad, tol)
+    _close(dbias, dy.sum((0, 2, 3)), tol)
     if Cin >= 8:
         wd = w.permute(1, 2, 3, 0).reshape(Cin, k * k * Cout).to(cuda, dt).contiguous()
         res = _rand(B, H, H, Cin, seed=11).to(cuda, dt)
@@ -146,10 +150,16 @@ def test_patchify_adjoint(cuda):
     dy = _rand(*y.shape, seed=3).double()
     y.backward(dy)
     wd = w.permute(2, 3, 1, 0).reshape(r * r * C, C).float().to(cuda)
-    dp = ops.gemm(dy.permute(0, 2, 3, 1).reshape(-1, C).float().to(cuda), wd)
+    dyt = dy.permute(0, 2, 3, 1).reshape(-1, C).float().to(cuda)
+    dp = ops.gemm(dyt, wd)
     dx = torch.empty(B, H, H, C, device=cuda)
     ops.unpatchify(dp, B, H // r, H // r, r, C, dx)
     _close(dx, x.grad.permute(0, 2, 3, 1), 1e-5)
+    # the same adjoint stored straight from the GEMM epilogue, accumulating onto a residual
+    res = _rand(B, H, H, C, seed=4).to(cuda)
+    dx2 = res.clone()
+    ops.gemm_unpatchify(dyt, wd, dx2, r, residual=dx2)
+    _close(dx2, x.grad.permute(0, 2, 3, 1) + res.cpu(), 1e-5)
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
@@ -167,8 +177,8 @@ def test_attention_bwd(cuda, dt, Nq, Nk, heads, hd):
     o.backward(do.to(dt).double())
     qc, kc, vc = (t.to(cuda, dt) for t in (q, k, v))
     oc = ops.attention(qc, kc, vc, heads, scale)
-    dkv = torch.zeros(B, Nk, 2 * C, device=cuda)
-    dq = ops.attention_bwd(qc, kc, vc, oc, do.to(cuda, dt), heads, scale, dkv[:, :, :C], dkv[:, :, C:])
+    dkv = torch.zeros(B, Nk, 2 * C, device=cuda, dtype=dt)
+    dq, _, _ = ops.attention_bwd(qc, kc, vc, oc, do.to(cuda, dt), heads, scale, dkv[:, :, :C], dkv[:, :, C:])
     tol = 1e-4 if dt == torch.float32 else 3e-2
     _close(dq, qr.grad, tol)
     _close(dkv[:, :, :C], kr.grad, tol)
@@ -199,6 +209,21 @@ def test_phase_loss_and_sgd(cuda):
         opt.step()
         ops.sgd(pc, g.to(cuda), buf, 5e-4, 0.9, 0.0, 1e-5, False, first=i == 0)
     _close(pc, pt.detach(), 1e-6)
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", ["gelu", "relu"])
+def test_gemm_activation_backward_epilogue(cuda, dt, act):
+    from svk import ops
+    M, N, K = 300, 96, 64
+    a, w, u = _rand(M, K, seed=1), _rand(N, K, seed=2, scale=0.1), _rand(M, N, seed=3)
+    s = torch.rand(3, generator=torch.Generator().manual_seed(4))
+    ur = u.to(dt).double().requires_grad_(True)
+    (F.gelu(ur) if act == "gelu" else F.relu(ur)).backward(a.to(dt).double() @ w.to(dt).double().t()
+                                                           * s.double().repeat_interleave(100)[:, None])
+    out = ops.gemm(a.to(cuda, dt), w.to(cuda, dt), row_scale=s.to(cuda), rows_per=100, dact=act,
+                   dact_src=u.to(cuda, dt))
+    _close(out, ur.grad, 1e-5 if dt == torch.float32 else 2e-2)
 
 
 def test_gemm_row_scale_and_dwconv_pre(cuda):
@@ -273,7 +298,7 @@ def test_train_step_grads_fp32_vs_oracle(cuda, variant):
     bad = []
     for n in names:
         a, b = tr.params[n].grad.detach().double().cpu(), grads[n]
-        scale = max(b.abs().max().item(), 1e-5 * gmax)
+        scale = max(b.abs().max().item(), 1e-3 * gmax)
         err = (a - b).abs().max().item()
         if err > 2e-3 * scale:
             bad.append(f"{n}: err {err:.3e} scale {scale:.3e}")
@@ -345,3 +370,41 @@ def test_train_loss_decreases(cuda):
         losses.append(loss.sum().item())
     assert all(np.isfinite(losses))
     assert losses[-1] < losses[0], losses
+
+
+def test_train_graph_replay_matches_eager(cuda):
+    """capture() + replays reproduce the eager iterations (same masks via the device step counter,
+    same SGD trajectory and BatchNorm buffers), to within the run-to-run spread of two eager runs
+    (f32 atomics make the bf16 step non-bit-reproducible)."""
+    variant = "mit_b0_evp"
+    B = 4
+    x, y, fl, lab, at = (t.to(cuda) for t in _train_inputs(B, 6))
+    runs = []
+    for mode in ("eager", "eager", "graph"):
+        m, _, t = _build(variant, cuda, torch.bfloat16)
+        p0 = {n: p.detach().clone() for n, p in t.params.items()}
+        if mode == "eager":
+            for _ in range(3):
+                t.step(x, y, fl, lab, at)
+        else:
+            t.step(x, y, fl, lab, at)
+            t.capture(x, y, fl, lab, at)
+            for _ in range(2):
+                t.step(x, y, fl, lab, at)
+        torch.cuda.synchronize()
+        assert t.steps == 3
+        assert int(m.head.linear_fuse.bn.num_batches_tracked) == 3
+        runs.append(({n: (p - p0[n]).double() for n, p in t.params.items()}, m.head.linear_fuse.bn.running_mean.clone()))
+    (ua, ra), (ub, rb), (ug, rg) = runs
+    report = []
+    worst = 0.0
+    for n in ua:
+        scale = ua[n].abs().max().item() + 1e-12
+        ee = (ua[n] - ub[n]).abs().max().item() / scale
+        eg = (ua[n] - ug[n]).abs().max().item() / scale
+        worst = max(worst, eg / max(ee, 1e-3))
+        report.append((eg, ee, n))
+    report.sort(reverse=True)
+    print("graph-vs-eager / eager-vs-eager relative update differences (worst 5):", report[:5])
+    assert worst <= 5.0, report[:5]
+    _close(rg, ra, 1e-2)
