@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(REPO, "deep-learning-for-surgical-video-analysis
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
 PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}     # MI355X dense MFMA (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0                              # MI355X HBM3E
 DATA = "synthetic (seeded Cholec80-shaped frames/segmaps/flow, resident in HBM; random-init weights)"
 
 
@@ -304,12 +305,21 @@ def main():
                         f"{nb / ms / 1e6:8.1f} GB/s  {shape:28s} {name}\n")
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
-    achieved = flops / (ms * 1e-3) / 1e12
     peak = PEAK_TFLOPS[args.dtype if args.workload != "mstcn" else "fp32"]
-    roofline = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+    # bound by arithmetic intensity vs the machine balance (peak FLOP/s / 8 TB/s): tall-skinny
+    # token GEMMs (K or N <= 128) are HBM-bound, the head / 4096-wide GEMMs MFMA-bound
+    intensity = flops / max(nbytes, 1)
+    hbm_bound = intensity < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    tflops = flops / (ms * 1e-3) / 1e12
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm" if hbm_bound else "mfma", "kernel": name,
+                "achieved": round(gbs if hbm_bound else tflops, 2), "peak": HBM_PEAK_GBS if hbm_bound else peak,
+                "unit": "GB/s" if hbm_bound else "TFLOP/s",
+                "frac": round(gbs / HBM_PEAK_GBS if hbm_bound else tflops / peak, 4), "traffic": None,
                 "launches_per_step": n // prof_steps, "avg_launch_us": round(ms * 1e3 / n, 2),
-                "algorithmic_flop_per_launch": flops / n,
+                "algorithmic_flop_per_launch": flops / n, "algorithmic_bytes_per_launch": nbytes / n,
+                "arith_intensity_flop_per_byte": round(intensity, 1),
+                "kernel_tflops": round(tflops, 2), "kernel_gbs": round(gbs, 1),
                 "all_gemm_tflops": round(sum(v[1] for v in per.values()) / (gemm_ms * 1e-3) / 1e12, 2),
                 "gemm_share_of_step": round(gemm_ms / prof_steps / (elapsed * 1e3 / args.steps), 3)}
 

@@ -134,7 +134,7 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
         es = a.element_size()
         vw = 16 // es
         vec = a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and lda % vw == 0 and w.stride(0) % vw == 0
-        nb = (M * K + N * K + M * N * (2 if residual is not None else 1)) * es
+        nb = (M * K + N * K + M * N * (1 + (residual is not None) + (dact is not None))) * es
         _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0, row_scale is not None or dact is not None),
                   2.0 * M * N * K, nb, (M, N, K))
     return out

@@ -408,3 +408,52 @@ def test_train_graph_replay_matches_eager(cuda):
     print("graph-vs-eager / eager-vs-eager relative update differences (worst 5):", report[:5])
     assert worst <= 5.0, report[:5]
     _close(rg, ra, 1e-2)
+
+
+def _ddp_rank(rank, world, port, out):
+    import os
+    import sys
+    import torch.distributed as dist
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "deep-learning-for-surgical-video-analysis_amd"), repo]
+    from models import mix_transformer_evp as mte
+    from svk.train import EVPTrainStep
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = mte.mit_b0_evp()
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
+    m = m.to(dev)
+    if rank == 1:                      # diverge rank 1's BN buffers: the step must re-sync them from rank 0
+        m.head.linear_fuse.bn.running_mean.add_(1.0)
+    tr = EVPTrainStep(m, dtype=torch.float32, drop=False, process_group=dist.group.WORLD, world_size=world)
+    x, y, fl, lab, at = (t.to(dev) for t in _train_inputs(2, 20 + rank))
+    rm_before = m.head.linear_fuse.bn.running_mean.clone()
+    tr.forward_backward(x, y, fl, lab, at)
+    local = tr.grad.clone()
+    tr.allreduce_grads()
+    avg = tr.grad.clone()
+    tr.optimizer_step()
+    torch.cuda.synchronize()
+    out[rank] = (local.cpu(), avg.cpu(), tr.flat.detach().cpu(), rm_before.cpu())
+    dist.destroy_process_group()
+
+
+def test_train_ddp_two_ranks_gloo(cuda):
+    """DDP semantics of the train step with 2 ranks (gloo over the one GPU of the test box; the
+    bench's multi-GPU runs use RCCL): averaged gradients, identical parameters after the step."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = mp.Manager().dict()
+    mp.spawn(_ddp_rank, args=(2, port, out), nprocs=2, join=True)
+    (l0, a0, p0, _), (l1, a1, p1, _) = out[0], out[1]
+    torch.testing.assert_close(a0, (l0 + l1) / 2, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(a1, a0)
+    torch.testing.assert_close(p1, p0)
+    assert not torch.equal(l0, l1)                 # the ranks really saw different frames
