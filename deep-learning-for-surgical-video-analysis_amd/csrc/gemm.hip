@@ -300,10 +300,7 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
   __syncthreads();
 
   const int fr = lane & 15, fk = (lane >> 4) * 8;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    fetch((kt + 1) * BK);     // past the end: clamped addresses, fully masked (no branch in the loop)
-    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
+  auto compute = [&](int buf) {
 #pragma unroll
     for (int ks = 0; ks < BK / 32; ++ks) {
       Chunk<T> fa[TM], fb[TN];
@@ -318,9 +315,19 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) mfma_step<T>(fa[i], fb[j], acc[i][j]);
     }
+  };
+  // steady state: prefetch K-step kt+1 into registers while the MFMAs of kt run; the last step is
+  // peeled (no dead prefetch / stash / barrier on the critical path — K = 64 GEMMs have one step)
+  for (int kt = 0; kt < nk - 1; ++kt) {
+    const int buf = kt & 1;
+    fetch((kt + 1) * BK);
+    __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of this step's MFMAs
+    compute(buf);
     stash(buf ^ 1);
     __syncthreads();
   }
+  compute((nk - 1) & 1);
+  __syncthreads();                       // sC (epilogue) aliases the operand buffers
 
   if constexpr (!EXT) {
     // Plain epilogue (bias + act + residual).  Part 1: bias + activation in registers, f32 tile -> LDS.
@@ -373,7 +380,6 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
     }
   } else {
     // Extended epilogue: + row scale (stochastic depth), activation backward (U), unpatchify store.
-  // Epilogue.
   T* C = static_cast<T*>(p.C);
   const T* R = static_cast<const T*>(p.R);
   const T* U = static_cast<const T*>(p.U);

@@ -113,6 +113,9 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
         _, rc, ldr = _rows(residual, "residual")
         if rc != N:
             raise _lib.SvkError("svk.gemm: residual width mismatch")
+    if (SKINNY and row_scale is None and a.dtype == torch.bfloat16 and N <= 64 and K <= 128 and M >= 2048
+            and a.data_ptr() % 16 == 0 and (K % 8 or lda % 8 == 0)):
+        return gemm_skinny(a, w, bias, act, residual, out, N, dact, dact_src)
     t0 = _prof_begin()
     if row_scale is None and dact is None:
         _lib.call("svk_gemm", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
@@ -137,6 +140,30 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
         nb = (M * K + N * K + M * N * (1 + (residual is not None) + (dact is not None))) * es
         _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0, row_scale is not None or dact is not None),
                   2.0 * M * N * K, nb, (M, N, K))
+    return out
+
+
+SKINNY = os.environ.get("SVK_SKINNY", "1") == "1"
+
+
+def gemm_skinny(a, w, bias=None, act=None, residual=None, out=None, n=None, dact=None, dact_src=None):
+    """svk_gemm_skinny (bf16, N <= 64, K <= 128): same contract as gemm() without row_scale."""
+    _chk(a, "a", torch.bfloat16); _chk(w, "w", torch.bfloat16); _chk(bias, "bias", torch.float32)
+    _chk(residual, "residual", torch.bfloat16); _chk(dact_src, "dact_src", torch.bfloat16)
+    M, K, lda = _rows(a, "a")
+    N = w.shape[0] if n is None else n
+    if w.shape[1] != K or w.stride(1) != 1:
+        raise _lib.SvkError("svk.gemm_skinny: weight shape mismatch")
+    if out is None:
+        out = torch.empty(*a.shape[:-1], N, device=a.device, dtype=a.dtype)
+    _, _, ldc = _rows(out, "out")
+    ldr = _rows(residual, "residual")[2] if residual is not None else 0
+    ldu = _rows(dact_src, "dact_src")[2] if dact_src is not None else 0
+    t0 = _prof_begin()
+    _lib.call("svk_gemm_skinny", _p(a), lda, _p(w), w.stride(0), _p(bias), _p(dact_src), ldu, ACT[dact],
+              _p(residual), ldr, _p(out), ldc, M, N, K, ACT[act], _stream())
+    _prof_end(t0, "skinny_gemm", 2.0 * M * N * K,
+              (M * K + N * K + M * N * (1 + (residual is not None) + (dact is not None))) * 2, (M, N, K, "skinny"))
     return out
 
 
@@ -349,10 +376,25 @@ def gemm_wgrad(dy, x, dw, db=None):
     if db is not None and (db.numel() != N or not db.is_contiguous()):
         raise _lib.SvkError("svk.gemm_wgrad: db shape mismatch")
     t0 = _prof_begin()
-    _lib.call("svk_gemm_wgrad", dtype_code(dy.dtype), _p(dy), ldy, _p(x), ldx, _p(dw), lddw, _p(db), M, N, K,
-              _stream())
-    _prof_end(t0, "wgrad_kernel", 2.0 * M * N * K, (M * (N + K)) * dy.element_size() + N * K * 4, (M, N, K, "wgrad"))
+    if SKINNY and _skinny_wgrad_ok(dy, x, M, N, K):
+        _lib.call("svk_wgrad_skinny", _p(dy), ldy, _p(x), ldx, _p(dw), lddw, _p(db), M, N, K, _stream())
+        name = "skinny_wgrad"
+    else:
+        _lib.call("svk_gemm_wgrad", dtype_code(dy.dtype), _p(dy), ldy, _p(x), ldx, _p(dw), lddw, _p(db), M, N, K,
+                  _stream())
+        name = "wgrad_kernel"
+    _prof_end(t0, name, 2.0 * M * N * K, (M * (N + K)) * dy.element_size() + N * K * 4, (M, N, K, "wgrad"))
     return dw
+
+
+def _pow2_tiles(x):
+    t = (x + 15) // 16
+    return 1 if t <= 1 else 2 if t <= 2 else 4 if t <= 4 else 8 if t <= 8 else 99
+
+
+def _skinny_wgrad_ok(dy, x, M, N, K):
+    return (dy.dtype == torch.bfloat16 and M >= 2048 and _pow2_tiles(N) * _pow2_tiles(K) <= 16
+            and dy.data_ptr() % 16 == 0 and x.data_ptr() % 16 == 0)
 
 
 def conv2d_wgrad(x, dy, k, stride, pad, dw, db=None):

@@ -148,6 +148,18 @@ int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, long ldw, con
 int svk_gemm_unpatchify(int dtype, const void* A, long lda, const void* W, long ldw, const void* R, void* Y,
                         int B, int H, int Wd, int s, int C, int K, void* stream);
 
+/* Skinny bf16 GEMM for the prompt path (PromptGenerator Linears, mix_transformer_evp.py:749-815):
+ * C = act(A W^T + bias) * uact'(U) + R with N <= 64, K <= 128 (W held in LDS, A streamed in the MFMA
+ * operand layout); same semantics as svk_gemm_ex without row scale.  A 16-byte aligned. */
+int svk_gemm_skinny(const void* A, long lda, const void* W, long ldw, const float* bias, const void* U, long ldu,
+                    int uact, const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act,
+                    void* stream);
+
+/* Skinny bf16 weight gradient: dW[N, K] += dY^T X, db[N] += colsum(dY) for N, K <= 128 with
+ * ceil(N/16) * ceil(K/16) <= 16 (rounded to powers of two). */
+int svk_wgrad_skinny(const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw, float* db, int M,
+                     int N, int K, void* stream);
+
 /* dW[n, k] += sum_m dY[m, n] * X[m, k] and db[n] += sum_m dY[m, n] (db may be NULL)
  * (f32, split-M MFMA with atomics): nn.Linear weight and bias gradients. */
 int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw,

