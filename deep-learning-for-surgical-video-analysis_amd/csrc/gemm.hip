@@ -29,31 +29,13 @@
 // ASRC = 1 turns the A loader into an im2col gather from an NHWC map (implicit-GEMM
 // convolution, weights packed [Cout][kh][kw][Cin] so that k = (i*kw + j)*Cin + ci).
 #include "svk_common.h"
+#include "gemm_args.h"
+#include <stdio.h>
 
 namespace svk {
 
 constexpr int NTHREADS = 256;
 
-struct GemmArgs {
-  const void* A; long lda;
-  const void* W; long ldw;
-  const float* bias;
-  const void* R; long ldr;
-  void* C; long ldc;
-  int M, N, K, act;
-  int vec_out;          // C (and R) rows 16-byte aligned with whole chunks -> vector epilogue
-  // implicit-GEMM conv geometry.  ASRC == 1 (forward im2col): source map H x Wd x Cin, GEMM rows
-  // are the OH x OW output pixels.  ASRC == 2 (data gradient, transposed-conv gather): source map
-  // is dY (H x Wd x Cin = OHy x OWy x Cout), GEMM rows are the OH x OW input pixels of the conv.
-  int H, Wd, Cin, OH, OW, kw, stride, pad;
-  int sshift;           // log2(stride) (ASRC == 2)
-  const float* rscale;  // optional per-row scale of act(A W^T + bias) before the residual add
-  int rdiv;             //   rscale index = m / rdiv (stochastic depth: rdiv = tokens per frame)
-  const void* U; long ldu; int uact;   // optional activation backward: v *= act'(U[m, n]) (same dtype as C)
-  // out_mode 1: C (and R) are an NHWC map [B, uH, uW, uC] and GEMM row m = (b, py, px) of the
-  // (uH/us) x (uW/us) patch grid, column n = (i, j, ci): the adjoint of a k = s patchify conv.
-  int out_mode, uH, uW, us, uC;
-};
 
 template <typename T> struct Chunk { T v[8]; };
 
@@ -478,10 +460,19 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
   a.vec_out = aligned16(a.C) && (a.ldc % vw == 0) && (!a.R || (aligned16(a.R) && a.ldr % vw == 0)) &&
               (!a.U || (aligned16(a.U) && a.ldu % vw == 0)) && (a.out_mode == 0 || a.uC % 8 == 0);
   const bool ext = a.rscale || a.U || a.out_mode;
+  if constexpr (sizeof(T) == 2 && ASRC == 0) {
+    if (vec && !ext && gemm_pk_try(a, st) == 0) return SVK_OK;
+  }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;
     const long nwg = (long)((M + BM - 1) / BM) * ((N + BN - 1) / BN);
     dim3 grid((unsigned)nwg);
+    static char names[2][2][96];
+    char* nm = names[vec][ext];
+    if (!nm[0])
+      snprintf(nm, 96, "gemm_kernel<%s, %d, %d, %s, %d, %s>", sizeof(T) == 2 ? "__bf16" : "float", BM, BN,
+               vec ? "true" : "false", ASRC, ext ? "true" : "false");
+    set_last_kernel(nm);
     if (ext) {
       if (vec) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, ASRC, true>), grid, dim3(NTHREADS), 0, st, a);
       else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, ASRC, true>), grid, dim3(NTHREADS), 0, st, a);

@@ -1,0 +1,32 @@
+// Argument block of the GEMM / implicit-GEMM conv kernels (gemm.hip, gemm_pk.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace svk {
+
+struct GemmArgs {
+  const void* A; long lda;
+  const void* W; long ldw;
+  const float* bias;
+  const void* R; long ldr;
+  void* C; long ldc;
+  int M, N, K, act;
+  int vec_out;          // C (and R) rows 16-byte aligned with whole chunks -> vector epilogue
+  // implicit-GEMM conv geometry.  ASRC == 1 (forward im2col): source map H x Wd x Cin, GEMM rows
+  // are the OH x OW output pixels.  ASRC == 2 (data gradient, transposed-conv gather): source map
+  // is dY (H x Wd x Cin = OHy x OWy x Cout), GEMM rows are the OH x OW input pixels of the conv.
+  int H, Wd, Cin, OH, OW, kw, stride, pad;
+  int sshift;           // log2(stride) (ASRC == 2)
+  const float* rscale;  // optional per-row scale of act(A W^T + bias) before the residual add
+  int rdiv;             //   rscale index = m / rdiv (stochastic depth: rdiv = tokens per frame)
+  const void* U; long ldu; int uact;   // optional activation backward: v *= act'(U[m, n]) (same dtype as C)
+  // out_mode 1: C (and R) are an NHWC map [B, uH, uW, uC] and GEMM row m = (b, py, px) of the
+  // (uH/us) x (uW/us) patch grid, column n = (i, j, ci): the adjoint of a k = s patchify conv.
+  int out_mode, uH, uW, us, uC;
+};
+
+// gemm_pk.hip: persistent LDS-DMA bf16 GEMM for the dense plain-epilogue case; returns 0 when it
+// launched, 1 when the arguments are not eligible (caller falls back to gemm_kernel).
+int gemm_pk_try(const GemmArgs& a, hipStream_t st);
+
+}  // namespace svk

@@ -1,0 +1,296 @@
+// Persistent, LDS-DMA-pipelined bf16 MFMA GEMM for the token GEMMs of the MiT/SegFormer path.
+//
+//   C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]        (bf16 in/out, f32 accumulate)
+//
+// Why persistent: most of the path's GEMMs have a short reduction (K = 64..512, i.e. 1..8 K-steps of
+// 64), so in a one-tile-per-workgroup kernel every tile pays the full global-load latency of its
+// first K-step and the drain of its epilogue with nothing to overlap them.  Here a fixed grid of
+// (CUs x resident workgroups) walks a continuous stream of (tile, K-step) pairs: the LDS-DMA for the
+// NEXT step — which at a tile boundary is the next tile's first step — is in flight while the MFMAs
+// of the current step run, so tile prologues are hidden behind the previous tile's last step.
+//
+// Staging: `global_load_lds_dwordx4` (no VGPR round trip, no ds_write pass).  The DMA writes each
+// wave-instruction's 64 x 16 B lane-linearly, so the LDS image is unpadded [rows][64 k] (128-B rows)
+// and the bank-conflict swizzle is applied on the SOURCE address: LDS chunk c' of row r holds global
+// 16-B chunk c' ^ (r & 7) — which makes every ds_read_b128 fragment read of the 16x16x32 MFMA
+// conflict-free (each 16-lane group hits 16 distinct 16-B bank slots).  K tails read a 16-byte
+// zero block instead of the operand (no masking instructions); rows past M / N are clamped (their
+// outputs are never stored).
+//
+// The MFMA is issued as W-fragment x A-fragment, i.e. it computes the tile transposed: each lane
+// then holds 4 consecutive output COLUMNS of one row, so the fused epilogue (bias, activation,
+// residual in f32, one rounding) stores 8-byte row pieces straight from the accumulators — no LDS
+// round trip and no extra barrier at tile boundaries.
+//
+// Synchronisation per K-step: issue DMA(next) -> s_waitcnt vmcnt(#DMA of next) (own DMA of the
+// current step landed) -> s_barrier (everyone's landed) -> fragment reads + MFMAs -> s_barrier
+// (nobody still reads the buffer the following step's DMA overwrites).  Raw s_barrier, never
+// __syncthreads (its fence would drain the in-flight DMA).
+#include "svk_common.h"
+#include "gemm_args.h"
+#include <stdio.h>
+#include <type_traits>
+
+namespace svk {
+
+__device__ __attribute__((aligned(16))) uint4 g_pk_zero[4];   // 64 zero bytes: the K-tail source
+
+typedef __attribute__((address_space(1))) void* gas_ptr;
+typedef __attribute__((address_space(3))) void* las_ptr;
+
+// Tile BM x BN x 64, WGM x WGN waves (each owning a (BM/WGM) x (BN/WGN) sub-tile of 16x16 MFMA
+// blocks), an NSTAGE-deep ring of LDS stages (the DMA runs NSTAGE-1 steps ahead).
+template <int BM_, int BN_, int WGM_, int WGN_, int NSTAGE_>
+struct PkCfg {
+  static constexpr int BM = BM_, BN = BN_, WGM = WGM_, WGN = WGN_, NSTAGE = NSTAGE_;
+  static constexpr int NT = 64 * WGM * WGN;
+  static constexpr int BK = 64;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES;
+  static constexpr int LDS = NSTAGE * STAGE;
+  static constexpr int A_LD = A_BYTES / (NT * 16);   // DMA instructions per thread per K-step
+  static constexpr int B_LD = B_BYTES / (NT * 16);
+  static constexpr int LD = A_LD + B_LD;
+  static_assert(A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "tile must split into whole DMA rounds");
+  static_assert(LD * (NSTAGE - 1) <= 63, "vmcnt range");
+};
+
+__device__ __forceinline__ int pk_xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// LDS-DMA issued from inline asm: hipcc does not track it, so it neither drains it with vmcnt(0)
+// before fragment reads of another stage nor before the next DMA (cdna_hip_programming.md §5.7);
+// completion is counted by hand (vmcnt; loads return in order).  M0 is saved/restored around it.
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void barrier_mem() { asm volatile("s_barrier" ::: "memory"); }
+
+template <int LD>
+__device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current stage landed
+  switch (pend) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LD) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LD) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LD) : "memory"); break;
+  }
+}
+
+template <class Cfg, bool KTAIL>
+__global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, int ntn, int ntiles, int nk) {
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
+  constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(1024))) char smem[Cfg::LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cfg::WGN, wn = wave % Cfg::WGN;
+  const bf16* A = static_cast<const bf16*>(p.A);
+  const bf16* Wt = static_cast<const bf16*>(p.W);
+  const int G = gridDim.x;
+  const int first = pk_xcd_remap(blockIdx.x, G);
+  if (first >= ntiles) return;
+  const char* zero = reinterpret_cast<const char*>(g_pk_zero);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
+
+  // this thread's DMA lane covers 16-byte chunk q = (wave * LD + i) * 64 + lane of the stage image
+  auto issue = [&](int tile, int kt, int buf) {
+    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN, k0 = kt * Cfg::BK;
+    const uint32_t sa = lds0 + buf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
+#pragma unroll
+    for (int i = 0; i < Cfg::A_LD; ++i) {
+      const int q = (wave * Cfg::A_LD + i) * 64 + lane;
+      const int r = q >> 3, c = (q & 7) ^ (r & 7);
+      const int m = min(m0 + r, p.M - 1), k = k0 + c * 8;
+      const char* src = reinterpret_cast<const char*>(A + (long)m * p.lda + k);
+      if constexpr (KTAIL) src = k < p.K ? src : zero;
+      dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
+    }
+#pragma unroll
+    for (int i = 0; i < Cfg::B_LD; ++i) {
+      const int q = (wave * Cfg::B_LD + i) * 64 + lane;
+      const int r = q >> 3, c = (q & 7) ^ (r & 7);
+      const int n = min(n0 + r, p.N - 1), k = k0 + c * 8;
+      const char* src = reinterpret_cast<const char*>(Wt + (long)n * p.ldw + k);
+      if constexpr (KTAIL) src = k < p.K ? src : zero;
+      dma16(src, __builtin_amdgcn_readfirstlane(sb + (wave * Cfg::B_LD + i) * 1024));
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+  auto compute = [&](int buf) {
+    const char* sa = smem + buf * Cfg::STAGE;
+    const char* sb = sa + Cfg::A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int cc = ((ks * 4 + fq) ^ (fr & 7)) * 16;   // swizzled chunk of this lane's 8 k
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * WM + i * 16 + fr) * 128 + cc);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // The bias is loaded BEFORE the tile's last K-step so that its latency hides behind the MFMAs;
+  // the residual is loaded at the start of the epilogue (all loads first, then the math) — holding
+  // it across the last step would cost 2 VGPRs per accumulator block and halve the occupancy.
+  // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
+  float4 ebias[TN];
+  const bf16* R = static_cast<const bf16*>(p.R);
+  auto epi_load = [&](int tile) {
+    const int n0 = (tile % ntn) * BN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
+      ebias[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto epilogue = [&](int tile, auto act_c) {
+    constexpr int ACT = decltype(act_c)::value;
+    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+    bf16* C = static_cast<bf16*>(p.C);
+    uint2 eres[TM][TN];
+    if (R) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
+          const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+          eres[i][j] = *reinterpret_cast<const uint2*>(R + (long)m * p.ldr + n);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + fq * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * WM + i * 16 + fr;
+        float v[4] = {acc[i][j][0] + ebias[j].x, acc[i][j][1] + ebias[j].y, acc[i][j][2] + ebias[j].z,
+                      acc[i][j][3] + ebias[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
+        if (R) {
+          v[0] += __uint_as_float(eres[i][j].x << 16);
+          v[1] += __uint_as_float(eres[i][j].x & 0xFFFF0000u);
+          v[2] += __uint_as_float(eres[i][j].y << 16);
+          v[3] += __uint_as_float(eres[i][j].y & 0xFFFF0000u);
+        }
+        bf16 o[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        if (m < p.M && n < p.N)   // N % 4 == 0: a 4-column group is all-in or all-out
+          *reinterpret_cast<uint2*>(C + (long)m * p.ldc + n) = *reinterpret_cast<const uint2*>(o);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+
+  // DMA issue cursor: the (tile, K-step) stream of this workgroup, up to NSTAGE steps in flight
+  // (the current one included); `inflight` counts issued steps not yet computed.
+  int itile = first, ikt = 0, ibuf = 0, inflight = 0, buf = 0;
+  auto issue_next = [&]() {
+    if (itile >= ntiles) return;
+    issue(itile, ikt, ibuf);
+    ++inflight;
+    ibuf = ibuf + 1 == NS ? 0 : ibuf + 1;
+    if (++ikt == nk) { ikt = 0; itile += G; }
+  };
+  // One pipeline step: top up the DMA ring (into the stage computed one step ago), wait for the
+  // oldest stage `buf`, compute from it.
+  auto step = [&]() {
+    issue_next();
+    wait_dma<Cfg::LD>(inflight - 1);   // steps in flight beyond the current one may stay outstanding
+    barrier_mem();
+    compute(buf);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    barrier_mem();                     // nobody still reads `buf` when a later DMA overwrites it
+    --inflight;
+    buf = buf + 1 == NS ? 0 : buf + 1;
+  };
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue_next();
+  for (int tile = first; tile < ntiles; tile += G) {
+    for (int kt = 0; kt < nk - 1; ++kt) step();
+    epi_load(tile);                   // bias / residual loads fly during the last step's MFMAs
+    step();
+    switch (p.act) {
+      case SVK_ACT_GELU: epilogue(tile, std::integral_constant<int, SVK_ACT_GELU>{}); break;
+      case SVK_ACT_RELU: epilogue(tile, std::integral_constant<int, SVK_ACT_RELU>{}); break;
+      case SVK_ACT_TANH: epilogue(tile, std::integral_constant<int, SVK_ACT_TANH>{}); break;
+      default: epilogue(tile, std::integral_constant<int, 0>{}); break;
+    }
+  }
+}
+
+// ---- host side -------------------------------------------------------------------------------
+static int pk_slots(const void* fn, int nt) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, nt, 0);
+  return std::max(1, cus) * std::max(1, per);
+}
+
+template <class Cfg, bool KTAIL>
+static int launch_pk(const GemmArgs& a, hipStream_t st) {
+  const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.N + Cfg::BN - 1) / Cfg::BN;
+  const long ntiles = (long)ntm * ntn;
+  const int nk = (a.K + 63) / 64;
+  static const int slots = pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL>), Cfg::NT);
+  const int grid = (int)std::min<long>(ntiles, slots);
+  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL>), dim3(grid), dim3(Cfg::NT), 0, st, a, ntn, (int)ntiles, nk);
+  static char name[96];
+  if (!name[0])
+    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s>", Cfg::BM, Cfg::BN, Cfg::WGM, Cfg::WGN,
+             Cfg::NSTAGE, KTAIL ? "true" : "false");
+  set_last_kernel(name);
+  return check_launch("gemm_pk");
+}
+
+template <class Cfg>
+static int launch_pk_k(const GemmArgs& a, hipStream_t st) {
+  return a.K % 64 ? launch_pk<Cfg, true>(a, st) : launch_pk<Cfg, false>(a, st);
+}
+
+// Eligible: bf16, dense K-contiguous operands (16-byte aligned rows, K % 8 == 0), plain epilogue,
+// C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when not eligible.
+int gemm_pk_try(const GemmArgs& a, hipStream_t st) {
+  static const int force = getenv("SVK_PK_CFG") ? atoi(getenv("SVK_PK_CFG")) : -1;   // tuning knob
+  if (getenv("SVK_NO_PK")) return 1;
+  auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
+  if (a.K % 8 || a.N % 4 || a.lda % 8 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4)) return 1;
+  if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
+  int cfg = force;
+  // measured on the MiT-b2 shapes (tools/gemm_bench.py): deeper rings at 1 workgroup/CU lose to
+  // 2-3 resident workgroups with a 2-stage ring; 128 x 64 tiles when N is not a multiple of 128
+  if (cfg < 0) cfg = (a.N <= 64 || a.N % 128 != 0) ? 10 : 0;
+  switch (cfg) {
+    case 1: return launch_pk_k<PkCfg<128, 128, 2, 2, 4>>(a, st);
+    case 2: return launch_pk_k<PkCfg<256, 128, 4, 2, 3>>(a, st);
+    case 3: return launch_pk_k<PkCfg<128, 128, 2, 2, 3>>(a, st);
+    case 4: return launch_pk_k<PkCfg<256, 128, 4, 2, 2>>(a, st);
+    case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>>(a, st);
+    case 11: return launch_pk_k<PkCfg<128, 64, 2, 2, 3>>(a, st);
+    case 12: return launch_pk_k<PkCfg<256, 64, 4, 1, 3>>(a, st);
+    default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>>(a, st);
+  }
+}
+
+}  // namespace svk

@@ -7,6 +7,9 @@
 namespace svk {
 
 static thread_local char g_err[512] = "";
+static thread_local const char* g_last_kernel = "";
+
+void set_last_kernel(const char* name) { g_last_kernel = name; }
 
 void set_error(const char* fmt, ...) {
   va_list ap;
@@ -28,3 +31,4 @@ int check_launch(const char* what) {
 
 extern "C" const char* svk_version(void) { return "svk 0.1.0 gfx950"; }
 extern "C" const char* svk_last_error(void) { return svk::g_err; }
+extern "C" const char* svk_last_kernel(void) { return svk::g_last_kernel; }

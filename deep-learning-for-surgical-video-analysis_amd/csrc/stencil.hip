@@ -4,67 +4,134 @@
 
 namespace svk {
 
-// ---- DWConv 3x3, pad 1, + bias + act (MixFFN, mix_transformer_evp.py:22-30, 62-63) ----------
-// One thread per (pixel, 8-channel group): 16-byte (bf16) / 32-byte (f32) vector loads along C.
 template <typename T>
-__global__ __launch_bounds__(256) void dwconv3x3_vec8(const T* __restrict__ X, const float* __restrict__ w,
-                                                      const float* __restrict__ bias, T* __restrict__ Y,
-                                                      T* __restrict__ Ypre, int B, int H, int W, int C, int act) {
-  const int CG = C >> 3;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * H * W * CG;
-  if (idx >= total) return;
-  const int cg = (int)(idx % CG);
-  const long pix = idx / CG;
-  const int x = (int)(pix % W);
-  const long t = pix / W;
-  const int y = (int)(t % H);
-  const int b = (int)(t / H);
-  const int c0 = cg * 8;
-  float acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) acc[j] = bias[c0 + j];
-#pragma unroll
-  for (int dy = -1; dy <= 1; ++dy) {
-    const int yy = y + dy;
-    if (yy < 0 || yy >= H) continue;
-#pragma unroll
-    for (int dx = -1; dx <= 1; ++dx) {
-      const int xx = x + dx;
-      if (xx < 0 || xx >= W) continue;
-      const T* src = X + (((long)b * H + yy) * W + xx) * C + c0;
-      T v[8];
-      if constexpr (sizeof(T) == 2) {
-        *reinterpret_cast<uint4*>(v) = *reinterpret_cast<const uint4*>(src);
-      } else {
-        reinterpret_cast<uint4*>(v)[0] = reinterpret_cast<const uint4*>(src)[0];
-        reinterpret_cast<uint4*>(v)[1] = reinterpret_cast<const uint4*>(src)[1];
-      }
-      const float* wt = w + ((dy + 1) * 3 + (dx + 1)) * C + c0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j] += to_f(v[j]) * wt[j];
-    }
-  }
-  T o[8];
-  if (Ypre) {   // pre-activation copy (training: the GELU backward needs it)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = from_f<T>(acc[j]);
-    T* dp = Ypre + pix * C + c0;
-    if constexpr (sizeof(T) == 2) {
-      *reinterpret_cast<uint4*>(dp) = *reinterpret_cast<const uint4*>(o);
-    } else {
-      reinterpret_cast<uint4*>(dp)[0] = reinterpret_cast<const uint4*>(o)[0];
-      reinterpret_cast<uint4*>(dp)[1] = reinterpret_cast<const uint4*>(o)[1];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = from_f<T>(apply_act(acc[j], act));
-  T* dst = Y + pix * C + c0;
+__device__ __forceinline__ void store_vec8(T* dst, const T* o) {
   if constexpr (sizeof(T) == 2) {
     *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(o);
   } else {
     reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(o)[0];
     reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(o)[1];
+  }
+}
+
+// ---- DWConv 3x3, pad 1, + bias + act (MixFFN, mix_transformer_evp.py:22-30, 62-63) ----------
+// One thread per (8-channel group, column x, strip of R rows): the 3 x (R + 2) input vectors of the
+// strip are all loaded up front (16-byte loads, addresses clamped, out-of-image taps zeroed by a
+// select — no branches, every load in flight at once), so each output costs 3(R+2)/R loads instead
+// of 9.  Consecutive lanes take consecutive channel groups: a wave reads whole contiguous pixel
+// rows.  bf16: products in packed f32 (v_pk_fma_f32), branch-free erf for the GELU.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct Vec8 { uint32_t u[sizeof(T) * 2]; };
+
+template <typename T>
+__device__ __forceinline__ void load8_masked(const T* p, bool ok, Vec8<T>& v) {
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(v.u) = *reinterpret_cast<const uint4*>(p);
+  } else {
+    reinterpret_cast<uint4*>(v.u)[0] = reinterpret_cast<const uint4*>(p)[0];
+    reinterpret_cast<uint4*>(v.u)[1] = reinterpret_cast<const uint4*>(p)[1];
+  }
+#pragma unroll
+  for (int j = 0; j < (int)(sizeof(T) * 2); ++j) v.u[j] = ok ? v.u[j] : 0u;
+}
+// element pair (2j, 2j+1) of a vector as f32
+template <typename T>
+__device__ __forceinline__ f32x2 pair(const Vec8<T>& v, int j) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t u = v.u[j];
+    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+  } else {
+    return f32x2{__uint_as_float(v.u[2 * j]), __uint_as_float(v.u[2 * j + 1])};
+  }
+}
+
+// Packed-f32 GELU (erf form, erf_fast: |err| <= 1.5e-7): the FMAs/MULs issue as v_pk_*_f32 (two
+// elements per instruction), only rcp/exp are per element.
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 az = f32x2{fabsf(z.x), fabsf(z.y)};
+  const f32x2 d = az * 0.3275911f + 1.0f;
+  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  f32x2 p = t * 1.061405429f - 1.453152027f;
+  p = p * t + 1.421413741f;
+  p = p * t - 0.284496736f;
+  p = p * t + 0.254829592f;
+  const f32x2 q = az * (az * -1.4426950408889634f);        // -z^2 * log2(e)
+  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2 y = 1.0f - (p * t) * e;
+  const f32x2 erf = f32x2{copysignf(y.x, z.x), copysignf(y.y, z.y)};
+  const f32x2 h = x * 0.5f;
+  return h * erf + h;
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, T* __restrict__ Y,
+                                                       T* __restrict__ Ypre, int B, int H, int W, int C, int act,
+                                                       int nstrip) {
+  const int CG = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * nstrip * W * CG;
+  if (idx >= total) return;
+  const int cg = (int)(idx % CG);
+  long t = idx / CG;
+  const int x = (int)(t % W);
+  t /= W;
+  const int s = (int)(t % nstrip);
+  const int b = (int)(t / nstrip);
+  const int c0 = cg * 8, y0 = s * R;
+  const T* base = X + (long)b * H * W * C + c0;
+  const int xl = x > 0 ? x - 1 : 0, xr = x < W - 1 ? x + 1 : W - 1;
+
+  Vec8<T> win[R + 2][3];
+#pragma unroll
+  for (int r = 0; r < R + 2; ++r) {
+    const int yy = y0 - 1 + r;
+    const bool oky = yy >= 0 && yy < H;
+    const int yc = min(max(yy, 0), H - 1);
+    const T* row = base + (long)yc * W * C;
+    load8_masked(row + (long)xl * C, oky && x > 0, win[r][0]);
+    load8_masked(row + (long)x * C, oky, win[r][1]);
+    load8_masked(row + (long)xr * C, oky && x < W - 1, win[r][2]);
+  }
+  f32x2 wt[9][4], bs[4];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wt[k][j] = *reinterpret_cast<const f32x2*>(w + k * C + c0 + 2 * j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f32x2*>(bias + c0 + 2 * j);
+
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int y = y0 + r;
+    if (y >= H) break;
+    f32x2 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bs[j];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = pair(win[r + dy][dx], j) * wt[dy * 3 + dx][j] + acc[j];
+    const long off = (((long)b * H + y) * W + x) * C + c0;
+    T o[8];
+    if (Ypre) {   // pre-activation copy (training: the GELU backward needs it)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[2 * j] = from_f<T>(acc[j].x); o[2 * j + 1] = from_f<T>(acc[j].y); }
+      store_vec8(Ypre + off, o);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x2 g;
+      if (sizeof(T) == 2 && act == SVK_ACT_GELU) g = gelu_fast2(acc[j]);
+      else g = f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
+      o[2 * j] = from_f<T>(g.x);
+      o[2 * j + 1] = from_f<T>(g.y);
+    }
+    store_vec8(Y + off, o);
   }
 }
 
@@ -92,7 +159,8 @@ __global__ void dwconv3x3_scalar(const T* __restrict__ X, const float* __restric
 }
 
 // ---- NCHW f32 -> NHWC T --------------------------------------------------------------------
-// One thread per pixel, all C channels: reads coalesced along W within each channel plane.
+// One thread per pixel: reads coalesced along W within each channel plane, the pixel's Cpad
+// channels written as whole 16-byte vectors (Cpad % 8 == 0) or scalars.
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W,
                                     int Cpad) {
@@ -102,7 +170,16 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ X, T* __restrict__
   const long b = pix / hw, p = pix - b * hw;
   const float* src = X + b * C * hw + p;
   T* dst = Y + pix * Cpad;
-  for (int c = 0; c < Cpad; ++c) dst[c] = from_f<T>(c < C ? src[(long)c * hw] : 0.f);
+  if ((Cpad & 7) == 0) {
+    for (int c0 = 0; c0 < Cpad; c0 += 8) {
+      T o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = from_f<T>(c0 + j < C ? src[(long)(c0 + j) * hw] : 0.f);
+      store_vec8(dst + c0, o);
+    }
+  } else {
+    for (int c = 0; c < Cpad; ++c) dst[c] = from_f<T>(c < C ? src[(long)c * hw] : 0.f);
+  }
 }
 
 // ---- GaussianFilter.conv_gauss: reflect pad 2 + binomial 5x5 / 256 (mix_transformer_evp.py:501-514)
@@ -112,30 +189,72 @@ __device__ __forceinline__ int reflect(int i, int n) {
   return i;
 }
 
-// One thread per output pixel, looping over channels: the 25 taps of neighbouring threads are
-// neighbouring addresses of one NCHW plane (coalesced), output written NHWC.
-template <typename T>
-__global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W, int Cpad) {
-  const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (pix >= (long)B * H * W) return;
-  const int x = (int)(pix % W);
-  const long t = pix / W;
-  const int y = (int)(t % H);
-  const int b = (int)(t / H);
-  const float k1[5] = {1.f, 4.f, 6.f, 4.f, 1.f};
-  int yy[5], xx[5];
+// One thread per (column x, strip of GR rows): the filter is separable ([1 4 6 4 1] / 16 twice,
+// exactly the reference's outer-product kernel), so each of the GR + 4 input rows is filtered
+// horizontally once (5 coalesced loads along W) and the strip's outputs are vertical 5-tap sums of
+// those row results.  Output NHWC, channels padded to Cpad, 16-byte stores when Cpad % 8 == 0.
+constexpr int GR = 8;
+template <typename T, int CMAX>
+__global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W, int Cpad,
+                                int nstrip) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * nstrip * W) return;
+  const int x = (int)(idx % W);
+  const long t = idx / W;
+  const int s = (int)(t % nstrip);
+  const int b = (int)(t / nstrip);
+  const int y0 = s * GR;
+  const float k1[5] = {1.f / 16.f, 4.f / 16.f, 6.f / 16.f, 4.f / 16.f, 1.f / 16.f};
+  int xx[5];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) { yy[i] = reflect(y + i - 2, H); xx[i] = reflect(x + i - 2, W); }
-  for (int c = 0; c < C; ++c) {
+  for (int j = 0; j < 5; ++j) xx[j] = reflect(x + j - 2, W);
+  float out[GR][CMAX];
+#pragma unroll
+  for (int c = 0; c < CMAX; ++c) {
+    if (c >= C) {
+#pragma unroll
+      for (int r = 0; r < GR; ++r) out[r][c] = 0.f;
+      continue;
+    }
     const float* src = X + ((long)b * C + c) * H * W;
-    float acc = 0.f;
+    float h[GR + 4];
 #pragma unroll
-    for (int i = 0; i < 5; ++i)
+    for (int r = 0; r < GR + 4; ++r) {
+      const int yy = reflect(min(y0 + r - 2, H + 1), H);   // rows past the strip's last valid output: clamp
+      const float* row = src + (long)yy * W;
+      float a = 0.f;
 #pragma unroll
-      for (int j = 0; j < 5; ++j) acc += src[(long)yy[i] * W + xx[j]] * (k1[i] * k1[j] * (1.0f / 256.f));
-    Y[pix * Cpad + c] = from_f<T>(acc);
+      for (int j = 0; j < 5; ++j) a += row[xx[j]] * k1[j];
+      h[r] = a;
+    }
+#pragma unroll
+    for (int r = 0; r < GR; ++r) {
+      float a = 0.f;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) a += h[r + i] * k1[i];
+      out[r][c] = a;
+    }
   }
-  for (int c = C; c < Cpad; ++c) Y[pix * Cpad + c] = from_f<T>(0.f);
+#pragma unroll
+  for (int r = 0; r < GR; ++r) {
+    const int y = y0 + r;
+    if (y >= H) break;
+    T* dst = Y + (((long)b * H + y) * W + x) * Cpad;
+    if ((Cpad & 7) == 0 && CMAX <= 8) {
+      T o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] = from_f<T>(c < CMAX ? out[r][c < CMAX ? c : 0] : 0.f);
+      store_vec8(dst, o);
+      for (int c = 8; c < Cpad; c += 8) {
+        T z[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) z[j] = from_f<T>(0.f);
+        store_vec8(dst + c, z);
+      }
+    } else {
+      for (int c = 0; c < Cpad; ++c) dst[c] = from_f<T>(c < CMAX ? out[r][c < CMAX ? c : 0] : 0.f);
+    }
+  }
 }
 
 // ---- bilinear resize, align_corners=False, no antialias (F.interpolate semantics) ----------
@@ -219,9 +338,11 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
   SVK_DISPATCH_DTYPE(dtype, T, {
     const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 15) == 0;
     if (vec) {
-      const long n = (long)B * H * W * (C / 8);
-      hipLaunchKernelGGL((dwconv3x3_vec8<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B, H,
-                         W, C, act);
+      constexpr int R = sizeof(T) == 2 ? 7 : 2;   // bf16: 56 / 28 / 14 / 7-row maps in whole strips
+      const int nstrip = (H + R - 1) / R;
+      const long n = (long)B * nstrip * W * (C / 8);
+      hipLaunchKernelGGL((dwconv3x3_strip<T, R>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B,
+                         H, W, C, act, nstrip);
     } else {
       const long n = (long)B * H * W * C;
       hipLaunchKernelGGL((dwconv3x3_scalar<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B,
@@ -249,11 +370,19 @@ extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, i
 
 extern "C" int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
                                     void* stream) {
-  if (B < 0 || C <= 0 || Cpad < C || H < 3 || W < 3 || !X || !Y) { set_error("svk_gauss5x5_reflect: bad args"); return SVK_EINVAL; }
+  if (B < 0 || C <= 0 || C > 8 || Cpad < C || H < 3 || W < 3 || !X || !Y) {
+    set_error("svk_gauss5x5_reflect: bad args (1 <= C <= 8)"); return SVK_EINVAL;
+  }
   if (B == 0) return SVK_OK;
-  const long n = (long)B * H * W;   // one thread per pixel
+  const int nstrip = (H + GR - 1) / GR;
+  const long n = (long)B * nstrip * W;   // one thread per (column, strip of GR rows)
   SVK_DISPATCH_DTYPE(dtype_out, T, {
-    hipLaunchKernelGGL((gauss5x5_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W, Cpad);
+    if (C <= 3)
+      hipLaunchKernelGGL((gauss5x5_kernel<T, 3>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W,
+                         Cpad, nstrip);
+    else
+      hipLaunchKernelGGL((gauss5x5_kernel<T, 8>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W,
+                         Cpad, nstrip);
     return check_launch("gauss5x5_reflect");
   });
 }

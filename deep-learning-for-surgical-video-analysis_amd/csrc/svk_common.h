@@ -15,6 +15,8 @@ namespace svk {
 // Thread-local last-error string (svk_last_error); set by the host wrappers only.
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
+// Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
+void set_last_kernel(const char* name);
 // gemm.hip: batched split-M weight-gradient reduction dW[z] += dY[z]^T X[z] (f32 atomics)
 int wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o,
                   long sx_i, float* dW, long lddw, long sw_o, long sw_i, int Z, int nzi, int M, int N, int K,
@@ -33,7 +35,7 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 // are rounded to 8 significant bits anyway; the f32 parity path keeps erff.
 __device__ __forceinline__ float erf_fast(float x) {
   const float ax = fabsf(x);
-  const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
@@ -52,6 +54,16 @@ __device__ __forceinline__ float apply_act(float v, int act) {
   }
 }
 
+// bf16 kernels: the output is rounded to 8 significant bits, so the GELU uses the branch-free erf.
+__device__ __forceinline__ float apply_act_fast(float v, int act) {
+  switch (act) {
+    case SVK_ACT_GELU: return gelu_fast(v);
+    case SVK_ACT_RELU: return v > 0.f ? v : 0.f;
+    case SVK_ACT_TANH: return tanhf(v);
+    default: return v;
+  }
+}
+
 // d act(u) / du (activation backward): GELU (erf form), ReLU, tanh.  The GELU derivative uses the
 // branch-free erf (|err| <= 1.5e-7, below bf16 resolution and f32-parity tolerance).
 __device__ __forceinline__ float act_grad(float u, int act) {
@@ -59,7 +71,7 @@ __device__ __forceinline__ float act_grad(float u, int act) {
     case SVK_ACT_GELU: {
       const float e = __expf(-0.5f * u * u);
       const float x = u * 0.70710678118654752f, ax = fabsf(x);
-      const float t = __frcp_rn(fmaf(0.3275911f, ax, 1.0f));
+      const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, ax, 1.0f));
       float p = fmaf(1.061405429f, t, -1.453152027f);
       p = fmaf(p, t, 1.421413741f);
       p = fmaf(p, t, -0.284496736f);

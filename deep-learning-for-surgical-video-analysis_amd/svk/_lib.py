@@ -62,7 +62,7 @@ SIGNATURES = {
     "svk_sgd": [P, P, P, c_long, c_float, c_float, c_float, c_float, c_int, c_int, P],
     "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],
 }
-STRING_FUNCS = ("svk_version", "svk_last_error")
+STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
 LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int]}
 
 _lib = None

@@ -68,14 +68,9 @@ def set_profiler(records):
     _PROF = records
 
 
-def _gemm_kernel_name(dt, M, N, vec, asrc, ext=False):
-    """Mirror of launch_gemm's tile choice (csrc/gemm.hip) -> the kernel symbol rocprof reports."""
-    if N <= 64:
-        bm, bn = (128, 64) if (M + 127) // 128 >= 512 else (64, 64)
-    else:
-        bm, bn = (128, 128) if ((M + 127) // 128) * ((N + 127) // 128) >= 512 else (64, 64)
-    t = "float" if dt == F32 else "__bf16"
-    return f"gemm_kernel<{t}, {bm}, {bn}, {'true' if vec else 'false'}, {asrc}, {'true' if ext else 'false'}>"
+def _last_kernel():
+    """The kernel instantiation the library launched last on this thread (svk_last_kernel)."""
+    return _lib.load().svk_last_kernel().decode()
 
 
 def _prof_begin():
@@ -138,7 +133,7 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
         vw = 16 // es
         vec = a.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0 and lda % vw == 0 and w.stride(0) % vw == 0
         nb = (M * K + N * K + M * N * (1 + (residual is not None) + (dact is not None))) * es
-        _prof_end(t0, _gemm_kernel_name(dtype_code(a.dtype), M, N, vec, 0, row_scale is not None or dact is not None),
+        _prof_end(t0, _last_kernel(),
                   2.0 * M * N * K, nb, (M, N, K))
     return out
 
@@ -189,7 +184,7 @@ def conv2d_nhwc(x, w_packed, k, stride, pad, bias=None, act=None, residual=None)
         M, K = B * OH * OW, k * k * Cin
         vec = x.data_ptr() % 16 == 0 and w_packed.data_ptr() % 16 == 0 and Cin % 8 == 0
         nb = (x.numel() + Cout * K + M * Cout) * x.element_size()
-        _prof_end(t0, _gemm_kernel_name(dtype_code(x.dtype), M, Cout, vec, 1), 2.0 * M * Cout * K, nb,
+        _prof_end(t0, _last_kernel(), 2.0 * M * Cout * K, nb,
                   (M, Cout, K, f"conv{k}s{stride}"))
     return out
 
@@ -431,7 +426,7 @@ def conv2d_dgrad(dy, wd_packed, H, W, Cin, k, stride, pad, residual=None, out=No
               _p(out), H, W, Cin, k, stride, pad, _stream())
     M = B * H * W
     vec = dy.data_ptr() % 16 == 0 and wd_packed.data_ptr() % 16 == 0 and Cout % 8 == 0
-    _prof_end(t0, _gemm_kernel_name(dtype_code(dy.dtype), M, Cin, vec, 2), 2.0 * M * Cin * k * k * Cout / stride ** 2,
+    _prof_end(t0, _last_kernel(), 2.0 * M * Cin * k * k * Cout / stride ** 2,
               (dy.numel() + out.numel()) * dy.element_size(), (M, Cin, k * k * Cout, f"convdgrad{k}s{stride}"))
     return out
 

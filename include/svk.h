@@ -33,6 +33,8 @@ enum { SVK_OK = 0, SVK_EINVAL = -1, SVK_EUNSUPPORTED = -2, SVK_ELAUNCH = -3 };
 
 const char* svk_version(void);
 const char* svk_last_error(void);
+/* Kernel instantiation launched last by the calling thread (GEMM / conv family; for profilers). */
+const char* svk_last_kernel(void);
 
 /* C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]
  * Replaces nn.Linear (+ activation, + residual add) at: Attention q/kv/proj

@@ -47,6 +47,35 @@ def test_gemm(cuda, dt, M, N, K, act):
     _close(got, ref, dt)
 
 
+@pytest.mark.parametrize("M,N,K,act,res", [(70000, 512, 128, None, True), (30000, 320, 1280, None, True),
+                                           (3000, 136, 80, "gelu", False), (5000, 96, 200, "relu", True),
+                                           (40000, 64, 256, None, True), (20001, 16, 16, None, False),
+                                           (12544, 2048, 512, "tanh", False)])
+def test_gemm_persistent_bf16(cuda, M, N, K, act, res):
+    """bf16 plain-epilogue GEMMs run on the persistent LDS-DMA kernel (more tiles than resident
+    workgroups, K tails, M tails); checked against fp64 and against the tiled kernel (SVK_NO_PK)."""
+    import os
+    from svk import ops
+    dt = torch.bfloat16
+    a = _rand(M, K, dt=dt, dev=cuda, seed=11)
+    w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=12)
+    b = _rand(N, dt=torch.float32, dev=cuda, seed=13)
+    r = _rand(M, N, dt=dt, dev=cuda, seed=14) if res else None
+    got = ops.gemm(a, w, b, act=act, residual=r)
+    os.environ["SVK_NO_PK"] = "1"
+    try:
+        tiled = ops.gemm(a, w, b, act=act, residual=r)
+    finally:
+        del os.environ["SVK_NO_PK"]
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().t() + b.double()
+    ref = {None: lambda t: t, "gelu": lambda t: F.gelu(t), "relu": torch.relu, "tanh": torch.tanh}[act](ref)
+    if res:
+        ref = ref + r.double()
+    _close(got, ref.cpu(), dt)
+    _close(got, tiled.double().cpu(), dt)
+
+
 @pytest.mark.parametrize("dt", DTS)
 def test_gemm_strided_views(cuda, dt):
     """kv[:, :, :C] style inputs and writes into a column slice (head concat buffer)."""

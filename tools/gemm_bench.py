@@ -40,6 +40,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-lib", action="store_true", help="skip the hipBLASLt comparison")
+    ap.add_argument("--no-conv", action="store_true")
     args = ap.parse_args()
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     dev = torch.device("cuda:0")
@@ -52,10 +54,15 @@ def main():
         out = torch.empty(M, N, device=dev, dtype=dt)
         ms = timeit(lambda: ops.gemm(a, w, b, residual=r, out=out), args.reps)
         nb = (M * K + N * K + M * N * (2 if res else 1)) * es
+        # hipBLASLt (torch.nn.functional.linear, bias fused, no residual) on the same shape: the
+        # library ceiling for a plain GEMM, for comparison only
+        bt = b.to(dt)
+        ml = timeit(lambda: torch.nn.functional.linear(a, w, bt), args.reps) if not args.no_lib else float("nan")
         print(f"gemm M={M:7d} N={N:5d} K={K:5d} res={int(res)}  {ms * 1e3:9.1f} us  "
-              f"{2 * M * N * K / ms / 1e9:8.1f} TF/s  {nb / ms / 1e6:8.1f} GB/s", flush=True)
+              f"{2 * M * N * K / ms / 1e9:8.1f} TF/s  {nb / ms / 1e6:8.1f} GB/s   hipblaslt {ml * 1e3:9.1f} us "
+              f"{2 * M * N * K / ml / 1e9:8.1f} TF/s", flush=True)
         del a, w, r, out
-    for B, H, W, Cin, Cout, k, s, p in CONVS:
+    for B, H, W, Cin, Cout, k, s, p in ([] if args.no_conv else CONVS):
         x = torch.randn(B, H, W, Cin, device=dev).to(dt)
         wp = torch.randn(Cout, k * k * Cin, device=dev).to(dt)
         b = torch.randn(Cout, device=dev)
