@@ -25,8 +25,8 @@ struct GemmArgs {
   int out_mode, uH, uW, us, uC;
 };
 
-// gemm_pk.hip: persistent LDS-DMA bf16 GEMM for the dense plain-epilogue case; returns 0 when it
-// launched, 1 when the arguments are not eligible (caller falls back to gemm_kernel).
-int gemm_pk_try(const GemmArgs& a, hipStream_t st);
+// gemm_pk.hip: persistent LDS-DMA bf16 GEMM / implicit-GEMM conv (asrc 1) for the plain-epilogue
+// case; returns 0 when it launched, 1 when the arguments are not eligible (caller falls back to gemm_kernel).
+int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
 
 }  // namespace svk

@@ -55,6 +55,19 @@ struct PkCfg {
   static_assert(LD * (NSTAGE - 1) <= 63, "vmcnt range");
 };
 
+// n / d for 0 <= n < 2^31 by multiply-high (d >= 1); host computes (mul, shr).
+struct FastDiv {
+  uint32_t mul, shr;
+  __device__ __forceinline__ int div(int n) const { return (int)((__umulhi((uint32_t)n, mul) + (uint32_t)n) >> shr); }
+};
+static FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  return FastDiv{(uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1), l};
+}
+// implicit-GEMM conv (ASRC == 1): divisors of the row / column decompositions
+struct PkConv { FastDiv hw, ow, cin, kw; };
+
 __device__ __forceinline__ int pk_xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
@@ -80,8 +93,8 @@ __device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current
   }
 }
 
-template <class Cfg, bool KTAIL>
-__global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, int ntn, int ntiles, int nk) {
+template <class Cfg, bool KTAIL, bool ELDS, int ASRC>
+__global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
   __shared__ __attribute__((aligned(1024))) char smem[Cfg::LDS];
@@ -98,17 +111,48 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, int ntn, int
   const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
 
   // this thread's DMA lane covers 16-byte chunk q = (wave * LD + i) * 64 + lane of the stage image
+  // ASRC == 1: im2col rows of this thread's A slots (output pixel -> first input tap), per tile
+  int crb[Cfg::A_LD], ciy[Cfg::A_LD], cix[Cfg::A_LD];
   auto issue = [&](int tile, int kt, int buf) {
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN, k0 = kt * Cfg::BK;
     const uint32_t sa = lds0 + buf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
+    if constexpr (ASRC == 1) {
+      // every A slot of a lane has the same 16-byte chunk column c (rows differ by multiples of 8)
+      const int c = (lane & 7) ^ ((lane >> 3) & 7);
+      if (kt == 0) {
 #pragma unroll
-    for (int i = 0; i < Cfg::A_LD; ++i) {
-      const int q = (wave * Cfg::A_LD + i) * 64 + lane;
-      const int r = q >> 3, c = (q & 7) ^ (r & 7);
-      const int m = min(m0 + r, p.M - 1), k = k0 + c * 8;
-      const char* src = reinterpret_cast<const char*>(A + (long)m * p.lda + k);
-      if constexpr (KTAIL) src = k < p.K ? src : zero;
-      dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
+        for (int i = 0; i < Cfg::A_LD; ++i) {
+          const int r = ((wave * Cfg::A_LD + i) * 64 + lane) >> 3;
+          const int m = m0 + r;
+          const int mm = m < p.M ? m : 0;
+          const int b = cv.hw.div(mm), rem = mm - b * (p.OH * p.OW);
+          const int oy = cv.ow.div(rem), ox = rem - oy * p.OW;
+          crb[i] = b * p.H * p.Wd * p.Cin;
+          ciy[i] = m < p.M ? oy * p.stride - p.pad : -0x40000000;   // invalid row: every tap out of range
+          cix[i] = ox * p.stride - p.pad;
+        }
+      }
+      const int k = k0 + c * 8;
+      const int kc = k < p.K ? k : 0;
+      const int tap = cv.cin.div(kc), ci = kc - tap * p.Cin;
+      const int ti = cv.kw.div(tap), tj = tap - ti * p.kw;
+#pragma unroll
+      for (int i = 0; i < Cfg::A_LD; ++i) {
+        const int iy = ciy[i] + ti, ix = cix[i] + tj;
+        const bool ok = k < p.K && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.Wd;
+        const char* src = ok ? reinterpret_cast<const char*>(A + crb[i] + ((long)iy * p.Wd + ix) * p.Cin + ci) : zero;
+        dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < Cfg::A_LD; ++i) {
+        const int q = (wave * Cfg::A_LD + i) * 64 + lane;
+        const int r = q >> 3, c = (q & 7) ^ (r & 7);
+        const int m = min(m0 + r, p.M - 1), k = k0 + c * 8;
+        const char* src = reinterpret_cast<const char*>(A + (long)m * p.lda + k);
+        if constexpr (KTAIL) src = k < p.K ? src : zero;
+        dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
+      }
     }
 #pragma unroll
     for (int i = 0; i < Cfg::B_LD; ++i) {
@@ -160,6 +204,8 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, int ntn, int
       ebias[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
     }
   };
+  constexpr int CPR = BN / 8;            // 16-byte chunks per staged output row
+  char* stile = nullptr;                  // ELDS: stage buffer consumed by the tile's last step
   auto epilogue = [&](int tile, auto act_c) {
     constexpr int ACT = decltype(act_c)::value;
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
@@ -192,9 +238,28 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, int ntn, int
           v[3] += __uint_as_float(eres[i][j].y & 0xFFFF0000u);
         }
         bf16 o[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-        if (m < p.M && n < p.N)   // N % 4 == 0: a 4-column group is all-in or all-out
+        if constexpr (ELDS) {
+          const int row = wm * WM + i * 16 + fr, col = wn * WN + j * 16 + fq * 4;
+          *reinterpret_cast<uint2*>(stile + row * (BN * 2) + (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col >> 2) & 1) * 8) =
+              *reinterpret_cast<const uint2*>(o);
+        } else if (m < p.M && n < p.N) {   // N % 4 == 0: a 4-column group is all-in or all-out
           *reinterpret_cast<uint2*>(C + (long)m * p.ldc + n) = *reinterpret_cast<const uint2*>(o);
+        }
       }
+    }
+    if constexpr (ELDS) {
+      // the tile, staged as bf16 rows in the stage buffer just consumed, leaves as whole 16-byte row
+      // chunks (a wave stores 4 full 256-byte rows per instruction instead of 16 x 32-byte pieces)
+      barrier_mem();
+#pragma unroll
+      for (int it = 0; it < (BM * CPR) / Cfg::NT; ++it) {
+        const int idx = tid + it * Cfg::NT;
+        const int row = idx / CPR, c = idx % CPR;
+        const uint4 v = *reinterpret_cast<const uint4*>(stile + row * (BN * 2) + ((c ^ (row & (CPR - 1))) << 4));
+        const int m = m0 + row, n = n0 + c * 8;
+        if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
+      }
+      barrier_mem();   // the next step's DMA overwrites this stage buffer
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -222,6 +287,7 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, int ntn, int
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_mem();                     // nobody still reads `buf` when a later DMA overwrites it
     --inflight;
+    stile = smem + buf * Cfg::STAGE;
     buf = buf + 1 == NS ? 0 : buf + 1;
   };
 #pragma unroll
@@ -248,48 +314,72 @@ static int pk_slots(const void* fn, int nt) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <class Cfg, bool KTAIL>
+template <class Cfg, bool KTAIL, bool ELDS, int ASRC>
 static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.N + Cfg::BN - 1) / Cfg::BN;
   const long ntiles = (long)ntm * ntn;
   const int nk = (a.K + 63) / 64;
-  static const int slots = pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL>), Cfg::NT);
+  static const int slots = pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC>), Cfg::NT);
   const int grid = (int)std::min<long>(ntiles, slots);
-  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL>), dim3(grid), dim3(Cfg::NT), 0, st, a, ntn, (int)ntiles, nk);
+  PkConv cv{};
+  if (ASRC == 1) {
+    cv.hw = make_fastdiv((uint32_t)(a.OH * a.OW));
+    cv.ow = make_fastdiv((uint32_t)a.OW);
+    cv.cin = make_fastdiv((uint32_t)a.Cin);
+    cv.kw = make_fastdiv((uint32_t)a.kw);
+  }
+  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn, (int)ntiles,
+                     nk);
   static char name[96];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s>", Cfg::BM, Cfg::BN, Cfg::WGM, Cfg::WGN,
-             Cfg::NSTAGE, KTAIL ? "true" : "false");
+    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d>", Cfg::BM, Cfg::BN, Cfg::WGM,
+             Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC);
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
 
-template <class Cfg>
-static int launch_pk_k(const GemmArgs& a, hipStream_t st) {
-  return a.K % 64 ? launch_pk<Cfg, true>(a, st) : launch_pk<Cfg, false>(a, st);
+template <class Cfg, int ASRC>
+static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
+  static const int elds_env = getenv("SVK_PK_ELDS") ? atoi(getenv("SVK_PK_ELDS")) : -1;   // tuning knob
+  auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (elds_env >= 0) elds = elds_env;
+  elds = elds && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
+  if (ASRC == 1) {   // the im2col loader zero-fills K tails itself
+    return elds ? launch_pk<Cfg, false, true, 1>(a, st) : launch_pk<Cfg, false, false, 1>(a, st);
+  }
+  if (elds) return a.K % 64 ? launch_pk<Cfg, true, true, 0>(a, st) : launch_pk<Cfg, false, true, 0>(a, st);
+  return a.K % 64 ? launch_pk<Cfg, true, false, 0>(a, st) : launch_pk<Cfg, false, false, 0>(a, st);
 }
 
-// Eligible: bf16, dense K-contiguous operands (16-byte aligned rows, K % 8 == 0), plain epilogue,
-// C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when not eligible.
-int gemm_pk_try(const GemmArgs& a, hipStream_t st) {
+// Eligible: bf16, K-contiguous operands (16-byte aligned rows, K % 8 == 0; conv: Cin % 8 == 0),
+// plain epilogue, C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when
+// not eligible.  asrc: 0 dense A, 1 implicit-GEMM conv (A = NHWC map, GemmArgs conv geometry).
+int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   static const int force = getenv("SVK_PK_CFG") ? atoi(getenv("SVK_PK_CFG")) : -1;   // tuning knob
   if (getenv("SVK_NO_PK")) return 1;
   auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
-  if (a.K % 8 || a.N % 4 || a.lda % 8 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4)) return 1;
+  if (a.K % 8 || a.N % 4 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4)) return 1;
+  if (asrc == 0 && a.lda % 8) return 1;
+  if (asrc == 1 && (a.Cin % 8 || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)) return 1;
   if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
   int cfg = force;
-  // measured on the MiT-b2 shapes (tools/gemm_bench.py): deeper rings at 1 workgroup/CU lose to
-  // 2-3 resident workgroups with a 2-stage ring; 128 x 64 tiles when N is not a multiple of 128
-  if (cfg < 0) cfg = (a.N <= 64 || a.N % 128 != 0) ? 10 : 0;
+  // Measured on the MiT-b2 shapes (tools/gemm_bench.py, profiles/r01/gemm_pk_tuning.txt): deeper
+  // rings at 1 workgroup/CU lose to 2-3 resident workgroups with a 2-stage ring.  The long-K
+  // (>= 512) GEMMs with N % 128 == 0 run best on 128 x 128 tiles with the register epilogue; all
+  // others (short K: output-write-bound) on 128 x 64 tiles with the LDS-staged 16-byte-store epilogue.
+  const bool big = a.K >= 512 && a.N % 128 == 0;
+  if (cfg < 0) cfg = big ? 0 : 10;
+  if (asrc == 1) {
+    switch (cfg) {
+      case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 1>(a, st, !big);
+      default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 1>(a, st, !big);
+    }
+  }
   switch (cfg) {
-    case 1: return launch_pk_k<PkCfg<128, 128, 2, 2, 4>>(a, st);
-    case 2: return launch_pk_k<PkCfg<256, 128, 4, 2, 3>>(a, st);
-    case 3: return launch_pk_k<PkCfg<128, 128, 2, 2, 3>>(a, st);
-    case 4: return launch_pk_k<PkCfg<256, 128, 4, 2, 2>>(a, st);
-    case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>>(a, st);
-    case 11: return launch_pk_k<PkCfg<128, 64, 2, 2, 3>>(a, st);
-    case 12: return launch_pk_k<PkCfg<256, 64, 4, 1, 3>>(a, st);
-    default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>>(a, st);
+    case 2: return launch_pk_k<PkCfg<256, 128, 4, 2, 2>, 0>(a, st, !big);
+    case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 0>(a, st, !big);
+    case 11: return launch_pk_k<PkCfg<128, 64, 2, 2, 3>, 0>(a, st, !big);
+    default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !big);
   }
 }
 

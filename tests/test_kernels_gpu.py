@@ -95,7 +95,9 @@ def test_gemm_strided_views(cuda, dt):
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p", [(2, 224, 224, 3, 64, 7, 4, 3), (2, 56, 56, 64, 128, 3, 2, 1),
                                                   (3, 56, 56, 64, 64, 8, 8, 0), (2, 224, 224, 2, 64, 7, 4, 3),
                                                   (1, 14, 14, 320, 512, 3, 2, 1), (2, 28, 28, 32, 80, 3, 2, 1),
-                                                  (2, 14, 14, 320, 320, 2, 2, 0)])
+                                                  (2, 14, 14, 320, 320, 2, 2, 0), (24, 224, 224, 8, 64, 7, 4, 3),
+                                                  (24, 224, 224, 8, 16, 7, 4, 3), (40, 56, 56, 64, 64, 8, 8, 0),
+                                                  (30, 28, 28, 128, 320, 3, 2, 1), (9, 14, 14, 320, 512, 3, 2, 1)])
 def test_conv2d_nhwc(cuda, dt, B, H, W, Cin, Cout, k, s, p):
     from svk import ops
     from svk.pack import conv_w
