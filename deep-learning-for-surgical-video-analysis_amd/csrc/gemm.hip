@@ -461,7 +461,7 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
               (!a.U || (aligned16(a.U) && a.ldu % vw == 0)) && (a.out_mode == 0 || a.uC % 8 == 0);
   const bool ext = a.rscale || a.U || a.out_mode;
   if constexpr (sizeof(T) == 2 && ASRC <= 1) {
-    if (vec && !ext && gemm_pk_try(a, st, ASRC) == 0) return SVK_OK;
+    if (vec && gemm_pk_try(a, st, ASRC) == 0) return SVK_OK;
   }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;

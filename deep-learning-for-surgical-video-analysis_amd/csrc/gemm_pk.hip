@@ -93,7 +93,7 @@ __device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current
   }
 }
 
-template <class Cfg, bool KTAIL, bool ELDS, int ASRC>
+template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT>
 __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
@@ -206,11 +206,14 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
   };
   constexpr int CPR = BN / 8;            // 16-byte chunks per staged output row
   char* stile = nullptr;                  // ELDS: stage buffer consumed by the tile's last step
+  // EXT (training): v = act(acc + bias) * rscale[m / rdiv] * uact'(U[m, n]) + R[m, n]; the template
+  // activation is then the BACKWARD one (uact), the forward act stays a runtime switch.
   auto epilogue = [&](int tile, auto act_c) {
     constexpr int ACT = decltype(act_c)::value;
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
     bf16* C = static_cast<bf16*>(p.C);
-    uint2 eres[TM][TN];
+    uint2 eres[TM][TN], eu[TM][TN];
+    float ers[TM];
     if (R) {
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -221,6 +224,22 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
           eres[i][j] = *reinterpret_cast<const uint2*>(R + (long)m * p.ldr + n);
         }
     }
+    if constexpr (EXT) {
+      const bf16* U = static_cast<const bf16*>(p.U);
+      if (U) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
+            const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+            eu[i][j] = *reinterpret_cast<const uint2*>(U + (long)m * p.ldu + n);
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        ers[i] = p.rscale ? p.rscale[min(m0 + wm * WM + i * 16 + fr, p.M - 1) / p.rdiv] : 1.f;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WN + j * 16 + fq * 4;
@@ -229,8 +248,19 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
         const int m = m0 + wm * WM + i * 16 + fr;
         float v[4] = {acc[i][j][0] + ebias[j].x, acc[i][j][1] + ebias[j].y, acc[i][j][2] + ebias[j].z,
                       acc[i][j][3] + ebias[j].w};
+        if constexpr (EXT) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
+          for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], p.act) * ers[i];
+          if (p.U) {
+            v[0] *= act_grad(__uint_as_float(eu[i][j].x << 16), ACT);
+            v[1] *= act_grad(__uint_as_float(eu[i][j].x & 0xFFFF0000u), ACT);
+            v[2] *= act_grad(__uint_as_float(eu[i][j].y << 16), ACT);
+            v[3] *= act_grad(__uint_as_float(eu[i][j].y & 0xFFFF0000u), ACT);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
+        }
         if (R) {
           v[0] += __uint_as_float(eres[i][j].x << 16);
           v[1] += __uint_as_float(eres[i][j].x & 0xFFFF0000u);
@@ -249,7 +279,9 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
     }
     if constexpr (ELDS) {
       // the tile, staged as bf16 rows in the stage buffer just consumed, leaves as whole 16-byte row
-      // chunks (a wave stores 4 full 256-byte rows per instruction instead of 16 x 32-byte pieces)
+      // chunks (a wave stores 4 full 256-byte rows per instruction instead of 16 x 32-byte pieces);
+      // the raw barrier does not wait for this wave's LDS writes, so retire them first
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier_mem();
 #pragma unroll
       for (int it = 0; it < (BM * CPR) / Cfg::NT; ++it) {
@@ -296,7 +328,7 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
     for (int kt = 0; kt < nk - 1; ++kt) step();
     epi_load(tile);                   // bias / residual loads fly during the last step's MFMAs
     step();
-    switch (p.act) {
+    switch (EXT ? p.uact : p.act) {
       case SVK_ACT_GELU: epilogue(tile, std::integral_constant<int, SVK_ACT_GELU>{}); break;
       case SVK_ACT_RELU: epilogue(tile, std::integral_constant<int, SVK_ACT_RELU>{}); break;
       case SVK_ACT_TANH: epilogue(tile, std::integral_constant<int, SVK_ACT_TANH>{}); break;
@@ -314,12 +346,12 @@ static int pk_slots(const void* fn, int nt) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <class Cfg, bool KTAIL, bool ELDS, int ASRC>
+template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT>
 static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.N + Cfg::BN - 1) / Cfg::BN;
   const long ntiles = (long)ntm * ntn;
   const int nk = (a.K + 63) / 64;
-  static const int slots = pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC>), Cfg::NT);
+  static const int slots = pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT>), Cfg::NT);
   const int grid = (int)std::min<long>(ntiles, slots);
   PkConv cv{};
   if (ASRC == 1) {
@@ -328,12 +360,13 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.cin = make_fastdiv((uint32_t)a.Cin);
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
-  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn, (int)ntiles,
+  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn, (int)ntiles,
                      nk);
   static char name[96];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d>", Cfg::BM, Cfg::BN, Cfg::WGM,
-             Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC);
+    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s>", Cfg::BM, Cfg::BN,
+             Cfg::WGM, Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC,
+             EXT ? "true" : "false");
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
@@ -344,11 +377,20 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   if (elds_env >= 0) elds = elds_env;
   elds = elds && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
-  if (ASRC == 1) {   // the im2col loader zero-fills K tails itself
-    return elds ? launch_pk<Cfg, false, true, 1>(a, st) : launch_pk<Cfg, false, false, 1>(a, st);
+  const bool tail = a.K % 64 != 0, ext = a.rscale || a.U;
+  if (ASRC == 1) {
+    // the im2col loader zero-fills the A side of a K tail itself, but the weight rows must read the
+    // zero block too: the last row's tail would otherwise read past the packed weights, and 0 x a
+    // NaN bit pattern found there is NaN.  No extended epilogue for convs.
+    if (elds) return tail ? launch_pk<Cfg, true, true, 1, false>(a, st) : launch_pk<Cfg, false, true, 1, false>(a, st);
+    return tail ? launch_pk<Cfg, true, false, 1, false>(a, st) : launch_pk<Cfg, false, false, 1, false>(a, st);
   }
-  if (elds) return a.K % 64 ? launch_pk<Cfg, true, true, 0>(a, st) : launch_pk<Cfg, false, true, 0>(a, st);
-  return a.K % 64 ? launch_pk<Cfg, true, false, 0>(a, st) : launch_pk<Cfg, false, false, 0>(a, st);
+  if (ext) {
+    if (elds) return tail ? launch_pk<Cfg, true, true, 0, true>(a, st) : launch_pk<Cfg, false, true, 0, true>(a, st);
+    return tail ? launch_pk<Cfg, true, false, 0, true>(a, st) : launch_pk<Cfg, false, false, 0, true>(a, st);
+  }
+  if (elds) return tail ? launch_pk<Cfg, true, true, 0, false>(a, st) : launch_pk<Cfg, false, true, 0, false>(a, st);
+  return tail ? launch_pk<Cfg, true, false, 0, false>(a, st) : launch_pk<Cfg, false, false, 0, false>(a, st);
 }
 
 // Eligible: bf16, K-contiguous operands (16-byte aligned rows, K % 8 == 0; conv: Cin % 8 == 0),
@@ -359,6 +401,7 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   if (getenv("SVK_NO_PK")) return 1;
   auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
   if (a.K % 8 || a.N % 4 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4)) return 1;
+  if (a.out_mode || (a.U && (a.ldu % 4 || !al(a.U, 8))) || (asrc != 0 && (a.U || a.rscale))) return 1;
   if (asrc == 0 && a.lda % 8) return 1;
   if (asrc == 1 && (a.Cin % 8 || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)) return 1;
   if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
@@ -376,9 +419,7 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     }
   }
   switch (cfg) {
-    case 2: return launch_pk_k<PkCfg<256, 128, 4, 2, 2>, 0>(a, st, !big);
     case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 0>(a, st, !big);
-    case 11: return launch_pk_k<PkCfg<128, 64, 2, 2, 3>, 0>(a, st, !big);
     default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !big);
   }
 }

@@ -76,6 +76,66 @@ def test_gemm_persistent_bf16(cuda, M, N, K, act, res):
     _close(got, tiled.double().cpu(), dt)
 
 
+@pytest.mark.parametrize("M,N,K,uact", [(60000, 256, 64, "gelu"), (20000, 320, 1280, "relu"), (7000, 72, 136, "gelu")])
+def test_gemm_persistent_ext_bf16(cuda, M, N, K, uact):
+    """Training epilogue on the persistent kernel: row scale (stochastic depth) x activation backward
+    from a saved pre-activation + residual; against fp64 and the tiled kernel (SVK_NO_PK)."""
+    import os
+    from svk import ops
+    dt = torch.bfloat16
+    a = _rand(M, K, dt=dt, dev=cuda, seed=21)
+    w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=22)
+    u = _rand(M, N, dt=dt, dev=cuda, seed=23)
+    r = _rand(M, N, dt=dt, dev=cuda, seed=24)
+    rows_per = 1000
+    s = torch.rand((M + rows_per - 1) // rows_per, generator=torch.Generator().manual_seed(25)).to(cuda)
+    kw = dict(residual=r, row_scale=s, rows_per=rows_per, dact=uact, dact_src=u)
+    got = ops.gemm(a, w, **kw)
+    os.environ["SVK_NO_PK"] = "1"
+    try:
+        tiled = ops.gemm(a, w, **kw)
+    finally:
+        del os.environ["SVK_NO_PK"]
+    torch.cuda.synchronize()
+    ur = u.double().requires_grad_(True)
+    g = (a.double() @ w.double().t()) * s.double().repeat_interleave(rows_per)[:M, None]
+    (F.gelu(ur) if uact == "gelu" else torch.relu(ur)).backward(g)
+    ref = ur.grad + r.double()
+    _close(got, ref.cpu(), dt)
+    _close(got, tiled.double().cpu(), dt)
+
+
+@pytest.mark.parametrize("kind", ["conv", "gemm"])
+def test_persistent_ktail_ignores_weight_slack(cuda, kind):
+    """K-tail steps of the persistent kernel read a zero block for BOTH operands: the bytes past the
+    last weight row (NaN here) must never reach the accumulators (0 x NaN = NaN).  Regression for the
+    im2col conv path, whose weight loads once ran past the packed weights on K % 64 != 0."""
+    from svk import ops
+    dt = torch.bfloat16
+    if kind == "conv":
+        B, H, W, Cin, Cout, k, s, p = 16, 224, 224, 8, 64, 7, 4, 3
+        K = k * k * Cin                                     # 392 = 6 x 64 + 8
+        x = _rand(B, H, W, Cin, dt=dt, dev=cuda, seed=31)
+    else:
+        M, Cout, K = 30000, 64, 200
+        x = _rand(M, K, dt=dt, dev=cuda, seed=31)
+    buf = torch.full((Cout * K + 4096,), float("nan"), device=cuda, dtype=dt)
+    w = buf[:Cout * K].view(Cout, K)
+    w.copy_(_rand(Cout, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=32))
+    b = _rand(Cout, dt=torch.float32, dev=cuda, seed=33)
+    if kind == "conv":
+        got = ops.conv2d_nhwc(x, w, k, s, p, bias=b)
+        wr = w.double().cpu().view(Cout, k, k, Cin).permute(0, 3, 1, 2)
+        ref = F.conv2d(x.cpu().double().permute(0, 3, 1, 2), wr, b.cpu().double(), stride=s, padding=p)
+        ref = ref.permute(0, 2, 3, 1)
+    else:
+        got = ops.gemm(x, w, b)
+        ref = x.cpu().double() @ w.cpu().double().t() + b.cpu().double()
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(got).all())
+    _close(got, ref, dt)
+
+
 @pytest.mark.parametrize("dt", DTS)
 def test_gemm_strided_views(cuda, dt):
     """kv[:, :, :C] style inputs and writes into a column slice (head concat buffer)."""
