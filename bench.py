@@ -51,6 +51,18 @@ def synthetic_batch(B, dev, seed):
     return x.contiguous(), y.contiguous(), flow
 
 
+def pmc_traffic(workload, kernel):
+    """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes of this workload
+    (FETCH_SIZE / WRITE_SIZE in separate passes, gfx950 FETCH correction; tools/pmc_traffic.py)."""
+    path = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            ent = json.load(f)[workload]["kernels"][kernel]
+    except (OSError, ValueError, KeyError):
+        return None, None
+    return ent["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+
+
 def video_lengths(n=40, seed=0):
     """Seeded test-split-like video lengths, U[1000, 6000] frames at 1 fps."""
     return [int(t) for t in np.random.default_rng(6000 + seed).integers(1000, 6001, size=n)]
@@ -322,6 +334,10 @@ def main():
                 "kernel_tflops": round(tflops, 2), "kernel_gbs": round(gbs, 1),
                 "all_gemm_tflops": round(sum(v[1] for v in per.values()) / (gemm_ms * 1e-3) / 1e12, 2),
                 "gemm_share_of_step": round(gemm_ms / prof_steps / (elapsed * 1e3 / args.steps), 3)}
+    traffic, src = pmc_traffic(args.workload, name)
+    if traffic is not None:
+        roofline["traffic"] = traffic
+        roofline["traffic_source"] = src + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, per launch)"
 
     if rank == 0:
         cpu = cpu_fn() if (world == 1 and not args.no_cpu_baseline) else None

@@ -373,10 +373,10 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
 
 template <class Cfg, int ASRC>
 static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
-  static const int elds_env = getenv("SVK_PK_ELDS") ? atoi(getenv("SVK_PK_ELDS")) : -1;   // tuning knob
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
-  if (elds_env >= 0) elds = elds_env;
-  elds = elds && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
+  if (g_tune[TUNE_PK_ELDS] >= 0) elds = g_tune[TUNE_PK_ELDS];
+  // the staged epilogue swizzles 16-byte chunks within a power-of-two row of chunks
+  elds = elds && (Cfg::BN & (Cfg::BN - 1)) == 0 && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
   const bool tail = a.K % 64 != 0, ext = a.rscale || a.U;
   if (ASRC == 1) {
     // the im2col loader zero-fills the A side of a K tail itself, but the weight rows must read the
@@ -397,7 +397,7 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
 // plain epilogue, C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when
 // not eligible.  asrc: 0 dense A, 1 implicit-GEMM conv (A = NHWC map, GemmArgs conv geometry).
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
-  static const int force = getenv("SVK_PK_CFG") ? atoi(getenv("SVK_PK_CFG")) : -1;   // tuning knob
+  const int force = g_tune[TUNE_PK_CFG];
   if (getenv("SVK_NO_PK")) return 1;
   auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
   if (a.K % 8 || a.N % 4 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4)) return 1;
@@ -406,21 +406,38 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   if (asrc == 1 && (a.Cin % 8 || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)) return 1;
   if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
   int cfg = force;
-  // Measured on the MiT-b2 shapes (tools/gemm_bench.py, profiles/r01/gemm_pk_tuning.txt): deeper
-  // rings at 1 workgroup/CU lose to 2-3 resident workgroups with a 2-stage ring.  The long-K
-  // (>= 512) GEMMs with N % 128 == 0 run best on 128 x 128 tiles with the register epilogue; all
-  // others (short K: output-write-bound) on 128 x 64 tiles with the LDS-staged 16-byte-store epilogue.
+  // Measured on the MiT-b2 B = 256 shapes, all variants interleaved in one process
+  // (tools/tune_bench.py, profiles/r01/tune_r01.txt):
+  //  * dense, long K (>= 512) with N % 128 == 0, or few rows (M < 32k, e.g. the stage-4 / head GEMMs
+  //    at M = 12544): 128 x 128 tiles with the register epilogue;
+  //  * every other dense shape (short K: output-write-bound): 128 x 64 with the LDS-staged epilogue;
+  //  * implicit-GEMM convs: 128 x 128 never wins (the im2col DMA address math per tile is the cost);
+  //    64 x 64 when the 128-row tiling leaves < 512 tiles and N <= 128 (the k = s patchify convs of
+  //    the sequence reduction: 98 row tiles at B = 256), 64 x 128 for N % 128 == 0, else 128 x 64.
   const bool big = a.K >= 512 && a.N % 128 == 0;
-  if (cfg < 0) cfg = big ? 0 : 10;
+  if (cfg < 0) {
+    if (asrc == 1) {
+      const long t128 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64);
+      cfg = (t128 < 512 && a.N <= 128) ? 30 : (a.N % 128 == 0 ? 20 : 10);
+    } else {
+      cfg = (big || (a.N % 128 == 0 && a.M < 32768)) ? 0 : 10;
+    }
+  }
+  const bool reg_epi = cfg == 0 && (big || a.M < 32768);
+  // cfg: 0 = 128x128, 10 = 128x64, 20 = 64x128, 30 = 64x64
   if (asrc == 1) {
     switch (cfg) {
       case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 1>(a, st, !big);
-      default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 1>(a, st, !big);
+      case 20: return launch_pk_k<PkCfg<64, 128, 2, 2, 2>, 1>(a, st, !big);
+      case 30: return launch_pk_k<PkCfg<64, 64, 2, 2, 2>, 1>(a, st, !big);
+      default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 1>(a, st, !reg_epi);
     }
   }
   switch (cfg) {
     case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 0>(a, st, !big);
-    default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !big);
+    case 20: return launch_pk_k<PkCfg<64, 128, 2, 2, 2>, 0>(a, st, !big);
+    case 30: return launch_pk_k<PkCfg<64, 64, 2, 2, 2>, 0>(a, st, !big);
+    default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
   }
 }
 

@@ -1,6 +1,8 @@
 // svk runtime: error reporting and version for the C ABI.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "svk_common.h"
 
@@ -27,7 +29,27 @@ int check_launch(const char* what) {
   return SVK_OK;
 }
 
+// Tuning knobs (tile configuration / kernel variant overrides for A/B measurements in one process);
+// initial values from the environment, -1 = automatic choice.
+static const char* const k_knob_names[TUNE_NKNOBS] = {"pk_cfg", "pk_elds", "dw_lds", "dw_rows"};
+static const char* const k_knob_env[TUNE_NKNOBS] = {"SVK_PK_CFG", "SVK_PK_ELDS", "SVK_DW_LDS", "SVK_DW_LR"};
+static int init_knob(int i) {
+  const char* e = getenv(k_knob_env[i]);
+  return e ? atoi(e) : -1;
+}
+int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3)};
+
 }  // namespace svk
+
+extern "C" int svk_tune(const char* knob, int value) {
+  for (int i = 0; i < svk::TUNE_NKNOBS; ++i)
+    if (knob && strcmp(knob, svk::k_knob_names[i]) == 0) {
+      svk::g_tune[i] = value;
+      return SVK_OK;
+    }
+  svk::set_error("svk_tune: unknown knob %s", knob ? knob : "(null)");
+  return SVK_EINVAL;
+}
 
 extern "C" const char* svk_version(void) { return "svk 0.1.0 gfx950"; }
 extern "C" const char* svk_last_error(void) { return svk::g_err; }

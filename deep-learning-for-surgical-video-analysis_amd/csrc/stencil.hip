@@ -135,6 +135,95 @@ __global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, 
   }
 }
 
+// LDS-tiled variant (bf16, C % 64 == 0): one workgroup per (frame, strip of R rows, 64-channel
+// block).  The (R + 2) x (W + 2) halo tile of the block's 64 channels is read from HBM once —
+// every 16-byte chunk by exactly one lane, out-of-image pixels as zeros (the conv's zero padding),
+// addresses clamped so the loads are branch-free — and the 9 taps of every output are then read
+// from LDS (a wave's 64 lanes = 8 pixels x 8 channel groups: 1 KiB contiguous per ds_read_b128,
+// conflict-free).  The strip kernel above reads each input vector 3 (R + 2) / R times through the
+// vector caches instead; here the only re-read is the 2-row halo (2 / R, mostly L2).
+// Workgroup ids are XCD-remapped so that consecutive strips of a frame (which share halo rows)
+// run on one XCD's L2.
+__global__ __launch_bounds__(256) void dwconv3x3_lds_bf16(const bf16* __restrict__ X, const float* __restrict__ w,
+                                                          const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                          bf16* __restrict__ Ypre, int H, int W, int C, int R,
+                                                          int nstrip, int act) {
+  extern __shared__ __attribute__((aligned(16))) uint4 tile[];   // [(R + 2)][(W + 2)][8] 16-byte chunks
+  const int ncb = C >> 6;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int s = id % nstrip, cb = (id / nstrip) % ncb, b = id / (nstrip * ncb);
+  const int y0 = s * R, TW = W + 2;
+  const int tid = threadIdx.x;
+  const bf16* Xb = X + (long)b * H * W * C + cb * 64;
+
+  // stage the halo tile: chunk i -> (row, col, c); branch-free clamped loads, zeros outside
+  const int nchunk = (R + 2) * TW * 8;
+  for (int i0 = 0; i0 < nchunk; i0 += 4 * 256) {
+    uint4 v[4];
+    bool ok[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 256 + tid;
+      const int row = i / (TW * 8), rem = i - row * (TW * 8), col = rem >> 3, c = rem & 7;
+      const int y = y0 - 1 + row, x = col - 1;
+      ok[u] = i < nchunk && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+      const int yc = min(max(y, 0), H - 1), xc = min(max(x, 0), W - 1);
+      v[u] = *reinterpret_cast<const uint4*>(Xb + ((long)yc * W + xc) * C + c * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 256 + tid;
+      if (i < nchunk) tile[i] = ok[u] ? v[u] : uint4{0u, 0u, 0u, 0u};
+    }
+  }
+
+  const int c = tid & 7, pl = tid >> 3;
+  const int c0 = cb * 64 + c * 8;
+  f32x2 wt[9][4], bs[4];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wt[k][j] = *reinterpret_cast<const f32x2*>(w + k * C + c0 + 2 * j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f32x2*>(bias + c0 + 2 * j);
+  __syncthreads();
+
+  const int rows = min(R, H - y0);
+  bf16* Yb = Y + (long)b * H * W * C + c0;
+  bf16* Pb = Ypre ? Ypre + (long)b * H * W * C + c0 : nullptr;
+  for (int q = pl; q < rows * W; q += 32) {
+    const int r = q / W, x = q - r * W;
+    f32x2 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bs[j];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        Vec8<bf16> v;
+        *reinterpret_cast<uint4*>(v.u) = tile[((r + dy) * TW + x + dx) * 8 + c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = pair(v, j) * wt[dy * 3 + dx][j] + acc[j];
+      }
+    const long off = ((long)(y0 + r) * W + x) * C;
+    bf16 o[8];
+    if (Pb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[2 * j] = (bf16)acc[j].x; o[2 * j + 1] = (bf16)acc[j].y; }
+      store_vec8(Pb + off, o);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x2 g = act == SVK_ACT_GELU ? gelu_fast2(acc[j]) : f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
+      o[2 * j] = (bf16)g.x;
+      o[2 * j + 1] = (bf16)g.y;
+    }
+    store_vec8(Yb + off, o);
+  }
+}
+
 template <typename T>
 __global__ void dwconv3x3_scalar(const T* __restrict__ X, const float* __restrict__ w, const float* __restrict__ bias,
                                  T* __restrict__ Y, T* __restrict__ Ypre, int B, int H, int W, int C, int act) {
@@ -337,6 +426,22 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
     const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 15) == 0;
+    const int lds_env = g_tune[TUNE_DW_LDS], rows_env = g_tune[TUNE_DW_ROWS];   // svk_tune knobs
+    if (sizeof(T) == 2 && vec && C % 64 == 0 && lds_env > 0) {
+      // strip height: the tallest strip whose halo tile fits 48 KiB (3 workgroups per CU)
+      int R = rows_env > 0 ? rows_env : 49152 / ((W + 2) * 128) - 2;
+      R = std::max(1, std::min(R, H));
+      const size_t lds = (size_t)(R + 2) * (W + 2) * 128;
+      if (lds <= 65536) {
+        const int nstrip = (H + R - 1) / R;
+        const long nwg = (long)B * nstrip * (C / 64);
+        if (nwg < 0x7fffffffL) {
+          hipLaunchKernelGGL(dwconv3x3_lds_bf16, dim3((unsigned)nwg), dim3(256), lds, st, (const bf16*)X, w, bias,
+                             (bf16*)Y, (bf16*)Ypre, H, W, C, R, nstrip, act);
+          return check_launch("dwconv3x3_lds");
+        }
+      }
+    }
     if (vec) {
       constexpr int R = sizeof(T) == 2 ? 7 : 2;   // bf16: 56 / 28 / 14 / 7-row maps in whole strips
       const int nstrip = (H + R - 1) / R;

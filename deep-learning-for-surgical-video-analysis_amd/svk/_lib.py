@@ -17,6 +17,7 @@ P = c_void_p
 # name -> argtypes; every entry point returns int status except the two string getters.
 SIGNATURES = {
     "svk_gemm": [c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, c_int, c_int, c_int, c_int, P],
+    "svk_tune": [c_char_p, c_int],
     "svk_conv2d_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_layernorm": [c_int, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
     "svk_attention": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,

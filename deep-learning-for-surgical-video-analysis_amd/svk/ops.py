@@ -68,6 +68,11 @@ def set_profiler(records):
     _PROF = records
 
 
+def tune(knob, value):
+    """Set a kernel-selection knob (svk_tune: "pk_cfg", "pk_elds", "dw_lds", "dw_rows"; -1 = auto)."""
+    _lib.call("svk_tune", knob.encode(), int(value))
+
+
 def _last_kernel():
     """The kernel instantiation the library launched last on this thread (svk_last_kernel)."""
     return _lib.load().svk_last_kernel().decode()

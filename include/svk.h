@@ -35,6 +35,11 @@ const char* svk_version(void);
 const char* svk_last_error(void);
 /* Kernel instantiation launched last by the calling thread (GEMM / conv family; for profilers). */
 const char* svk_last_kernel(void);
+/* Tuning knobs for A/B measurements inside one process (no effect on results): "pk_cfg" (persistent
+ * GEMM tile: -1 auto, 0 128x128, 10 128x64, 20 64x128, 30 64x64), "pk_elds" (-1 auto,
+ * 0/1 staged epilogue), "dw_lds" (1 = LDS-tiled depthwise conv), "dw_rows" (its strip height).
+ * Initial values from SVK_PK_CFG / SVK_PK_ELDS / SVK_DW_LDS / SVK_DW_LR. */
+int svk_tune(const char* knob, int value);
 
 /* C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]
  * Replaces nn.Linear (+ activation, + residual add) at: Attention q/kv/proj

@@ -105,6 +105,58 @@ def test_gemm_persistent_ext_bf16(cuda, M, N, K, uact):
     _close(got, tiled.double().cpu(), dt)
 
 
+@pytest.mark.parametrize("cfg", [0, 10, 20, 30])
+def test_persistent_tile_configs(cuda, cfg):
+    """Every persistent-GEMM tile configuration (forced through svk_tune) on dense and implicit-GEMM
+    shapes with M / N / K tails, staged and register epilogues."""
+    from svk import ops
+    dt = torch.bfloat16
+    try:
+        ops.tune("pk_cfg", cfg)
+        for M, N, K, res in ((5000, 320, 1280, True), (777, 136, 200, False), (12544, 512, 512, True)):
+            a = _rand(M, K, dt=dt, dev=cuda, seed=51)
+            w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=52)
+            b = _rand(N, dt=torch.float32, dev=cuda, seed=53)
+            r = _rand(M, N, dt=dt, dev=cuda, seed=54) if res else None
+            got = ops.gemm(a, w, b, act="gelu", residual=r)
+            ref = F.gelu(a.double() @ w.double().t() + b.double())
+            if res:
+                ref = ref + r.double()
+            _close(got, ref.cpu(), dt)
+        x = _rand(6, 28, 28, 128, dt=dt, dev=cuda, seed=55)
+        wc = _rand(320, 3 * 3 * 128, dt=dt, dev=cuda, scale=(9 * 128) ** -0.5, seed=56)
+        bc = _rand(320, dt=torch.float32, dev=cuda, seed=57)
+        got = ops.conv2d_nhwc(x, wc, 3, 2, 1, bias=bc, act="relu")
+        wr = wc.double().cpu().view(320, 3, 3, 128).permute(0, 3, 1, 2)
+        ref = F.conv2d(x.cpu().double().permute(0, 3, 1, 2), wr, bc.cpu().double(), stride=2, padding=1)
+        _close(got, torch.relu(ref).permute(0, 2, 3, 1), dt)
+    finally:
+        ops.tune("pk_cfg", -1)
+
+
+@pytest.mark.parametrize("rows", [1, 3, 8])
+def test_dwconv_lds_variant(cuda, rows):
+    """The LDS-tiled depthwise conv (svk_tune dw_lds = 1) at several strip heights, with the
+    pre-activation store, against fp64."""
+    from svk import ops
+    dt = torch.bfloat16
+    try:
+        ops.tune("dw_lds", 1)
+        ops.tune("dw_rows", rows)
+        for B, H, W, C in ((2, 28, 28, 256), (3, 7, 7, 128), (1, 10, 13, 64)):
+            x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=61)
+            w = _rand(C, 1, 3, 3, dt=torch.float32, dev="cpu", scale=0.4, seed=62)
+            b = _rand(C, dt=torch.float32, dev=cuda, seed=63)
+            pre = torch.empty_like(x)
+            got = ops.dwconv3x3(x, w.reshape(C, 9).t().contiguous().to(cuda), b, act="gelu", pre_out=pre)
+            ref = F.conv2d(x.cpu().double().permute(0, 3, 1, 2), w.double(), b.cpu().double(), padding=1, groups=C)
+            _close(pre, ref.permute(0, 2, 3, 1), dt)
+            _close(got, F.gelu(ref).permute(0, 2, 3, 1), dt)
+    finally:
+        ops.tune("dw_lds", -1)
+        ops.tune("dw_rows", -1)
+
+
 @pytest.mark.parametrize("kind", ["conv", "gemm"])
 def test_persistent_ktail_ignores_weight_slack(cuda, kind):
     """K-tail steps of the persistent kernel read a zero block for BOTH operands: the bytes past the
@@ -205,7 +257,8 @@ def test_attention(cuda, dt, B, Nq, Nk, heads, hd):
 
 
 @pytest.mark.parametrize("dt", DTS)
-@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 256), (1, 7, 7, 2048), (2, 14, 14, 1280), (1, 5, 6, 12)])
+@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 256), (1, 7, 7, 2048), (2, 14, 14, 1280), (1, 5, 6, 12),
+                                     (3, 28, 28, 512), (2, 30, 17, 128), (1, 9, 3, 64)])
 def test_dwconv3x3_gelu(cuda, dt, B, H, W, C):
     from svk import ops
     x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=15)

@@ -1,0 +1,63 @@
+"""HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE; one counter group per
+pass, MI355X_MICROARCH.md 'HBM'): bytes = 2 x FETCH_SIZE x 1024 (gfx950 FETCH_SIZE counts half the
+bytes of a wide streaming read) + WRITE_SIZE x 1024, averaged over every dispatch of a kernel.
+Writes {workload: {kernel: {...}}} into a JSON file that bench.py reads for roofline.traffic.
+
+Usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON WORKLOAD"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+
+def kernel_key(name):
+    """rocprofv3 kernel name -> the instantiation name bench.py reports (svk_last_kernel form)."""
+    n = name.strip()
+    if n.startswith("void "):
+        n = n[5:]
+    n = n.replace("svk::", "")
+    depth = 0
+    for i, ch in enumerate(n):      # cut the argument list: first '(' outside template brackets
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            return n[:i]
+    return n
+
+
+def per_kernel(path, counter):
+    vals = defaultdict(list)
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter:
+                vals[kernel_key(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    fetch_csv, write_csv, out_json, workload = sys.argv[1:5]
+    fetch, write = per_kernel(fetch_csv, "FETCH_SIZE"), per_kernel(write_csv, "WRITE_SIZE")
+    table = {}
+    for k in sorted(set(fetch) & set(write)):
+        f, w = fetch[k], write[k]
+        fk, wk = sum(f) / len(f), sum(w) / len(w)
+        table[k] = {"dispatches": len(f), "fetch_size_kb_avg": round(fk, 1), "write_size_kb_avg": round(wk, 1),
+                    "hbm_bytes_per_launch": round((2.0 * fk + wk) * 1024.0)}
+    data = {}
+    if os.path.exists(out_json):
+        with open(out_json) as fh:
+            data = json.load(fh)
+    data[workload] = {"source": [os.path.relpath(fetch_csv), os.path.relpath(write_csv)],
+                      "formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, averaged", "kernels": table}
+    with open(out_json, "w") as fh:
+        json.dump(data, fh, indent=1, sort_keys=True)
+    for k, v in sorted(table.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["dispatches"])[:15]:
+        print(f"{v['hbm_bytes_per_launch'] / 1e6:10.2f} MB/launch  n={v['dispatches']:5d}  {k[:110]}")
+
+
+if __name__ == "__main__":
+    main()

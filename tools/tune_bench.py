@@ -1,0 +1,104 @@
+"""In-process A/B of kernel variants on the MiT-b2 (B = 256) shapes: every variant of a shape is timed
+in interleaved rounds (median of rounds), switching variants with svk_tune.
+Usage (GPU box): python tools/tune_bench.py [gemm|dw|all] [--rounds 5]"""
+import argparse
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "deep-learning-for-surgical-video-analysis_amd"))
+from svk import ops  # noqa: E402
+
+# (M, N, K, residual) at B = 256 frames: token GEMMs and the implicit-GEMM convs (as (B, H, W, Cin, Cout, k, s, p))
+GEMMS = [(802816, 256, 64, False), (802816, 64, 256, True), (200704, 512, 128, False), (200704, 128, 512, True),
+         (200704, 128, 128, True), (50176, 1280, 320, False), (50176, 320, 1280, True), (50176, 320, 320, True),
+         (12544, 2048, 512, False), (12544, 512, 2048, True), (12544, 2048, 1024, False), (12544, 512, 512, True),
+         (12544, 1024, 512, False), (12544, 640, 320, False)]
+CONVS = [(256, 224, 224, 8, 64, 7, 4, 3), (256, 56, 56, 64, 64, 8, 8, 0), (256, 56, 56, 64, 128, 3, 2, 1),
+         (256, 28, 28, 128, 128, 4, 4, 0), (256, 28, 28, 128, 320, 3, 2, 1), (256, 14, 14, 320, 320, 2, 2, 0),
+         (256, 14, 14, 320, 512, 3, 2, 1)]
+CFGS = [0, 10, 20, 30]
+DW = [(56, 256), (28, 512), (14, 1280), (7, 2048)]
+
+
+def timeit(fn, reps):
+    fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps * 1e3   # us
+
+
+def ab(name, variants, fn, rounds, reps, flops=None, nbytes=None):
+    res = {v: [] for v, _ in variants}
+    for _ in range(rounds):
+        for v, setup in variants:
+            setup()
+            res[v].append(timeit(fn, reps))
+    med = {v: statistics.median(t) for v, t in res.items()}
+    best = min(med, key=med.get)
+    parts = []
+    for v, t in med.items():
+        extra = f" {flops / t / 1e6:6.0f}TF" if flops else ""
+        extra += f" {nbytes / t / 1e3:6.0f}GB/s" if nbytes else ""
+        parts.append(f"{v}={t:7.1f}us{extra}{' *' if v == best else ''}")
+    print(f"{name:34s} " + "  ".join(parts), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("what", nargs="?", default="all")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    dt = torch.bfloat16
+    if args.what in ("gemm", "all"):
+        for M, N, K, res in GEMMS:
+            a = torch.randn(M, K, device=dev).to(dt)
+            w = (torch.randn(N, K, device=dev) * K ** -0.5).to(dt)
+            b = torch.randn(N, device=dev)
+            r = torch.randn(M, N, device=dev).to(dt) if res else None
+            out = torch.empty(M, N, device=dev, dtype=dt)
+            variants = [(f"c{c}", (lambda c=c: ops.tune("pk_cfg", c))) for c in CFGS]
+            ab(f"gemm {M}x{N}x{K}{' +R' if res else ''}", variants, lambda: ops.gemm(a, w, b, residual=r, out=out),
+               args.rounds, args.reps, flops=2.0 * M * N * K, nbytes=(M * K + N * K + M * N * (2 if res else 1)) * 2)
+            del a, w, r, out
+        for B, H, W, Cin, Cout, k, s, p in CONVS:
+            x = torch.randn(B, H, W, Cin, device=dev).to(dt)
+            wp = (torch.randn(Cout, k * k * Cin, device=dev) * (k * k * Cin) ** -0.5).to(dt)
+            b = torch.randn(Cout, device=dev)
+            OH = (H + 2 * p - k) // s + 1
+            M, K = B * OH * OH, k * k * Cin
+            variants = [(f"c{c}", (lambda c=c: ops.tune("pk_cfg", c))) for c in CFGS]
+            ab(f"conv {M}x{Cout}x{K} k{k}s{s}", variants, lambda: ops.conv2d_nhwc(x, wp, k, s, p, bias=b),
+               args.rounds, args.reps, flops=2.0 * M * Cout * K, nbytes=(x.numel() + Cout * K + M * Cout) * 2)
+            del x, wp
+        ops.tune("pk_cfg", -1)
+    if args.what in ("dw", "all"):
+        for H, C in DW:
+            x = torch.randn(256, H, H, C, device=dev).to(dt)
+            taps = torch.randn(9, C, device=dev)
+            bias = torch.randn(C, device=dev)
+
+            def knob(lds, rows):
+                def f():
+                    ops.tune("dw_lds", lds)
+                    ops.tune("dw_rows", rows)
+                return f
+            variants = [("strip", knob(0, -1))] + [(f"lds{r}", knob(1, r)) for r in (2, 4, 7, 8, 14) if r <= H]
+            ab(f"dwconv H={H} C={C}", variants, lambda: ops.dwconv3x3(x, taps, bias, act="gelu"), args.rounds,
+               args.reps, nbytes=2 * x.numel() * 2)
+            del x
+        ops.tune("dw_lds", -1)
+        ops.tune("dw_rows", -1)
+
+
+if __name__ == "__main__":
+    main()
