@@ -721,6 +721,61 @@ extern "C" int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, in
   });
 }
 
+// Sequence-reduction conv + LayerNorm (Attention.sr -> Attention.norm, mix_transformer_evp.py:115-117):
+// for the long-K patchify convs whose row-tile grid cannot fill the chip, split K into ks parts
+// written as f32 slabs and reduce them in the LayerNorm kernel (workspace ks * M * Cout * 4 bytes);
+// otherwise the conv writes Y and the LayerNorm runs in place.
+static int conv_ln_ksplit(int dtype, long M, int N, int K, int Cin) {
+  // measured (B = 256): splitting pays for the N <= 128 stages (64 x 64 tiles, 196 / 392 of them);
+  // at N = 320 (490 128 x 64 tiles) the extra slab pass costs more than the occupancy gains
+  if (dtype != SVK_BF16 || K % 64 || Cin % 8 || N % 4 || N > 128) return 1;
+  const int nk = K / 64;
+  const long tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  int ks = 1;
+  while (tiles * ks < 768 && nk % (2 * ks) == 0 && nk / (2 * ks) >= 4) ks *= 2;
+  return ks;
+}
+
+extern "C" long svk_conv2d_ln_workspace(int dtype, int B, int H, int W, int Cin, int Cout, int k, int stride, int pad) {
+  if (B <= 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || k <= 0 || stride <= 0 || pad < 0) return 0;
+  const long OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  if (OH <= 0 || OW <= 0) return 0;
+  const long M = (long)B * OH * OW;
+  const int ks = conv_ln_ksplit(dtype, M, Cout, k * k * Cin, Cin);
+  return ks > 1 ? (long)ks * M * Cout * 4 : 0;
+}
+
+extern "C" int svk_conv2d_ln_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* Wt,
+                                  const float* bias, const float* gamma, const float* beta, float eps, void* Y,
+                                  int Cout, int k, int stride, int pad, void* ws, long ws_bytes, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || Cout <= 0 || k <= 0 || stride <= 0 || pad < 0 || !X || !Wt || !Y ||
+      !bias || !gamma || !beta) {
+    set_error("svk_conv2d_ln_nhwc: bad args"); return SVK_EINVAL;
+  }
+  const int OH = (H + 2 * pad - k) / stride + 1, OW = (W + 2 * pad - k) / stride + 1;
+  if (OH <= 0 || OW <= 0) { set_error("svk_conv2d_ln_nhwc: empty output"); return SVK_EINVAL; }
+  if (B == 0) return SVK_OK;
+  const long M = (long)B * OH * OW;
+  if (M > 0x7fffffffL) { set_error("svk_conv2d_ln_nhwc: too many output pixels"); return SVK_EUNSUPPORTED; }
+  hipStream_t st = (hipStream_t)stream;
+  const int ks = conv_ln_ksplit(dtype, M, Cout, k * k * Cin, Cin);
+  if (ks > 1 && ws && ws_bytes >= (long)ks * M * Cout * 4) {
+    GemmArgs a{};
+    a.A = X; a.lda = 0; a.W = Wt; a.ldw = (long)k * k * Cin; a.C = Y; a.ldc = Cout;
+    a.M = (int)M; a.N = Cout; a.K = k * k * Cin;
+    a.H = H; a.Wd = W; a.Cin = Cin; a.OH = OH; a.OW = OW; a.kw = k; a.stride = stride; a.pad = pad;
+    a.ksplit = ks; a.slab = static_cast<float*>(ws);
+    if (gemm_pk_conv_splitk(a, st) == 0) {
+      int rc = check_launch("conv2d_ln splitk");
+      if (rc) return rc;
+      return splitk_layernorm(a.slab, ks, bias, static_cast<bf16*>(Y), (int)M, Cout, gamma, beta, eps, st);
+    }
+  }
+  int rc = svk_conv2d_nhwc(dtype, X, B, H, W, Cin, Wt, bias, nullptr, Y, Cout, k, stride, pad, SVK_ACT_NONE, stream);
+  if (rc) return rc;
+  return svk_layernorm(dtype, Y, Cout, Y, Cout, gamma, beta, (int)M, Cout, eps, stream);
+}
+
 extern "C" int svk_conv2d_dgrad_nhwc(int dtype, const void* dY, int B, int OH, int OW, int Cout, const void* Wd,
                                      const void* R, void* dX, int H, int W, int Cin, int k, int stride, int pad,
                                      void* stream) {

@@ -23,10 +23,13 @@ struct GemmArgs {
   // out_mode 1: C (and R) are an NHWC map [B, uH, uW, uC] and GEMM row m = (b, py, px) of the
   // (uH/us) x (uW/us) patch grid, column n = (i, j, ci): the adjoint of a k = s patchify conv.
   int out_mode, uH, uW, us, uC;
+  // split-K (gemm_pk_conv_splitk): raw f32 partial sums of ksplit K parts -> slab [ksplit][M][N]
+  int ksplit; float* slab;
 };
 
 // gemm_pk.hip: persistent LDS-DMA bf16 GEMM / implicit-GEMM conv (asrc 1) for the plain-epilogue
 // case; returns 0 when it launched, 1 when the arguments are not eligible (caller falls back to gemm_kernel).
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
+int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
 
 }  // namespace svk

@@ -93,8 +93,11 @@ __device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current
   }
 }
 
-template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT>
-__global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk) {
+// SPLIT: split-K — unit u = (tile u / ks, K part u % ks) covers nk K-steps of the tile's ks * nk; the
+// epilogue stores raw f32 partial sums to slab part (p.slab + (part * M + m) * N + n) and a separate
+// reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
+template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
+__global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
   __shared__ __attribute__((aligned(1024))) char smem[Cfg::LDS];
@@ -113,8 +116,9 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
   // this thread's DMA lane covers 16-byte chunk q = (wave * LD + i) * 64 + lane of the stage image
   // ASRC == 1: im2col rows of this thread's A slots (output pixel -> first input tap), per tile
   int crb[Cfg::A_LD], ciy[Cfg::A_LD], cix[Cfg::A_LD];
-  auto issue = [&](int tile, int kt, int buf) {
-    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN, k0 = kt * Cfg::BK;
+  auto issue = [&](int unit, int kt, int buf) {
+    const int tile = SPLIT ? unit / ks : unit, part = unit - tile * ks;
+    const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN, k0 = (SPLIT ? part * nk + kt : kt) * Cfg::BK;
     const uint32_t sa = lds0 + buf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
     if constexpr (ASRC == 1) {
       // every A slot of a lane has the same 16-byte chunk column c (rows differ by multiples of 8)
@@ -196,8 +200,8 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
   float4 ebias[TN];
   const bf16* R = static_cast<const bf16*>(p.R);
-  auto epi_load = [&](int tile) {
-    const int n0 = (tile % ntn) * BN;
+  auto epi_load = [&](int unit) {
+    const int n0 = ((SPLIT ? unit / ks : unit) % ntn) * BN;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
@@ -208,9 +212,23 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
   char* stile = nullptr;                  // ELDS: stage buffer consumed by the tile's last step
   // EXT (training): v = act(acc + bias) * rscale[m / rdiv] * uact'(U[m, n]) + R[m, n]; the template
   // activation is then the BACKWARD one (uact), the forward act stays a runtime switch.
-  auto epilogue = [&](int tile, auto act_c) {
+  auto epilogue = [&](int unit, auto act_c) {
     constexpr int ACT = decltype(act_c)::value;
+    const int tile = SPLIT ? unit / ks : unit, part = unit - tile * ks;
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN;
+    if constexpr (SPLIT) {   // raw partial sums, 16-byte f32 stores (N % 4 == 0)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + fq * 4;
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wm * WM + i * 16 + fr;
+          if (m < p.M && n < p.N) *reinterpret_cast<f32x4*>(p.slab + ((long)part * p.M + m) * p.N + n) = acc[i][j];
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      return;
+    }
     bf16* C = static_cast<bf16*>(p.C);
     uint2 eres[TM][TN], eu[TM][TN];
     float ers[TM];
@@ -346,12 +364,14 @@ static int pk_slots(const void* fn, int nt) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT>
+template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
 static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.N + Cfg::BN - 1) / Cfg::BN;
-  const long ntiles = (long)ntm * ntn;
-  const int nk = (a.K + 63) / 64;
-  static const int slots = pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT>), Cfg::NT);
+  const int ks = SPLIT ? a.ksplit : 1;
+  const long ntiles = (long)ntm * ntn * ks;
+  const int nk = (a.K + 63) / 64 / ks;   // K-steps per unit (the caller makes ks divide them)
+  static const int slots =
+      pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), Cfg::NT);
   const int grid = (int)std::min<long>(ntiles, slots);
   PkConv cv{};
   if (ASRC == 1) {
@@ -360,13 +380,13 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.cin = make_fastdiv((uint32_t)a.Cin);
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
-  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn, (int)ntiles,
-                     nk);
+  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
+                     (int)ntiles, nk, ks);
   static char name[96];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s>", Cfg::BM, Cfg::BN,
+    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s%s>", Cfg::BM, Cfg::BN,
              Cfg::WGM, Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC,
-             EXT ? "true" : "false");
+             EXT ? "true" : "false", SPLIT ? ", true" : "");
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
@@ -439,6 +459,18 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 30: return launch_pk_k<PkCfg<64, 64, 2, 2, 2>, 0>(a, st, !big);
     default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
   }
+}
+
+// Split-K implicit-GEMM conv into f32 partial slabs (a.ksplit parts, a.slab [ksplit][M][N]): for the
+// k = s patchify convs of the sequence reduction, whose 98-row-tile grids (B = 256) cannot fill the
+// chip with a long K (2048 / 4096).  Returns 1 when not eligible.
+int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st) {
+  auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
+  if (a.ksplit < 2 || !a.slab || a.K % 64 || ((a.K / 64) % a.ksplit) || a.N % 4 || a.Cin % 8 || !al(a.A, 16) ||
+      !al(a.W, 16) || !al(a.slab, 16) || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)
+    return 1;
+  if (a.N <= 128) return launch_pk<PkCfg<64, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
+  return launch_pk<PkCfg<128, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
 }
 
 }  // namespace svk

@@ -1,5 +1,6 @@
 // Row-wise normalisation / reduction kernels: LayerNorm, softmax over channels, row-mean pool.
 #include "svk_common.h"
+#include <type_traits>
 
 namespace svk {
 
@@ -151,6 +152,87 @@ __global__ void mean_rows_kernel(const T* __restrict__ X, long ldx, float* __res
   float s = 0.f;
   for (int r = 0; r < R; ++r) s += to_f(x[(long)r * ldx]);
   Y[(long)b * C + c] = s / R;
+}
+
+// Split-K reduction + bias + LayerNorm (svk_conv2d_ln_nhwc): Y[m, :] = LN(sum_s S[s][m][:] + bias),
+// bf16 out.  Same lane layout as layernorm_vec_kernel: LPR lanes per row, NCH 8-channel chunks per
+// lane, f32 sums, two-pass mean / variance over the row held in registers.
+template <int LPR, int NCH>
+__global__ __launch_bounds__(256) void splitk_ln_kernel(const float* __restrict__ S, int ks, const float* __restrict__ bias,
+                                                        bf16* __restrict__ Y, const float* __restrict__ g,
+                                                        const float* __restrict__ b, int M, int C, float eps) {
+  constexpr int RPW = 64 / LPR;
+  const int lane = threadIdx.x & 63, sub = lane % LPR;
+  const long row = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / LPR;
+  const bool valid = row < M;
+  const int nchunks = C >> 3;
+  float v[NCH][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = sub + LPR * i;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    if (valid && ch < nchunks) {
+      const float4 b0 = *reinterpret_cast<const float4*>(bias + ch * 8), b1 = *reinterpret_cast<const float4*>(bias + ch * 8 + 4);
+      v[i][0] = b0.x; v[i][1] = b0.y; v[i][2] = b0.z; v[i][3] = b0.w;
+      v[i][4] = b1.x; v[i][5] = b1.y; v[i][6] = b1.z; v[i][7] = b1.w;
+      for (int k = 0; k < ks; ++k) {
+        const float* src = S + ((long)k * M + row) * C + ch * 8;
+        const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+        v[i][0] += x0.x; v[i][1] += x0.y; v[i][2] += x0.z; v[i][3] += x0.w;
+        v[i][4] += x1.x; v[i][5] += x1.y; v[i][6] += x1.z; v[i][7] += x1.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[i][e];
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mean = s / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = sub + LPR * i;
+    if (ch < nchunks) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
+  }
+#pragma unroll
+  for (int o = LPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rstd = 1.0f / sqrtf(q / C + eps);
+  if (!valid) return;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int ch = sub + LPR * i;
+    if (ch >= nchunks) continue;
+    bf16 t[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t[e] = (bf16)((v[i][e] - mean) * rstd * g[ch * 8 + e] + b[ch * 8 + e]);
+    *reinterpret_cast<uint4*>(Y + row * C + ch * 8) = *reinterpret_cast<const uint4*>(t);
+  }
+}
+
+int splitk_layernorm(const float* S, int ks, const float* bias, bf16* Y, int M, int C, const float* gamma,
+                     const float* beta, float eps, hipStream_t st) {
+  if (C % 8 || C > 4096) { set_error("splitk_layernorm: C %% 8 != 0 or C > 4096"); return SVK_EUNSUPPORTED; }
+  const int nch = C / 8;
+  auto go = [&](auto lpr_c, auto nch_c) {
+    constexpr int LPR = decltype(lpr_c)::value, NCH = decltype(nch_c)::value;
+    constexpr int RPB = 4 * (64 / LPR);
+    hipLaunchKernelGGL((splitk_ln_kernel<LPR, NCH>), dim3((M + RPB - 1) / RPB), dim3(256), 0, st, S, ks, bias, Y, gamma,
+                       beta, M, C, eps);
+  };
+  using I1 = std::integral_constant<int, 1>;
+  if (nch <= 8) go(std::integral_constant<int, 8>{}, I1{});
+  else if (nch <= 16) go(std::integral_constant<int, 16>{}, I1{});
+  else if (nch <= 32) go(std::integral_constant<int, 32>{}, I1{});
+  else if (nch <= 64) go(std::integral_constant<int, 64>{}, I1{});
+  else if (nch <= 128) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 2>{});
+  else if (nch <= 256) go(std::integral_constant<int, 64>{}, std::integral_constant<int, 4>{});
+  else go(std::integral_constant<int, 64>{}, std::integral_constant<int, 8>{});
+  return check_launch("splitk_ln");
 }
 
 }  // namespace svk

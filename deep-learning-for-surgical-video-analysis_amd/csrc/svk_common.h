@@ -20,6 +20,9 @@ enum { TUNE_PK_CFG = 0, TUNE_PK_ELDS = 1, TUNE_DW_LDS = 2, TUNE_DW_ROWS = 3, TUN
 extern int g_tune[TUNE_NKNOBS];
 // Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
 void set_last_kernel(const char* name);
+// norm.hip: Y = LN(sum of ks f32 split-K slabs [ks][M][C] + bias), bf16 out (svk_conv2d_ln_nhwc)
+int splitk_layernorm(const float* S, int ks, const float* bias, __bf16* Y, int M, int C, const float* gamma,
+                     const float* beta, float eps, hipStream_t st);
 // gemm.hip: batched split-M weight-gradient reduction dW[z] += dY[z]^T X[z] (f32 atomics)
 int wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o,
                   long sx_i, float* dW, long lddw, long sw_o, long sw_i, int Z, int nzi, int M, int N, int K,

@@ -121,9 +121,9 @@ class Attention(nn.Module):
         q = ops.gemm(x, p["wq"], p["bq"])
         if self.sr_ratio > 1:
             r = self.sr_ratio
-            xs = ops.conv2d_nhwc(x.view(B, H, W, C), p["wsr"], r, r, 0, bias=p["bsr"])   # patchify GEMM, K = C*r*r
+            # patchify GEMM (K = C*r*r) + LayerNorm in one call (split-K for the long-K stages)
+            xs = ops.conv2d_ln_nhwc(x.view(B, H, W, C), p["wsr"], r, r, 0, p["bsr"], p["gn"], p["bn"], self.norm.eps)
             xs = xs.view(B, -1, C)
-            ops.layernorm(xs, p["gn"], p["bn"], self.norm.eps, out=xs)
         else:
             xs = x
         kv = ops.gemm(xs, p["wkv"], p["bkv"])                                # [B, Nk, 2C]: k | v

@@ -20,6 +20,8 @@ SIGNATURES = {
     "svk_tune": [c_char_p, c_int],
     "svk_conv2d_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_layernorm": [c_int, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
+    "svk_conv2d_ln_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, c_int, c_int, c_int,
+                           c_int, P, c_long, P],
     "svk_attention": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
                       c_int, c_int, c_int, c_int, c_int, c_float, P],
     "svk_dwconv3x3": [c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
@@ -64,7 +66,8 @@ SIGNATURES = {
     "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],
 }
 STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
-LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int]}
+LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
+              "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]}
 
 _lib = None
 

@@ -194,6 +194,34 @@ def conv2d_nhwc(x, w_packed, k, stride, pad, bias=None, act=None, residual=None)
     return out
 
 
+def conv2d_ln_nhwc(x, w_packed, k, stride, pad, bias, gamma, beta, eps):
+    """LN(conv(x) + bias) over the output channels (Attention.sr + Attention.norm); long-K bf16
+    patchify convs run split-K with an f32 workspace reduced inside the LayerNorm."""
+    _chk(x, "x"); _chk(w_packed, "w", x.dtype)
+    for t, nm in ((bias, "bias"), (gamma, "gamma"), (beta, "beta")):
+        _chk(t, nm, torch.float32)
+    if not x.is_contiguous() or x.dim() != 4:
+        raise _lib.SvkError("svk.conv2d_ln_nhwc: x must be contiguous NHWC [B,H,W,C]")
+    B, H, W, Cin = x.shape
+    Cout = w_packed.shape[0]
+    if w_packed.shape[1] != k * k * Cin or not w_packed.is_contiguous():
+        raise _lib.SvkError("svk.conv2d_ln_nhwc: packed weight shape mismatch")
+    OH, OW = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    out = torch.empty(B, OH, OW, Cout, device=x.device, dtype=x.dtype)
+    lib = _lib.load()
+    nbytes = lib.svk_conv2d_ln_workspace(dtype_code(x.dtype), B, H, W, Cin, Cout, k, stride, pad)
+    ws = torch.empty((nbytes + 15) // 16 * 4, device=x.device, dtype=torch.float32) if nbytes > 0 else None
+    t0 = _prof_begin()
+    _lib.call("svk_conv2d_ln_nhwc", dtype_code(x.dtype), _p(x), B, H, W, Cin, _p(w_packed), _p(bias), _p(gamma),
+              _p(beta), float(eps), _p(out), Cout, k, stride, pad, _p(ws), 0 if ws is None else ws.numel() * 4,
+              _stream())
+    if t0 is not None:
+        M, K = B * OH * OW, k * k * Cin
+        _prof_end(t0, _last_kernel(), 2.0 * M * Cout * K, (x.numel() + Cout * K + M * Cout) * x.element_size(),
+                  (M, Cout, K, f"convln{k}s{stride}"))
+    return out
+
+
 def layernorm(x, gamma, beta, eps, out=None):
     _chk(x, "x"); _chk(gamma, "gamma", torch.float32); _chk(beta, "beta", torch.float32)
     M, C, ldx = _rows(x, "x")

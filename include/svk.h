@@ -60,6 +60,15 @@ int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, cons
                     const float* bias, const void* R, void* Y, int Cout, int k, int stride, int pad,
                     int act, void* stream);
 
+/* Sequence-reduction conv + LayerNorm, Y = LN(conv(X) + bias) (Attention.sr + Attention.norm,
+ * mix_transformer_evp.py:115-117).  bf16 long-K patchify convs split K over svk_conv2d_ln_workspace()
+ * bytes of caller-owned f32 workspace (0 = no split; ws may then be NULL) and reduce the parts inside
+ * the LayerNorm; otherwise conv then in-place LayerNorm.  Y contiguous [B, OH, OW, Cout]. */
+long svk_conv2d_ln_workspace(int dtype, int B, int H, int W, int Cin, int Cout, int k, int stride, int pad);
+int svk_conv2d_ln_nhwc(int dtype, const void* X, int B, int H, int W, int Cin, const void* Wt, const float* bias,
+                       const float* gamma, const float* beta, float eps, void* Y, int Cout, int k, int stride,
+                       int pad, void* ws, long ws_bytes, void* stream);
+
 /* Row LayerNorm: Y = (X - mean) / sqrt(var + eps) * gamma + beta over C channels.
  * Replaces every nn.LayerNorm on the path (mix_transformer_evp.py:90, 139-146, 190,
  * 245-269, 876). */

@@ -393,3 +393,25 @@ def test_cast(cuda):
     torch.cuda.synchronize()
     assert torch.equal(y.cpu(), x.cpu().to(torch.bfloat16))
     assert torch.equal(z.cpu(), y.cpu().float())
+
+
+@pytest.mark.parametrize("dt", DTS)
+@pytest.mark.parametrize("B,H,Cin,r", [(256, 56, 64, 8), (256, 28, 128, 4), (256, 14, 320, 2), (3, 56, 64, 8),
+                                       (5, 28, 128, 4)])
+def test_conv2d_ln_sequence_reduction(cuda, dt, B, H, Cin, r):
+    """Attention.sr + Attention.norm as one call (split-K slabs reduced inside the LayerNorm for the
+    long-K bf16 patchify convs at B = 256) against fp64 conv + LayerNorm."""
+    from svk import ops
+    from svk.pack import conv_w
+    x = _rand(B, H, H, Cin, dt=dt, dev=cuda, seed=71)
+    w = _rand(Cin, Cin, r, r, dt=torch.float32, dev="cpu", scale=(Cin * r * r) ** -0.5, seed=72).to(dt)
+    b = _rand(Cin, dt=torch.float32, dev=cuda, seed=73)
+    g = _rand(Cin, dt=torch.float32, dev=cuda, seed=74)
+    be = _rand(Cin, dt=torch.float32, dev=cuda, seed=75)
+    got = ops.conv2d_ln_nhwc(x, conv_w(w, dt).to(cuda), r, r, 0, b, g, be, 1e-5)
+    torch.cuda.synchronize()
+    nb = min(B, 4)                                   # fp64 reference on a few frames (frames are independent)
+    ref = F.conv2d(x[:nb].cpu().double().permute(0, 3, 1, 2), w.double(), b.cpu().double(), stride=r)
+    ref = F.layer_norm(ref.permute(0, 2, 3, 1), (Cin,), g.cpu().double(), be.cpu().double(), 1e-5)
+    _close(got[:nb], ref, dt)
+    assert bool(torch.isfinite(got).all())
