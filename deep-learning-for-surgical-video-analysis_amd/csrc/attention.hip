@@ -8,6 +8,7 @@
 // (running max / sum), then the 4 partial states are merged with wave shuffles.
 // Q is read once, O written once: the kernel is bound by the Q/O HBM traffic.
 #include "svk_common.h"
+#include <type_traits>
 
 namespace svk {
 
@@ -236,6 +237,165 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restric
   }
 }
 
+// Resident-K/V variant for Nk <= 64 * NKC (every attention of the path: 49 reduced keys, 196 / 49 flow
+// tokens): the whole K (row-major) and V (transposed) of one (batch, head) are staged in LDS ONCE per
+// workgroup of QB = 256 queries — 4x fewer stagings per query than one 64-query block — and each
+// wave then walks its 16-query tiles (tile t = wave, wave + 4, ...), the softmax over all keys
+// computed chunk by chunk exactly as in attention_mfma_bf16.  The output tile goes through a
+// per-wave LDS patch and leaves as 16-byte row pieces (one head row = hd * 2 bytes) instead of
+// 2-byte scattered stores.
+template <int HDP, int NKC>
+__global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __restrict__ Q, long ldq, long sbq,
+                                                               const bf16* __restrict__ K, long ldk, long sbk,
+                                                               const bf16* __restrict__ V, long ldv, long sbv,
+                                                               bf16* __restrict__ O, long ldo, long sbo, int Nq,
+                                                               int Nk, int hd, float scale_log2) {
+  constexpr int KC = 64, NKP = NKC * KC;
+  constexpr int KLD = HDP + 8;    // sK row stride (elements)
+  constexpr int VLD = NKP + 8;    // sVt row stride (elements)
+  constexpr int OLD = HDP + 8;    // per-wave output patch row stride
+  constexpr int NKS = HDP / 32, NDT = HDP / 16;
+  constexpr int QB = 256;
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) bf16 sK[NKP][KLD];
+  __shared__ __attribute__((aligned(16))) bf16 sVt[HDP][VLD];
+  __shared__ __attribute__((aligned(16))) bf16 sO[4][16][OLD];
+
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const bf16* Qb = Q + (long)b * sbq + (long)h * hd;
+  const bf16* Kb = K + (long)b * sbk + (long)h * hd;
+  const bf16* Vb = V + (long)b * sbv + (long)h * hd;
+  bf16* Ob = O + (long)b * sbo + (long)h * hd;
+  const bf16 zero = (bf16)0.f;
+
+  // stage K [key][d] and V^T [d][key] for all keys (zeros past Nk / hd)
+  for (int e = tid; e < NKP * (HDP / 8); e += 256) {
+    const int key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
+    bf16x8 kv, vv;
+    if (key < Nk && d0 < hd) {
+      kv = *reinterpret_cast<const bf16x8*>(Kb + (long)key * ldk + d0);
+      vv = *reinterpret_cast<const bf16x8*>(Vb + (long)key * ldv + d0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { kv[j] = zero; vv[j] = zero; }
+    }
+    *reinterpret_cast<bf16x8*>(&sK[key][d0]) = kv;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[j];
+  }
+  __syncthreads();
+
+  const int qbase = blockIdx.x * QB;
+  for (int qt = wave; qt < QB / 16; qt += 4) {
+    const int q0 = qbase + qt * 16;
+    if (q0 >= Nq) break;
+    bf16x8 qf[NKS];
+    {
+      const int qr = q0 + c;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int d0 = 32 * ks + 8 * g;
+        if (qr < Nq && d0 < hd) {
+          qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * ldq + d0);
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) qf[ks][j] = zero;
+        }
+      }
+    }
+    f32x4 o[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < NKC; ++ch) {
+      const int kc0 = ch * KC;
+      f32x4 s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sK[kc0 + 16 * t + c][32 * ks + 8 * g]);
+          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], s[t], 0, 0, 0);
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kc0 + 16 * t + 4 * g + r;
+          const float v = key < Nk ? s[t][r] * scale_log2 : -INFINITY;
+          s[t][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f(m_run - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[t][r] - m_new);
+          s[t][r] = p;
+          ps += p;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l_run = l_run * alpha + ps;
+      m_run = m_new;
+      if (ch > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) o[dt][r] *= ar;
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        bf16x8 pa;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[j] = (bf16)s[2 * s2][j];
+          pa[4 + j] = (bf16)s[2 * s2 + 1][j];
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 4 * g]);
+          const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 16 + 4 * g]);
+          bf16x8 vb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { vb[j] = v0[j]; vb[4 + j] = v1[j]; }
+          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+        }
+      }
+    }
+    // normalise; stage the 16 x hd tile in this wave's LDS patch; 16-byte row pieces out
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float inv = 1.0f / __shfl(l_run, 4 * g + r, 64);
+#pragma unroll
+      for (int dt = 0; dt < NDT; ++dt) sO[wave][4 * g + r][16 * dt + c] = (bf16)(o[dt][r] * inv);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int cpr = hd >> 3;   // 16-byte pieces per row (hd % 8 == 0)
+    for (int e = lane; e < 16 * cpr; e += 64) {
+      const int row = e / cpr, cc = e - row * cpr;
+      const int q = q0 + row;
+      if (q < Nq) *reinterpret_cast<uint4*>(Ob + (long)q * ldo + cc * 8) = *reinterpret_cast<const uint4*>(&sO[wave][row][cc * 8]);
+    }
+    __builtin_amdgcn_wave_barrier();   // the patch is rewritten by this wave's next tile
+  }
+}
+
 }  // namespace svk
 
 using namespace svk;
@@ -253,6 +413,28 @@ extern "C" int svk_attention(int dtype, const void* Q, long ldq, long sbq, const
   dim3 grid((Nq + 63) / 64, heads, B), block(256);
   if (dtype == SVK_BF16) {
     const float sl2 = scale * 1.4426950408889634f;   // softmax via exp2
+    const bool res_ok = hd % 8 == 0 && ((ldq | ldk | ldv | ldo | sbq | sbk | sbv | sbo) % 8) == 0 &&
+                        ((((uintptr_t)Q) | ((uintptr_t)K) | ((uintptr_t)V) | ((uintptr_t)O)) & 15) == 0;
+    if (res_ok) {
+      const int nkc = (Nk + 63) / 64;
+      dim3 rgrid((Nq + 255) / 256, heads, B);
+      auto go = [&](auto hdp_c, auto nkc_c) {
+        constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
+        hipLaunchKernelGGL((attention_mfma_bf16_res<HDP, NKC>), rgrid, block, 0, st, (const bf16*)Q, ldq, sbq,
+                           (const bf16*)K, ldk, sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);
+      };
+      auto by_nkc = [&](auto hdp) {
+        switch (nkc) {
+          case 1: go(hdp, std::integral_constant<int, 1>{}); break;
+          case 2: go(hdp, std::integral_constant<int, 2>{}); break;
+          case 3: go(hdp, std::integral_constant<int, 3>{}); break;
+          default: go(hdp, std::integral_constant<int, 4>{}); break;
+        }
+      };
+      if (hd <= 32) by_nkc(std::integral_constant<int, 32>{});
+      else by_nkc(std::integral_constant<int, 64>{});
+      return check_launch("attention_mfma_bf16_res");
+    }
     if (hd <= 32)
       hipLaunchKernelGGL((attention_mfma_bf16<32>), grid, block, 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K, ldk,
                          sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);

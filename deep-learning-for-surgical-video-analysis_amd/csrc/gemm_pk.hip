@@ -384,9 +384,9 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
                      (int)ntiles, nk, ks);
   static char name[96];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s%s>", Cfg::BM, Cfg::BN,
+    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", Cfg::BM, Cfg::BN,
              Cfg::WGM, Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC,
-             EXT ? "true" : "false", SPLIT ? ", true" : "");
+             EXT ? "true" : "false", SPLIT ? "true" : "false");   // the demangled instantiation name
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
