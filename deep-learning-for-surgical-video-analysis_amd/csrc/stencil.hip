@@ -1,6 +1,7 @@
 // Memory-bound stencil / layout kernels over NHWC maps: depthwise 3x3 (+bias+GELU),
 // input packing NCHW->NHWC, Gaussian 5x5 reflect filter, bilinear resize, window unfold, cast.
 #include "svk_common.h"
+#include <type_traits>
 
 namespace svk {
 
@@ -132,6 +133,216 @@ __global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, 
       o[2 * j + 1] = from_f<T>(g.y);
     }
     store_vec8(Y + off, o);
+  }
+}
+
+// Rolling-window variant (bf16, C % 4 == 0): one thread per (4-channel group, column x, strip of R
+// rows).  Only three input rows (3 columns x 4 channels, 8-byte loads) are live at a time — the next
+// row is loaded while the current output row is computed — and the taps are 9 x 4 floats, so the
+// kernel needs ~80 VGPRs (6 waves / SIMD) where the all-rows-up-front strip kernel needs ~240 (2 per
+// SIMD): the loads' latency is hidden by occupancy instead of by one thread's register window.
+template <int R>
+__global__ __launch_bounds__(256) void dwconv3x3_roll_bf16(const bf16* __restrict__ X, const float* __restrict__ w,
+                                                           const float* __restrict__ bias, bf16* __restrict__ Y,
+                                                           bf16* __restrict__ Ypre, int B, int H, int W, int C,
+                                                           int act, int nstrip) {
+  const int CG = C >> 2;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * nstrip * W * CG;
+  if (idx >= total) return;
+  const int cg = (int)(idx % CG);
+  long t = idx / CG;
+  const int x = (int)(t % W);
+  t /= W;
+  const int s = (int)(t % nstrip);
+  const int b = (int)(t / nstrip);
+  const int c0 = cg * 4, y0 = s * R;
+  const bf16* base = X + (long)b * H * W * C + c0;
+  const int xl = x > 0 ? x - 1 : 0, xr = x < W - 1 ? x + 1 : W - 1;
+  f32x2 wt[9][2], bs[2];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) wt[k][j] = *reinterpret_cast<const f32x2*>(w + k * C + c0 + 2 * j);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) bs[j] = *reinterpret_cast<const f32x2*>(bias + c0 + 2 * j);
+
+  auto load_row = [&](int yy, uint2* v) {
+    const bool oky = yy >= 0 && yy < H;
+    const bf16* row = base + (long)min(max(yy, 0), H - 1) * W * C;
+    const uint2 a = *reinterpret_cast<const uint2*>(row + (long)xl * C);
+    const uint2 m = *reinterpret_cast<const uint2*>(row + (long)x * C);
+    const uint2 c = *reinterpret_cast<const uint2*>(row + (long)xr * C);
+    const bool okl = oky && x > 0, okr = oky && x < W - 1;
+    v[0] = okl ? a : uint2{0u, 0u};
+    v[1] = oky ? m : uint2{0u, 0u};
+    v[2] = okr ? c : uint2{0u, 0u};
+  };
+  auto lo = [](uint32_t u) { return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)}; };
+  uint2 win[3][3];
+  load_row(y0 - 1, win[0]);
+  load_row(y0, win[1]);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int y = y0 + r;
+    if (y >= H) break;
+    load_row(y + 1, win[(r + 2) % 3]);
+    f32x2 acc[2] = {bs[0], bs[1]};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const uint2* v = win[(r + dy) % 3];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        acc[0] = lo(v[dx].x) * wt[dy * 3 + dx][0] + acc[0];
+        acc[1] = lo(v[dx].y) * wt[dy * 3 + dx][1] + acc[1];
+      }
+    }
+    const long off = (((long)b * H + y) * W + x) * C + c0;
+    if (Ypre) {
+      bf16 o[4] = {(bf16)acc[0].x, (bf16)acc[0].y, (bf16)acc[1].x, (bf16)acc[1].y};
+      *reinterpret_cast<uint2*>(Ypre + off) = *reinterpret_cast<const uint2*>(o);
+    }
+    f32x2 g0, g1;
+    if (act == SVK_ACT_GELU) {
+      g0 = gelu_fast2(acc[0]);
+      g1 = gelu_fast2(acc[1]);
+    } else {
+      g0 = f32x2{apply_act(acc[0].x, act), apply_act(acc[0].y, act)};
+      g1 = f32x2{apply_act(acc[1].x, act), apply_act(acc[1].y, act)};
+    }
+    bf16 o[4] = {(bf16)g0.x, (bf16)g0.y, (bf16)g1.x, (bf16)g1.y};
+    *reinterpret_cast<uint2*>(Y + off) = *reinterpret_cast<const uint2*>(o);
+  }
+}
+
+// ---- MixFFN front half in one kernel: G = act(dwconv3x3(XN W1^T + b1) + db) ------------------------
+// (Mlp.fc1 -> DWConv -> GELU, mix_transformer_evp.py:60-63 / 24-30).  One workgroup per (frame, strip
+// of R image rows, 64 hidden channels): it computes the fc1 outputs of the strip plus one halo row
+// above and below ((R + 2) x W tokens, MFMA 16x16x32 with the W1 chunk in LDS and the XN rows read as
+// A fragments straight from global memory), rounds them to bf16 exactly like the unfused fc1 GEMM
+// output and keeps them in an LDS halo tile (zero columns / out-of-image rows = the conv's zero
+// padding), then runs the depthwise conv + GELU from LDS and writes G.  The hidden map H — the
+// largest tensor of the path — never goes to HBM: the unfused path writes it once and reads it
+// (through the vector caches) about 1.4 times.  The halo rows cost (R + 2) / R of the fc1 MFMA work.
+template <int KS>   // K = 32 * KS (fc1 input channels)
+__global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ XN, const bf16* __restrict__ W1,
+                                                       const float* __restrict__ b1, const float* __restrict__ taps,
+                                                       const float* __restrict__ db, bf16* __restrict__ G, int H, int W,
+                                                       int K, int HID, int R, int nstrip, int act) {
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  char* smem = reinterpret_cast<char*>(smem4);
+  const int WLD = K + 8;                                   // W1 chunk row stride (elements)
+  bf16* sW = reinterpret_cast<bf16*>(smem);                // [64][WLD]
+  const int TW = W + 2;
+  char* sH = smem + 64 * WLD * 2;                          // [(R + 2)][TW][64] bf16
+  const int nnb = HID >> 6;
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int id = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int nb = id % nnb, s = (id / nnb) % nstrip, b = id / (nnb * nstrip);
+  const int y0 = s * R;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // W1 rows nb*64 .. +63 -> LDS; zero halo columns of the hidden tile
+  for (int e = tid; e < 64 * (K >> 3); e += 256) {
+    const int n = e / (K >> 3), k8 = (e - n * (K >> 3)) * 8;
+    *reinterpret_cast<uint4*>(sW + n * WLD + k8) = *reinterpret_cast<const uint4*>(W1 + (long)(nb * 64 + n) * K + k8);
+  }
+  for (int e = tid; e < (R + 2) * 2 * 8; e += 256) {
+    const int hr = e >> 4, side = (e >> 3) & 1, c = e & 7;
+    reinterpret_cast<uint4*>(sH + ((hr * TW + (side ? TW - 1 : 0)) * 64) * 2)[c] = uint4{0u, 0u, 0u, 0u};
+  }
+  __syncthreads();
+
+  // fc1 over the (R + 2) x W halo tokens: lane -> token fr of the 16-token tile, 4 channels 4fq + r of
+  // each 16-channel block (W1 fragment as the A operand: the tile comes out transposed)
+  const int ntok = (R + 2) * W, mt_n = (ntok + 15) >> 4;
+  const bf16* Xb = XN + (long)b * H * W * K;
+  float bias4[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias4[j][r] = b1[nb * 64 + j * 16 + 4 * fq + r];
+  // A fragments of this wave's m-tiles, software-pipelined: the next tile's K row is in flight
+  // while the current tile's MFMAs run (rows clamped into the image; invalid tokens stored as zeros)
+  auto load_a = [&](int mt, bf16x8* a) {
+    const int t = mt * 16 + fr;
+    const int hr = t / W, x = t - hr * W;
+    const int y = min(max(y0 - 1 + hr, 0), H - 1);
+    const bf16* xr = Xb + ((long)y * W + min(x, W - 1)) * K + fq * 8;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(xr + ks * 32);
+  };
+  bf16x8 anext[KS];
+  if (wave < mt_n) load_a(wave, anext);
+  for (int mt = wave; mt < mt_n; mt += 4) {
+    const int t = mt * 16 + fr;
+    const int hr = t / W, x = t - hr * W;
+    const int y = y0 - 1 + hr;
+    const bool valid = t < ntok && (unsigned)y < (unsigned)H;
+    bf16x8 a[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) a[ks] = anext[ks];
+    if (mt + 4 < mt_n) load_a(mt + 4, anext);
+    f32x4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bf16x8 w = *reinterpret_cast<const bf16x8*>(sW + (j * 16 + fr) * WLD + ks * 32 + fq * 8);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a[ks], acc[j], 0, 0, 0);
+      }
+    if (t < ntok) {
+      char* dst = sH + ((hr * TW + x + 1) * 64) * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bf16 o[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = valid ? (bf16)(acc[j][r] + bias4[j][r]) : (bf16)0.f;
+        *reinterpret_cast<uint2*>(dst + (j * 16 + 4 * fq) * 2) = *reinterpret_cast<const uint2*>(o);
+      }
+    }
+  }
+
+  // depthwise 3x3 + bias + act from the LDS tile (same arithmetic order as dwconv3x3_strip)
+  const int c = tid & 7, pl = tid >> 3;
+  const int c0 = nb * 64 + c * 8;
+  f32x2 wt[9][4], bs[4];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wt[k][j] = *reinterpret_cast<const f32x2*>(taps + k * HID + c0 + 2 * j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f32x2*>(db + c0 + 2 * j);
+  __syncthreads();
+  const uint4* tile = reinterpret_cast<const uint4*>(sH);
+  const int rows = min(R, H - y0);
+  bf16* Gb = G + (long)b * H * W * HID + c0;
+  for (int q = pl; q < rows * W; q += 32) {
+    const int r = q / W, x = q - r * W;
+    f32x2 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bs[j];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        Vec8<bf16> v;
+        *reinterpret_cast<uint4*>(v.u) = tile[((r + dy) * TW + x + dx) * 8 + c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = pair(v, j) * wt[dy * 3 + dx][j] + acc[j];
+      }
+    bf16 o[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f32x2 g = act == SVK_ACT_GELU ? gelu_fast2(acc[j]) : f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
+      o[2 * j] = (bf16)g.x;
+      o[2 * j + 1] = (bf16)g.y;
+    }
+    store_vec8(Gb + ((long)(y0 + r) * W + x) * HID, o);
   }
 }
 
@@ -427,7 +638,15 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
   SVK_DISPATCH_DTYPE(dtype, T, {
     const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 15) == 0;
     const int lds_env = g_tune[TUNE_DW_LDS], rows_env = g_tune[TUNE_DW_ROWS];   // svk_tune knobs
-    if (sizeof(T) == 2 && vec && C % 64 == 0 && lds_env > 0) {
+    if (sizeof(T) == 2 && lds_env == 2 && C % 4 == 0 && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 7) == 0) {
+      constexpr int RR = 8;
+      const int nstrip = (H + RR - 1) / RR;
+      const long n = (long)B * nstrip * W * (C / 4);
+      hipLaunchKernelGGL((dwconv3x3_roll_bf16<RR>), grid1d(n), dim3(256), 0, st, (const bf16*)X, w, bias, (bf16*)Y,
+                         (bf16*)Ypre, B, H, W, C, act, nstrip);
+      return check_launch("dwconv3x3_roll");
+    }
+    if (sizeof(T) == 2 && vec && C % 64 == 0 && lds_env == 1) {
       // strip height: the tallest strip whose halo tile fits 48 KiB (3 workgroups per CU)
       int R = rows_env > 0 ? rows_env : 49152 / ((W + 2) * 128) - 2;
       R = std::max(1, std::min(R, H));
@@ -455,6 +674,40 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
     }
     return check_launch("dwconv3x3");
   });
+}
+
+// fc1 + depthwise conv + activation (MixFFN front half) in one pass; see fc1_dwconv_bf16.
+extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
+                                     const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act,
+                                     void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || C <= 0 || hidden <= 0 || !XN || !W1 || !b1 || !taps || !dbias || !G) {
+    set_error("svk_mixffn_fc1_dwconv: bad args"); return SVK_EINVAL;
+  }
+  if (dtype != SVK_BF16 || (C != 32 && C != 64 && C != 128) || hidden % 64 ||
+      ((((uintptr_t)XN) | ((uintptr_t)W1) | ((uintptr_t)G)) & 15)) {
+    set_error("svk_mixffn_fc1_dwconv: needs bf16, C in {32, 64, 128}, hidden %% 64 == 0, 16-byte aligned maps");
+    return SVK_EUNSUPPORTED;
+  }
+  if (B == 0) return SVK_OK;
+  // strip height: halo tile <= 44 KiB, strips of equal height
+  const int rmax = std::max(1, std::min(H, 45056 / ((W + 2) * 128) - 2));
+  const int nst0 = (H + rmax - 1) / rmax;
+  const int R = (H + nst0 - 1) / nst0, nstrip = (H + R - 1) / R;
+  const size_t lds = (size_t)64 * (C + 8) * 2 + (size_t)(R + 2) * (W + 2) * 128;
+  if (lds > 160 * 1024) { set_error("svk_mixffn_fc1_dwconv: tile too large"); return SVK_EUNSUPPORTED; }
+  hipStream_t st = (hipStream_t)stream;
+  const long nwg = (long)B * nstrip * (hidden / 64);
+  auto go = [&](auto ks_c) {
+    constexpr int KS = decltype(ks_c)::value;
+    if (lds > 65536)
+      (void)hipFuncSetAttribute((const void*)fc1_dwconv_bf16<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((fc1_dwconv_bf16<KS>), dim3((unsigned)nwg), dim3(256), lds, st, (const bf16*)XN, (const bf16*)W1,
+                       b1, taps, dbias, (bf16*)G, H, W, C, hidden, R, nstrip, act);
+  };
+  if (C == 32) go(std::integral_constant<int, 1>{});
+  else if (C == 64) go(std::integral_constant<int, 2>{});
+  else go(std::integral_constant<int, 4>{});
+  return check_launch("fc1_dwconv");
 }
 
 extern "C" int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B, int H,

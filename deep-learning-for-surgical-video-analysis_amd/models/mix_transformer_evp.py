@@ -79,6 +79,14 @@ class Mlp(nn.Module):
             y = ops.mixffn_fused(x.contiguous().view(B, H, W, C), residual.contiguous().view(B, H, W, C),
                                  p["w1"], p["b1"], pd["taps"], pd["b"], p["w2"], p["b2"])
             return y.view(B, N, C)
+        hid = self.fc1.out_features
+        # measured: wins where the hidden map is largest (stages 1-2, C <= 128); at C = 320 / 512 the
+        # recomputed halo fc1 work outweighs the saved traffic
+        if ops.FC1_DWCONV and x.dtype == torch.bfloat16 and C in (32, 64, 128) and hid % 64 == 0:
+            # fc1 -> DWConv -> GELU in one kernel, the hidden map kept on chip (Mlp.forward :60-63)
+            pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
+            g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")
+            return ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
         h = ops.gemm(x, p["w1"], p["b1"])
         h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)
         return ops.gemm(h, p["w2"], p["b2"], residual=residual)

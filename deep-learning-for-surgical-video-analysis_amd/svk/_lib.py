@@ -25,6 +25,7 @@ SIGNATURES = {
     "svk_attention": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
                       c_int, c_int, c_int, c_int, c_int, c_float, P],
     "svk_dwconv3x3": [c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_mixffn_fc1_dwconv": [c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_nchw_to_nhwc": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_gauss5x5_reflect": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_resize_bilinear": [c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P],

@@ -275,6 +275,32 @@ def mixffn_fused(xn, x, w1, b1, taps, dbias, w2, b2):
     return out
 
 
+FC1_DWCONV = os.environ.get("SVK_FC1_DWCONV", "1") == "1"
+
+
+def mixffn_fc1_dwconv(xn, w1, b1, taps, dbias, act="gelu"):
+    """act(dwconv3x3(xn @ w1.T + b1) + dbias) on an NHWC [B, H, W, C] bf16 map -> [B, H, W, hidden];
+    the hidden map never leaves the chip (svk_mixffn_fc1_dwconv)."""
+    _chk(xn, "xn", torch.bfloat16); _chk(w1, "w1", torch.bfloat16)
+    for t, nm in ((b1, "b1"), (taps, "taps"), (dbias, "dbias")):
+        _chk(t, nm, torch.float32)
+    if not xn.is_contiguous() or xn.dim() != 4 or not w1.is_contiguous():
+        raise _lib.SvkError("svk.mixffn_fc1_dwconv: xn must be contiguous NHWC, w1 contiguous")
+    B, H, W, C = xn.shape
+    hid = w1.shape[0]
+    if w1.shape[1] != C or taps.shape != (9, hid) or b1.numel() != hid or dbias.numel() != hid:
+        raise _lib.SvkError("svk.mixffn_fc1_dwconv: shape mismatch")
+    out = torch.empty(B, H, W, hid, device=xn.device, dtype=xn.dtype)
+    t0 = _prof_begin()
+    _lib.call("svk_mixffn_fc1_dwconv", BF16, _p(xn), _p(w1), _p(b1), _p(taps), _p(dbias), _p(out), B, H, W, C, hid,
+              ACT[act], _stream())
+    if t0 is not None:
+        M = B * H * W
+        _prof_end(t0, "fc1_dwconv_bf16", 2.0 * M * C * hid, (xn.numel() + out.numel() + w1.numel()) * 2,
+                  (M, hid, C, "fc1dw"))
+    return out
+
+
 def dwconv3x3(x, taps, bias, act=None, pre_out=None):
     """x [B, H, W, C] NHWC contiguous; taps [9, C] f32; bias [C] f32.  ``pre_out`` (same shape)
     additionally receives the pre-activation map."""

@@ -96,6 +96,13 @@ int svk_mixffn_fused(int dtype, const void* XN, const void* X, const void* W1, c
                      const float* taps, const float* dbias, const void* W2, const float* b2, void* Y,
                      int B, int H, int W, int C, void* stream);
 
+/* MixFFN front half, G = act(dwconv3x3(XN W1^T + b1) + dbias) over NHWC maps (Mlp.fc1 -> DWConv -> GELU,
+ * mix_transformer_evp.py:60-63, 24-30): the 4C-wide hidden map stays on chip (fc1 recomputed on one
+ * halo row above / below each strip).  bf16, C in {32, 64, 128}, hidden % 64 == 0; W1 [hidden][C] bf16,
+ * b1 [hidden], taps [9][hidden], dbias [hidden] f32; G [B, H, W, hidden]. */
+int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
+                          const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act, void* stream);
+
 /* NCHW f32 -> NHWC dtype with the channel dim zero-padded to Cpad >= C (input packing of frames /
  * flow, view(-1,3,224,224) at :354; padding to 8 lets the first convs take the vector path). */
 int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,

@@ -134,16 +134,16 @@ def test_persistent_tile_configs(cuda, cfg):
         ops.tune("pk_cfg", -1)
 
 
-@pytest.mark.parametrize("rows", [1, 3, 8])
-def test_dwconv_lds_variant(cuda, rows):
+@pytest.mark.parametrize("lds,rows", [(1, 1), (1, 3), (1, 8), (2, -1)])
+def test_dwconv_lds_variant(cuda, lds, rows):
     """The LDS-tiled depthwise conv (svk_tune dw_lds = 1) at several strip heights, with the
     pre-activation store, against fp64."""
     from svk import ops
     dt = torch.bfloat16
     try:
-        ops.tune("dw_lds", 1)
+        ops.tune("dw_lds", lds)
         ops.tune("dw_rows", rows)
-        for B, H, W, C in ((2, 28, 28, 256), (3, 7, 7, 128), (1, 10, 13, 64)):
+        for B, H, W, C in ((2, 28, 28, 256), (3, 7, 7, 128), (1, 10, 13, 64), (2, 19, 5, 68)):
             x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=61)
             w = _rand(C, 1, 3, 3, dt=torch.float32, dev="cpu", scale=0.4, seed=62)
             b = _rand(C, dt=torch.float32, dev=cuda, seed=63)
@@ -415,3 +415,27 @@ def test_conv2d_ln_sequence_reduction(cuda, dt, B, H, Cin, r):
     ref = F.layer_norm(ref.permute(0, 2, 3, 1), (Cin,), g.cpu().double(), be.cpu().double(), 1e-5)
     _close(got[:nb], ref, dt)
     assert bool(torch.isfinite(got).all())
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (3, 28, 28, 128), (2, 14, 14, 128), (4, 7, 7, 64),
+                                     (1, 9, 13, 32), (2, 30, 17, 64)])
+def test_mixffn_fc1_dwconv(cuda, B, H, W, C):
+    """fc1 -> dwconv3x3 -> GELU in one kernel (hidden kept on chip) against the unfused svk kernels
+    (fc1 GEMM, bf16 hidden, depthwise conv) and fp64 torch on the same bf16-rounded hidden."""
+    from svk import ops
+    dt = torch.bfloat16
+    hid = 4 * C
+    xn = _rand(B, H, W, C, dt=dt, dev=cuda, seed=81)
+    w1 = _rand(hid, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=82)
+    b1 = _rand(hid, dt=torch.float32, dev=cuda, scale=0.1, seed=83)
+    taps = _rand(9, hid, dt=torch.float32, dev=cuda, scale=0.3, seed=84)
+    db = _rand(hid, dt=torch.float32, dev=cuda, scale=0.1, seed=85)
+    got = ops.mixffn_fc1_dwconv(xn, w1, b1, taps, db, act="gelu")
+    h = ops.gemm(xn.view(B, H * W, C), w1, b1).view(B, H, W, hid)
+    unfused = ops.dwconv3x3(h, taps, db, act="gelu")
+    torch.cuda.synchronize()
+    _close(got, unfused.double().cpu(), dt)
+    hr = (xn.cpu().double() @ w1.cpu().double().t() + b1.cpu().double()).to(dt).double()
+    k = taps.cpu().double().t().reshape(hid, 1, 3, 3)
+    ref = F.gelu(F.conv2d(hr.permute(0, 3, 1, 2), k, db.cpu().double(), padding=1, groups=hid)).permute(0, 2, 3, 1)
+    _close(got, ref, dt)

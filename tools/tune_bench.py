@@ -92,7 +92,7 @@ def main():
                     ops.tune("dw_lds", lds)
                     ops.tune("dw_rows", rows)
                 return f
-            variants = [("strip", knob(0, -1))] + [(f"lds{r}", knob(1, r)) for r in (2, 4, 7, 8, 14) if r <= H]
+            variants = [("strip", knob(0, -1)), ("roll", knob(2, -1))] + [(f"lds{r}", knob(1, r)) for r in (7, 14) if r <= H]
             ab(f"dwconv H={H} C={C}", variants, lambda: ops.dwconv3x3(x, taps, bias, act="gelu"), args.rounds,
                args.reps, nbytes=2 * x.numel() * 2)
             del x
