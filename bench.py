@@ -57,10 +57,19 @@ def pmc_traffic(workload, kernel):
     path = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
     try:
         with open(path) as f:
-            ent = json.load(f)[workload]["kernels"][kernel]
+            table = json.load(f)[workload]["kernels"]
     except (OSError, ValueError, KeyError):
         return None, None
-    return ent["hbm_bytes_per_launch"], os.path.relpath(path, REPO)
+    src = os.path.relpath(path, REPO)
+    if kernel in table:
+        return table[kernel]["hbm_bytes_per_launch"], src
+    # a name without template arguments (e.g. "wgrad_kernel") covers all of its instantiations:
+    # dispatch-weighted mean over them
+    ents = [v for k, v in table.items() if k.startswith(kernel + "<")]
+    n = sum(v["dispatches"] for v in ents)
+    if not n:
+        return None, None
+    return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in ents) / n), src + " (all instantiations)"
 
 
 def video_lengths(n=40, seed=0):

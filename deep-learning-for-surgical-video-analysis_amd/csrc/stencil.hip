@@ -689,8 +689,10 @@ extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, 
     return SVK_EUNSUPPORTED;
   }
   if (B == 0) return SVK_OK;
-  // strip height: halo tile <= 44 KiB, strips of equal height
-  const int rmax = std::max(1, std::min(H, 45056 / ((W + 2) * 128) - 2));
+  // strip height: halo tile <= 44 KiB (measured best at B = 256 against 48 KiB for W1 + tile), strips
+  // of equal height; the svk_tune "dw_rows" knob overrides it
+  int rmax = std::max(1, std::min(H, 45056 / ((W + 2) * 128) - 2));
+  if (g_tune[TUNE_DW_ROWS] > 0) rmax = std::min(H, g_tune[TUNE_DW_ROWS]);
   const int nst0 = (H + rmax - 1) / rmax;
   const int R = (H + nst0 - 1) / nst0, nstrip = (H + R - 1) / R;
   const size_t lds = (size_t)64 * (C + 8) * 2 + (size_t)(R + 2) * (W + 2) * 128;

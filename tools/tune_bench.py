@@ -98,6 +98,19 @@ def main():
             del x
         ops.tune("dw_lds", -1)
         ops.tune("dw_rows", -1)
+    if args.what in ("fc1dw", "all"):
+        for H, C in ((56, 64), (28, 128)):
+            hid = 4 * C
+            xn = torch.randn(256, H, H, C, device=dev).to(dt)
+            w1 = (torch.randn(hid, C, device=dev) * C ** -0.5).to(dt)
+            b1 = torch.randn(hid, device=dev)
+            taps = torch.randn(9, hid, device=dev)
+            db = torch.randn(hid, device=dev)
+            variants = [(f"R{r}", (lambda r=r: ops.tune("dw_rows", r))) for r in (-1, 2, 3, 4, 6, 7, 8, 14) if r <= H]
+            ab(f"fc1dw H={H} C={C}", variants, lambda: ops.mixffn_fc1_dwconv(xn, w1, b1, taps, db), args.rounds,
+               args.reps, nbytes=(xn.numel() + 256 * H * H * hid) * 2)
+            del xn
+        ops.tune("dw_rows", -1)
 
 
 if __name__ == "__main__":
