@@ -4,7 +4,8 @@ Default workload (the headline, BASELINE.json metric): SegFormer/MiT-b2-EVP LFB 
 extraction (generate_evp_LFB.py's hot loop) — frames/s at 224x224 with optical-flow fusion,
 return_features=True ([B, 2048]).  One step = one forward of a B-frame batch (default B = 256)
 whose frames, segmaps and flow are already resident in HBM.  Other workloads (``--workload``):
-``mstcn`` (config 3: MultiStageModel_S(4,10,64,256) over 40 full-length videos), ``e2e``
+``mstcn`` (config 3: MultiStageModel_S(4,10,64,256) over 40 full-length videos), ``mamba``
+(config 3 as tecno.py instantiates it at HEAD: CausalMambaModel, the selective-scan path), ``e2e``
 (config 5: SegFormer -> MS-TCN(2,8,32,2048) -> Transformer(len 30) on 256-frame chunks) and
 ``train`` (configs 2/4: the train_evp.py stage-1 step, B = 88 per GPU, DDP over RCCL when N > 1).
 
@@ -109,6 +110,21 @@ def cpu_baseline_mstcn(budget_s, T=2456):
             "sample": f"{n} videos x {T} frames (MultiStageModel_S(4,10,64,256,14,causal), fp32) in {dt:.1f} s"}
 
 
+def cpu_baseline_mamba(budget_s, T=2456):
+    from oracle import mamba as OM, inputs as I
+    sd = OM.init_state_dict(OM.mamba_shapes(256, 64, 10, 14), 1)
+    x = I.lfb(T, 256, 7).transpose(2, 1)
+    with torch.no_grad():
+        n, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < budget_s or n == 0:
+            OM.causal_mamba(x, sd, 10, dtype=torch.float32)
+            n += 1
+        dt = time.perf_counter() - t0
+    return {"value": round(n * T / dt, 1), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} videos x {T} frames (CausalMambaModel(4,10,64,256,14), 10 Mamba blocks d_state 64, "
+                      f"fp32 restatement of mamba_ssm's reference scan) in {dt:.1f} s"}
+
+
 # ---------------------------------------------------------------------------------------------
 def workload_extract(args, dev, rank, dtype):
     from models import mix_transformer_evp as mte
@@ -155,6 +171,28 @@ def workload_mstcn(args, dev, rank, dtype):
                           "over 40 full-length videos (T ~ U[1000, 6000]) per step",
               "model": "MultiStageModel_S(4,10,64,256,14,True)", "videos_per_step": 40}
     return step, sum(lens), config, check, (lambda: cpu_baseline_mstcn(args.cpu_baseline_seconds))
+
+
+def workload_mamba(args, dev, rank, dtype):
+    from models import mstcn
+    torch.manual_seed(0)
+    model = mstcn.CausalMambaModel(4, 10, 64, 256, 14, True).to(dev).eval()     # tecno.py:153
+    lens = video_lengths(40, seed=rank)
+    feats = [torch.randn(1, T, 256, device=dev) for T in lens]
+
+    def step():
+        out = None
+        for f in feats:
+            out = model(f.transpose(2, 1))
+        return out
+
+    def check(out):
+        assert out.shape == (1, 1, 14, lens[-1]) and torch.isfinite(out).all()
+
+    config = {"workload": "tecno.py CausalMambaModel(f_maps 64, f_dim 256, 10 Mamba blocks: d_state 64, d_conv 4, "
+                          "expand 2) over 40 full-length videos (T ~ U[1000, 6000]) per step",
+              "model": "CausalMambaModel(4,10,64,256,14,True)", "videos_per_step": 40}
+    return step, sum(lens), config, check, (lambda: cpu_baseline_mamba(args.cpu_baseline_seconds))
 
 
 def workload_e2e(args, dev, rank, dtype):
@@ -240,7 +278,7 @@ def workload_train(args, dev, rank, dtype):
     return step, args.batch, config, check, (lambda: cpu_baseline_train(args.variant, args.cpu_baseline_seconds))
 
 
-WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "e2e": workload_e2e, "train": workload_train}
+WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": workload_mamba, "e2e": workload_e2e, "train": workload_train}
 
 
 def main():
@@ -326,11 +364,13 @@ def main():
                         f"{nb / ms / 1e6:8.1f} GB/s  {shape:28s} {name}\n")
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
-    peak = PEAK_TFLOPS[args.dtype if args.workload != "mstcn" else "fp32"]
+    f32_only = args.workload in ("mstcn", "mamba")
+    peak = PEAK_TFLOPS["fp32" if f32_only else args.dtype]
     # bound by arithmetic intensity vs the machine balance (peak FLOP/s / 8 TB/s): tall-skinny
     # token GEMMs (K or N <= 128) are HBM-bound, the head / 4096-wide GEMMs MFMA-bound
     intensity = flops / max(nbytes, 1)
-    hbm_bound = intensity < peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    # the selective scan is a VALU recurrence (no MFMA work at all): priced against HBM
+    hbm_bound = intensity < peak * 1e12 / (HBM_PEAK_GBS * 1e9) or name.startswith("mamba_scan")
     tflops = flops / (ms * 1e-3) / 1e12
     gbs = nbytes / (ms * 1e-3) / 1e9
     roofline = {"bound": "hbm" if hbm_bound else "mfma", "kernel": name,
@@ -360,7 +400,7 @@ def main():
                 "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": "fp32" if args.workload == "mstcn" else args.dtype, "data": DATA, "config": config,
+                "dtype": "fp32" if f32_only else args.dtype, "data": DATA, "config": config,
                 "roofline": roofline, "cpu_baseline": cpu, "svk": svk.version()}
         print(json.dumps(line), flush=True)
     if world > 1:

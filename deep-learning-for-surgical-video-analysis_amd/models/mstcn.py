@@ -13,6 +13,7 @@ Output: ``[stages, B, classes, T]`` like the reference, returned as a view of th
 time-major [stages, B, T, classes] buffer the kernels write.
 """
 import copy
+import math
 
 import torch
 import torch.nn as nn
@@ -21,10 +22,6 @@ from svk import ops
 from svk.pack import get_packed
 from ._common import check_inference
 
-try:
-    from mamba_ssm import Mamba
-except ImportError:
-    Mamba = None
 
 
 def _w1x1(conv):
@@ -145,14 +142,118 @@ class MultiStageModel_S(nn.Module):
         return parser
 
 
+class Mamba(nn.Module):
+    """Selective state-space block with the parameter names, shapes and initialisation of
+    ``mamba_ssm.Mamba`` (v1, mamba_simple.py) — the module the reference imports at mstcn.py:9 and
+    stacks at mstcn.py:316-322 — so checkpoints written by the reference load strictly.  The forward is
+    MI355X-native: in_proj / x_proj / out_proj are MFMA GEMMs (f32), the causal depthwise conv + SiLU is
+    ``svk_mamba_conv_silu`` and the selective scan (dt projection, softplus, D skip and silu(z) gate
+    fused) is ``svk_mamba_scan``.  ``forward_tm`` adds the block's residual in out_proj's epilogue
+    (CausalMambaModel: ``x = x + blk(x)``, mstcn.py:335)."""
+
+    def __init__(self, d_model, d_state=16, d_conv=4, expand=2, dt_rank="auto", dt_min=0.001, dt_max=0.1,
+                 dt_init="random", dt_scale=1.0, dt_init_floor=1e-4, conv_bias=True, bias=False,
+                 use_fast_path=True, layer_idx=None, device=None, dtype=None):
+        super().__init__()
+        self.d_model, self.d_state, self.d_conv, self.expand = d_model, d_state, d_conv, expand
+        self.d_inner = int(expand * d_model)
+        self.dt_rank = math.ceil(d_model / 16) if dt_rank == "auto" else dt_rank
+        self.layer_idx = layer_idx
+        self.in_proj = nn.Linear(d_model, self.d_inner * 2, bias=bias)
+        self.conv1d = nn.Conv1d(self.d_inner, self.d_inner, d_conv, groups=self.d_inner, padding=d_conv - 1,
+                                bias=conv_bias)
+        self.activation = "silu"
+        self.act = nn.SiLU()
+        self.x_proj = nn.Linear(self.d_inner, self.dt_rank + d_state * 2, bias=False)
+        self.dt_proj = nn.Linear(self.dt_rank, self.d_inner, bias=True)
+        std = self.dt_rank ** -0.5 * dt_scale
+        if dt_init == "constant":
+            nn.init.constant_(self.dt_proj.weight, std)
+        else:
+            nn.init.uniform_(self.dt_proj.weight, -std, std)
+        dt = torch.exp(torch.rand(self.d_inner) * (math.log(dt_max) - math.log(dt_min)) + math.log(dt_min))
+        dt = dt.clamp(min=dt_init_floor)
+        with torch.no_grad():
+            self.dt_proj.bias.copy_(dt + torch.log(-torch.expm1(-dt)))
+        A = torch.arange(1, d_state + 1, dtype=torch.float32).repeat(self.d_inner, 1)
+        self.A_log = nn.Parameter(torch.log(A))
+        self.D = nn.Parameter(torch.ones(self.d_inner))
+        self.out_proj = nn.Linear(self.d_inner, d_model, bias=bias)
+
+    def _pack(self, dt):
+        f = lambda t: t.detach().float().contiguous()
+        return dict(w_in=f(self.in_proj.weight), b_in=None if self.in_proj.bias is None else f(self.in_proj.bias),
+                    conv_w=f(self.conv1d.weight[:, 0, :]),
+                    conv_b=None if self.conv1d.bias is None else f(self.conv1d.bias),
+                    w_x=f(self.x_proj.weight), w_dt=f(self.dt_proj.weight), b_dt=f(self.dt_proj.bias),
+                    a_neg=(-torch.exp(self.A_log.detach().float())).contiguous(), d_skip=f(self.D),
+                    w_out=f(self.out_proj.weight),
+                    b_out=None if self.out_proj.bias is None else f(self.out_proj.bias))
+
+    def forward_tm(self, x, B, T, residual=None):
+        """x [B*T, d_model] f32 time-major -> out_proj(y) (+ residual) [B*T, d_model]."""
+        p = get_packed(self, torch.float32, self._pack)
+        di = self.d_inner
+        xz = ops.gemm(x, p["w_in"], p["b_in"])                           # [BT, 2 Di]
+        xc = ops.mamba_conv_silu(xz[:, :di], p["conv_w"], p["conv_b"], B, T)
+        xdbl = ops.gemm(xc, p["w_x"])                                     # [BT, R + 2N]
+        y = ops.mamba_scan(xc, xdbl, xz[:, di:], p["w_dt"], p["b_dt"], p["a_neg"], p["d_skip"], B, T)
+        return ops.gemm(y, p["w_out"], p["b_out"], residual=residual)
+
+    def forward(self, hidden_states):
+        """mamba_ssm signature: [B, L, d_model] -> [B, L, d_model]."""
+        check_inference(self, hidden_states)
+        B, L, Dm = hidden_states.shape
+        x = hidden_states.float().contiguous().view(B * L, Dm)
+        return self.forward_tm(x, B, L).view(B, L, Dm)
+
+
 class CausalMambaModel(nn.Module):
-    """(mstcn.py:282-343).  Needs the ``mamba_ssm`` selective-scan kernels; like the reference it
-    raises ImportError when they are unavailable (mstcn.py:301-302).  An MI355X selective-scan
-    kernel is the SURVEY §8(f) rank-2 "next" item."""
+    """(mstcn.py:282-343).  Same constructor, submodule names and state_dict keys as the reference
+    (``in_proj``, ``blocks.{i}`` = Mamba v1 blocks, ``dropout``, ``norm``, ``head``); the reference raises
+    ImportError without ``mamba_ssm`` (mstcn.py:301-302) — this build carries its own selective-scan
+    kernels instead.  Eval-mode forward: x [B, f_dim, T] -> [1, B, classes, T], all time-major f32:
+    in_proj GEMM, per block (GEMM, conv+SiLU, GEMM, scan, GEMM + residual), LayerNorm, head GEMM."""
 
     def __init__(self, mstcn_stages, mstcn_layers, mstcn_f_maps, mstcn_f_dim, out_features, mstcn_causal_conv,
                  mamba_d_state=64, mamba_d_conv=4, mamba_expand=2, mamba_dropout=0.1):
         super().__init__()
-        if Mamba is None:
-            raise ImportError("mamba_ssm is not installed. Please run: pip install mamba-ssm")
-        raise NotImplementedError("CausalMambaModel: svk selective-scan kernel not built yet (SURVEY §8(f) rank 2)")
+        self.num_stages = mstcn_stages
+        self.num_layers = mstcn_layers
+        self.num_f_maps = mstcn_f_maps
+        self.dim = mstcn_f_dim
+        self.num_classes = out_features
+        self.causal_conv = mstcn_causal_conv
+        self.mamba_d_state = mamba_d_state
+        self.mamba_d_conv = mamba_d_conv if 2 <= mamba_d_conv <= 4 else 4     # mstcn.py:313
+        self.mamba_expand = mamba_expand
+        if mamba_d_state not in (16, 32, 64):
+            raise ValueError("CausalMambaModel: the svk selective scan supports d_state in {16, 32, 64}")
+        self.in_proj = nn.Linear(self.dim, self.num_f_maps)
+        self.blocks = nn.ModuleList([Mamba(d_model=self.num_f_maps, d_state=self.mamba_d_state,
+                                           d_conv=self.mamba_d_conv, expand=self.mamba_expand)
+                                     for _ in range(self.num_layers)])
+        if self.blocks and self.blocks[0].dt_rank > 16:
+            raise ValueError("CausalMambaModel: the svk selective scan supports dt_rank <= 16 (f_maps <= 256)")
+        self.dropout = nn.Dropout(mamba_dropout)
+        self.norm = nn.LayerNorm(self.num_f_maps)
+        self.head = nn.Linear(self.num_f_maps, self.num_classes)
+
+    def _pack(self, dt):
+        f = lambda t: t.detach().float().contiguous()
+        return dict(w_in=f(self.in_proj.weight), b_in=f(self.in_proj.bias), g=f(self.norm.weight),
+                    b=f(self.norm.bias), w_h=f(self.head.weight), b_h=f(self.head.bias))
+
+    def forward(self, x):
+        check_inference(self, x)
+        B, C, T = x.shape
+        p = get_packed(self, torch.float32, self._pack)
+        xt = x.transpose(1, 2)                                            # [B, T, C]
+        if xt.dtype != torch.float32 or not xt.is_contiguous():
+            xt = xt.float().contiguous()
+        h = ops.gemm(xt.view(B * T, C), p["w_in"], p["b_in"])
+        for blk in self.blocks:
+            h = blk.forward_tm(h, B, T, residual=h)                       # x = x + blk(x); dropout: eval identity
+        h = ops.layernorm(h, p["g"], p["b"], self.norm.eps)
+        logits = ops.gemm(h, p["w_h"], p["b_h"])                          # [B*T, classes]
+        return logits.view(B, T, self.num_classes).permute(0, 2, 1).unsqueeze(0)

@@ -32,6 +32,8 @@ SIGNATURES = {
     "svk_mean_rows": [c_int, P, c_long, P, c_int, c_int, c_int, P],
     "svk_softmax_rows": [P, c_long, P, c_long, c_int, c_int, P],
     "svk_mstcn_layer": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mamba_conv_silu": [P, c_long, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mamba_scan": [P, P, c_long, P, c_long, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P],
     "svk_window_unfold": [c_int, P, c_long, P, P, c_int, c_int, c_int, P],
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
     "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
@@ -68,7 +70,8 @@ SIGNATURES = {
 }
 STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
 LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
-              "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int]}
+              "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
+              "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int]}
 
 _lib = None
 

@@ -383,6 +383,55 @@ def mstcn_layer(x, wd_packed, bd, w1, b1, dilation, causal, out=None):
     return out
 
 
+def mamba_conv_silu(x, w, bias, B, T):
+    """x [B*T, Di] f32 (row stride may exceed Di: the x-half of in_proj's xz) -> silu(causal depthwise
+    conv) [B*T, Di]; w [Di, K]."""
+    _chk(x, "x", torch.float32); _chk(w, "w", torch.float32); _chk(bias, "bias", torch.float32)
+    M, Di, ldx = _rows(x, "x")
+    if M != B * T or w.shape[0] != Di or not w.is_contiguous():
+        raise _lib.SvkError(f"svk.mamba_conv_silu: x {tuple(x.shape)} / w {tuple(w.shape)} vs B={B} T={T}")
+    out = torch.empty(M, Di, device=x.device, dtype=torch.float32)
+    _lib.call("svk_mamba_conv_silu", _p(x), ldx, _p(w), _p(bias), _p(out), B, T, Di, w.shape[1], _stream())
+    return out
+
+
+def mamba_seg_len(B, T, Di, N, target_groups=512):
+    """Time-segment length for the two-pass scan: enough (video, channel-group, segment) workgroups
+    for ~2 per CU (256 CUs), segments a multiple of the 32-step chunk; >= T means one sequential pass."""
+    groups = B * -(-Di // (4 * (64 // N)))
+    S = max(1, min(target_groups // max(groups, 1), -(-T // 64)))
+    if S <= 1:
+        return max(T, 1)
+    return -(-(-(-T // S)) // 32) * 32
+
+
+def mamba_scan(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
+    """Selective scan with the dt projection, softplus, D skip and silu(z) gate fused:
+    u [B*T, Di], xdbl [B*T, R+2N] (dt_low | B | C), z [B*T, Di] (may be strided), w_dt [Di, R],
+    a_neg = -exp(A_log) [Di, N] -> y [B*T, Di] (f32)."""
+    for t, nm in ((u, "u"), (xdbl, "xdbl"), (z, "z"), (w_dt, "w_dt"), (b_dt, "b_dt"), (a_neg, "A"),
+                  (d_skip, "D")):
+        _chk(t, nm, torch.float32)
+    M, Di, ldu = _rows(u, "u")
+    Mx, W, ldxd = _rows(xdbl, "xdbl")
+    Mz, Dz, ldz = _rows(z, "z")
+    Dn, N = a_neg.shape
+    R = w_dt.shape[1]
+    if (M != B * T or Mx != M or Mz != M or Dz != Di or ldu != Di or Dn != Di or W != R + 2 * N
+            or not (w_dt.is_contiguous() and a_neg.is_contiguous())):
+        raise _lib.SvkError("svk.mamba_scan: shape mismatch")
+    out = torch.empty(M, Di, device=u.device, dtype=torch.float32)
+    seg = mamba_seg_len(B, T, Di, N) if seg_len is None else int(seg_len)
+    nws = _lib.load().svk_mamba_scan_workspace(B, T, Di, N, seg)
+    ws = torch.empty(nws // 4, device=u.device, dtype=torch.float32) if nws > 0 else None
+    t0 = _prof_begin()
+    _lib.call("svk_mamba_scan", _p(u), _p(xdbl), ldxd, _p(z), ldz, _p(w_dt), _p(b_dt), _p(a_neg), _p(d_skip),
+              _p(out), B, T, Di, N, R, seg, _p(ws), _stream())
+    # algorithmic: u, z, dt_low|B|C in, y out (f32); per (row, channel): 2R + 6 FLOP, per state 6 FLOP
+    _prof_end(t0, f"mamba_scan_kernel<{N}>", M * Di * (2 * R + 6 + 6 * N), 4 * M * (3 * Di + W), (M, Di, N))
+    return out
+
+
 def window_unfold(x, length, pos=None):
     """x [T, C] -> [T, length, C] causal windows (zero left-pad) + pos[length, C]."""
     _chk(x, "x"); _chk(pos, "pos", torch.float32)

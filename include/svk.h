@@ -133,6 +133,27 @@ int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C,
 int svk_mstcn_layer(const float* X, const float* Wd, const float* bd, const float* W1,
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
+/* CausalMambaModel (mstcn.py:282-343) block internals; the reference's Mamba is mamba_ssm's
+ * `Mamba` (mamba_simple.py, imported at mstcn.py:9), absent from the reference snapshot.
+ * Causal depthwise Conv1d (pad K-1, keep the first T outputs) + SiLU over B videos of T
+ * time-major rows: Y[b*T+t, d] = silu(bias[d] + sum_k W[d, k] X[b*T + t-(K-1)+k, d]).
+ * Replaces Mamba.conv1d + act (x = act(conv1d(x)[..., :seqlen])).  K <= 8, bias may be NULL. */
+int svk_mamba_conv_silu(const float* X, long ldx, const float* W, const float* bias, float* Y, int B, int T,
+                        int Di, int K, void* stream);
+
+/* Selective scan (mamba_ssm selective_scan_fn with delta_bias, delta_softplus=True, z gate):
+ * delta = softplus(Wdt[d,:] . XD[r, 0:R] + bdt[d]); h = exp(delta A[d,n]) h + delta XD[r, R+n] U[r,d];
+ * Y[r,d] = (sum_n XD[r, R+N+n] h[n] + Dp[d] U[r,d]) * silu(Z[r,d]), rows r = b*T+t, state reset per
+ * video.  U/Y [B*T, Di]; XD [B*T, >= R+2N] (x_proj output: dt_low | B | C); A = -exp(A_log) [Di, N];
+ * Wdt [Di, R].  N in {16, 32, 64}, R <= 16. */
+int svk_mamba_scan(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
+                   const float* bdt, const float* A, const float* Dp, float* Y, int B, int T, int Di, int N,
+                   int R, int seg_len, float* ws, void* stream);
+/* seg_len >= T: one sequential pass (ws may be NULL).  Otherwise time is split into ceil(T/seg_len)
+ * segments (seg_len a multiple of 32) scanned concurrently in two passes; ws (caller-owned) holds
+ * svk_mamba_scan_workspace(B, T, Di, N, seg_len) bytes of per-segment end states and delta sums. */
+long svk_mamba_scan_workspace(int B, int T, int Di, int N, int seg_len);
+
 /* Causal window unfold (adapter_transformer.py:336-343 as pad + unfold):
  * Y[t, i, c] = X[t - len + 1 + i, c] (0 if negative) + pos[i, c] (pos may be NULL). */
 int svk_window_unfold(int dtype, const void* X, long ldx, const float* pos, void* Y, int T, int C,

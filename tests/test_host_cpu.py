@@ -70,8 +70,9 @@ def test_mstcn_and_transformer_surface(golden):
     assert len(m.state_dict()) == 72
     t = adapter_transformer.Transformer(32, 2048, 14, 30)
     assert sorted(t.state_dict()) == sorted(SH.transformer_shapes(32, 2048, 14))
-    with pytest.raises(ImportError):
-        mstcn.CausalMambaModel(2, 8, 64, 2048, 14, True)
+    from oracle import mamba as OM
+    mm = mstcn.CausalMambaModel(2, 8, 64, 2048, 14, True)      # tecno.py:153 (svk scan, no mamba_ssm)
+    assert {k: tuple(v.shape) for k, v in mm.state_dict().items()} == OM.mamba_shapes(2048, 64, 8, 14)
 
 
 def test_no_cpu_fallback():
