@@ -395,9 +395,13 @@ def mamba_conv_silu(x, w, bias, B, T):
     return out
 
 
-def mamba_seg_len(B, T, Di, N, target_groups=512):
+MAMBA_GROUPS = int(os.environ.get("SVK_MAMBA_GROUPS", "512"))
+
+
+def mamba_seg_len(B, T, Di, N, target_groups=None):
     """Time-segment length for the two-pass scan: enough (video, channel-group, segment) workgroups
     for ~2 per CU (256 CUs), segments a multiple of the 32-step chunk; >= T means one sequential pass."""
+    target_groups = MAMBA_GROUPS if target_groups is None else target_groups
     groups = B * -(-Di // (4 * (64 // N)))
     S = max(1, min(target_groups // max(groups, 1), -(-T // 64)))
     if S <= 1:
