@@ -195,6 +195,38 @@ def workload_mamba(args, dev, rank, dtype):
     return step, sum(lens), config, check, (lambda: cpu_baseline_mamba(args.cpu_baseline_seconds))
 
 
+def cpu_baseline_preproc(budget_s, H=480, W=854):
+    from oracle import preproc as OP
+    img = np.random.default_rng(0).integers(0, 256, size=(H, W, 3), dtype=np.uint8)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        OP.frame_transform(img)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames {H}x{W} (numpy restatement of Pillow's resize + torch crop/normalise) in {dt:.1f} s"}
+
+
+def workload_preproc(args, dev, rank, dtype):
+    from svk.preproc import frame_transform
+    H, W = 480, 854                                           # Cholec80 frame size (854x480 video)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    frames = torch.randint(0, 256, (args.batch, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    out = torch.empty(args.batch, 3, 224, 224, device=dev)
+
+    def step():
+        return frame_transform(frames, out=out)
+
+    def check(o):
+        assert o.shape == (args.batch, 3, 224, 224) and torch.isfinite(o).all()
+
+    config = {"workload": "generate_evp_LFB.py eval transform on decoded frames: Resize((250, 250)) [Pillow bilinear, "
+                          "bit-exact] -> CenterCrop(224) -> ToTensor -> Normalize, 480x854 uint8 RGB -> [B, 3, 224, 224] f32",
+              "per_gpu_batch": args.batch}
+    return step, args.batch, config, check, (lambda: cpu_baseline_preproc(min(args.cpu_baseline_seconds, 10.0)))
+
+
 def workload_e2e(args, dev, rank, dtype):
     from models import mix_transformer_evp as mte, mstcn, adapter_transformer
     torch.manual_seed(0)
@@ -278,7 +310,7 @@ def workload_train(args, dev, rank, dtype):
     return step, args.batch, config, check, (lambda: cpu_baseline_train(args.variant, args.cpu_baseline_seconds))
 
 
-WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": workload_mamba, "e2e": workload_e2e, "train": workload_train}
+WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": workload_mamba, "preproc": workload_preproc, "e2e": workload_e2e, "train": workload_train}
 
 
 def main():
@@ -364,13 +396,13 @@ def main():
                         f"{nb / ms / 1e6:8.1f} GB/s  {shape:28s} {name}\n")
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
-    f32_only = args.workload in ("mstcn", "mamba")
+    f32_only = args.workload in ("mstcn", "mamba", "preproc")
     peak = PEAK_TFLOPS["fp32" if f32_only else args.dtype]
     # bound by arithmetic intensity vs the machine balance (peak FLOP/s / 8 TB/s): tall-skinny
     # token GEMMs (K or N <= 128) are HBM-bound, the head / 4096-wide GEMMs MFMA-bound
     intensity = flops / max(nbytes, 1)
     # the selective scan is a VALU recurrence (no MFMA work at all): priced against HBM
-    hbm_bound = intensity < peak * 1e12 / (HBM_PEAK_GBS * 1e9) or name.startswith("mamba_scan")
+    hbm_bound = intensity < peak * 1e12 / (HBM_PEAK_GBS * 1e9) or name.startswith(("mamba_scan", "frame_preproc"))
     tflops = flops / (ms * 1e-3) / 1e12
     gbs = nbytes / (ms * 1e-3) / 1e9
     roofline = {"bound": "hbm" if hbm_bound else "mfma", "kernel": name,

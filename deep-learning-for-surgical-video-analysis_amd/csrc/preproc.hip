@@ -1,0 +1,137 @@
+// Frame preprocessing on the GPU: the extraction/eval transform of
+// generate_evp_LFB.py:243-247 — transforms.Resize((250, 250)) on the decoded PIL RGB frame, CenterCrop(224),
+// ToTensor, Normalize(mean, std) — applied to a batch of decoded uint8 HWC frames (and, identically, to the
+// RGB segmaps: CholecFlowDataset applies the same transform to both, data_process.py:455-462).
+//
+// Resize is Pillow's separable antialiased bilinear resampling for 8-bit images, bit-exact: per output
+// coordinate a window [xmin, xmin + n) with fixed-point coefficients (22 fractional bits) that the host
+// computes exactly as Pillow does (svk/preproc.py); horizontal pass first, rounded (+2^21) and clipped to
+// uint8, then the vertical pass over the horizontal result, rounded and clipped again.  Only the 224x224
+// window CenterCrop keeps is produced: the horizontal pass runs for the kept columns, the vertical pass for
+// the kept rows.  ToTensor + Normalize are the same f32 operations torch performs (u8 / 255, then
+// (v - mean) / std), with correctly-rounded divisions, so the output equals the DataLoader's tensor.
+//
+// Layout: frames [B, H, W, 3] uint8 (decoder output, row-major HWC); tmp [B, H, CW, 3] uint8 (horizontal
+// result, caller-owned workspace); out [B, 3, CH, CW] f32 (the DataLoader's NCHW tensor).
+#include "svk_common.h"
+
+namespace svk {
+
+constexpr int PP_PREC = 22;
+
+__device__ __forceinline__ int pp_clip8(int ss) {
+  const int v = ss >> PP_PREC;
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// Horizontal pass: a workgroup owns PP_ROWS consecutive input rows of one frame — one contiguous byte range
+// of the HWC frame — and stages it in LDS with 16-byte loads (the range start aligned down to 16 bytes),
+// then every thread produces kept columns of those rows from LDS (taps of neighbouring output columns
+// overlap, so each input byte is read from HBM once).  Rows beyond H (last block) are skipped.
+constexpr int PP_ROWS = 4;     // 8 rows with a column-per-thread walk measured slower (358 vs 180 us)
+
+__global__ __launch_bounds__(256) void pp_resize_h(const uint8_t* __restrict__ in, uint8_t* __restrict__ tmp,
+                                                   const int* __restrict__ xb, const int* __restrict__ xk, int ksx,
+                                                   int B, int H, int W, int CW, int cx0) {
+  extern __shared__ uint4 pp_lds[];
+  uint8_t* rows = reinterpret_cast<uint8_t*>(pp_lds);
+  const int blocks_per_frame = (H + PP_ROWS - 1) / PP_ROWS;
+  const int b = blockIdx.x / blocks_per_frame;
+  const int y0 = (blockIdx.x - b * blocks_per_frame) * PP_ROWS;
+  const int nr = min(PP_ROWS, H - y0);
+  const long rowbytes = (long)W * 3;
+  const long start = ((long)b * H + y0) * rowbytes;
+  const long astart = start & ~15L;
+  const int lead = (int)(start - astart);
+  const long total_bytes = (long)B * H * rowbytes;
+  const int nbytes = lead + (int)(nr * rowbytes);
+  const int nvec = (nbytes + 15) >> 4;
+  const uint4* src = reinterpret_cast<const uint4*>(in + astart);
+  const long nvec_full = (total_bytes - astart) >> 4;          // whole 16-byte vectors inside the frames buffer
+  for (int v = threadIdx.x; v < nvec; v += 256) {
+    if (v < nvec_full) {
+      pp_lds[v] = src[v];
+    } else {                                                   // the buffer's ragged tail: byte loads
+      uint8_t* d = rows + 16 * v;
+      for (int q = 0; q < 16; ++q) d[q] = astart + 16L * v + q < total_bytes ? in[astart + 16L * v + q] : 0;
+    }
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < nr * CW; e += 256) {
+    const int r = e / CW, ox = e - r * CW;
+    const int x = cx0 + ox;
+    const int xmin = xb[2 * x], n = xb[2 * x + 1];
+    const int* k = xk + (long)x * ksx;
+    const uint8_t* p = rows + lead + r * rowbytes + xmin * 3;
+    int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
+    for (int j = 0; j < n; ++j) {
+      const int c = k[j];
+      s0 += p[3 * j] * c;
+      s1 += p[3 * j + 1] * c;
+      s2 += p[3 * j + 2] * c;
+    }
+    uint8_t* dst = tmp + ((((long)b * H + y0 + r) * CW) + ox) * 3;
+    dst[0] = (uint8_t)pp_clip8(s0);
+    dst[1] = (uint8_t)pp_clip8(s1);
+    dst[2] = (uint8_t)pp_clip8(s2);
+  }
+}
+
+// one thread per (b, kept row, kept column): vertical taps over tmp, then ToTensor + Normalize per channel
+__global__ __launch_bounds__(256) void pp_resize_v_norm(const uint8_t* __restrict__ tmp, float* __restrict__ out,
+                                                        const int* __restrict__ yb, const int* __restrict__ yk,
+                                                        int ksy, int B, int H, int CH, int CW, int cy0, float m0,
+                                                        float m1, float m2, float s0d, float s1d, float s2d) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * CH * CW;
+  if (i >= total) return;
+  const int ox = (int)(i % CW);
+  const long r = i / CW;
+  const int oy = (int)(r % CH);
+  const int b = (int)(r / CH);
+  const int y = cy0 + oy;
+  const int ymin = yb[2 * y], n = yb[2 * y + 1];
+  const int* k = yk + (long)y * ksy;
+  const uint8_t* src = tmp + (((long)b * H + ymin) * CW + ox) * 3;
+  int a0 = 1 << (PP_PREC - 1), a1 = a0, a2 = a0;
+  for (int j = 0; j < n; ++j) {
+    const int c = k[j];
+    const uint8_t* p = src + (long)j * CW * 3;
+    a0 += p[0] * c;
+    a1 += p[1] * c;
+    a2 += p[2] * c;
+  }
+  const long plane = (long)CH * CW;
+  float* o = out + (long)b * 3 * plane + (long)oy * CW + ox;
+  o[0] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a0), 255.f) - m0, s0d);
+  o[plane] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a1), 255.f) - m1, s1d);
+  o[2 * plane] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a2), 255.f) - m2, s2d);
+}
+
+}  // namespace svk
+
+using namespace svk;
+
+extern "C" int svk_frame_preproc(const void* frames, void* tmp, float* out, const int* xbounds, const int* xcoef,
+                                 int ksx, const int* ybounds, const int* ycoef, int ksy, int B, int H, int W,
+                                 int crop_y0, int crop_x0, int CH, int CW, const float* mean, const float* std,
+                                 void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || CH <= 0 || CW <= 0 || crop_y0 < 0 || crop_x0 < 0 || ksx <= 0 || ksy <= 0 ||
+      !frames || !tmp || !out || !xbounds || !xcoef || !ybounds || !ycoef || !mean || !std) {
+    set_error("svk_frame_preproc: bad args (B=%d H=%d W=%d crop %dx%d at (%d, %d))", B, H, W, CH, CW, crop_y0,
+              crop_x0);
+    return SVK_EINVAL;
+  }
+  if (B == 0) return SVK_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const long tv = (long)B * CH * CW;
+  const long lds = ((16 + (long)PP_ROWS * W * 3 + 15) / 16) * 16;
+  if (lds > 64 * 1024) { set_error("svk_frame_preproc: frame width %d too large (W*3*%d > 64 KiB)", W, PP_ROWS); return SVK_EUNSUPPORTED; }
+  const int bpf = (H + PP_ROWS - 1) / PP_ROWS;
+  hipLaunchKernelGGL(pp_resize_h, dim3((unsigned)((long)B * bpf)), dim3(256), (size_t)lds, s, (const uint8_t*)frames,
+                     (uint8_t*)tmp, xbounds, xcoef, ksx, B, H, W, CW, crop_x0);
+  hipLaunchKernelGGL(pp_resize_v_norm, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, (const uint8_t*)tmp,
+                     out, ybounds, ycoef, ksy, B, H, CH, CW, crop_y0, mean[0], mean[1], mean[2], std[0], std[1],
+                     std[2]);
+  return check_launch("frame_preproc");
+}

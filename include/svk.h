@@ -154,6 +154,18 @@ int svk_mamba_scan(const float* U, const float* XD, long ldxd, const float* Z, l
  * svk_mamba_scan_workspace(B, T, Di, N, seg_len) bytes of per-segment end states and delta sums. */
 long svk_mamba_scan_workspace(int B, int T, int Di, int N, int seg_len);
 
+/* Frame preprocessing: generate_evp_LFB.py:243-247's Resize((OH, OW)) ->
+ * CenterCrop -> ToTensor -> Normalize on decoded uint8 RGB frames [B, H, W, 3], bit-exact to Pillow's
+ * 8-bit bilinear resampling (libImaging/Resample.c: horizontal then vertical pass, 22-bit fixed-point
+ * coefficients, round + clip to uint8 after each pass) and torch's f32 (u8 / 255 - mean) / std.
+ * xbounds [OW, 2] / ybounds [OH, 2] = (first tap, tap count), xcoef [OW, ksx] / ycoef [OH, ksy]: Pillow's
+ * fixed-point coefficients (device arrays, built by svk/preproc.py); only the CH x CW crop window at
+ * (crop_y0, crop_x0) of the resized frame is produced.  tmp: caller-owned [B, H, CW, 3] uint8 scratch.
+ * out [B, 3, CH, CW] f32.  mean / std: HOST arrays of 3 floats. */
+int svk_frame_preproc(const void* frames, void* tmp, float* out, const int* xbounds, const int* xcoef, int ksx,
+                      const int* ybounds, const int* ycoef, int ksy, int B, int H, int W, int crop_y0,
+                      int crop_x0, int CH, int CW, const float* mean, const float* std, void* stream);
+
 /* Causal window unfold (adapter_transformer.py:336-343 as pad + unfold):
  * Y[t, i, c] = X[t - len + 1 + i, c] (0 if negative) + pos[i, c] (pos may be NULL). */
 int svk_window_unfold(int dtype, const void* X, long ldx, const float* pos, void* Y, int T, int C,
