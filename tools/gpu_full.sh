@@ -25,3 +25,10 @@ step bench_x timeout -k 10 400 python bench.py --steps ${STEPS:-10} --warmup 3 >
 tail -1 $O/bench_extract.log | cut -c1-600
 step bench_t timeout -k 10 300 python bench.py --workload train --steps ${STEPS:-10} --warmup 3 --no-cpu-baseline > $O/bench_train.log 2>&1
 tail -1 $O/bench_train.log | cut -c1-600
+# widened rows: CausalMambaModel (selective scan) and the frame transform
+step prof_m timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_m -o run -- $B --workload mamba --steps 2 --warmup 1 > $O/prof_m.log 2>&1
+step prof_p timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_p -o run -- $B --workload preproc --steps 5 --warmup 1 > $O/prof_p.log 2>&1
+step bench_m timeout -k 10 200 python bench.py --workload mamba --steps 3 --warmup 1 --cpu-baseline-seconds 15 > $O/bench_mamba.log 2>&1
+tail -1 $O/bench_mamba.log | cut -c1-300
+step bench_p timeout -k 10 200 python bench.py --workload preproc --steps 10 --warmup 2 --cpu-baseline-seconds 10 > $O/bench_preproc.log 2>&1
+tail -1 $O/bench_preproc.log | cut -c1-300
