@@ -108,6 +108,42 @@ __global__ __launch_bounds__(256) void pp_resize_v_norm(const uint8_t* __restric
   o[2 * plane] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a2), 255.f) - m2, s2d);
 }
 
+// Optical-flow transform (CholecFlowDataset, data_process.py:425-447 + the CenterCrop of the transform):
+// cv2.resize(flow, (OW, OH), INTER_LINEAR) on the float32 [H, W, 2] .npy field, u *= OW / W, v *= OH / H,
+// then CenterCrop.  cv2's float INTER_LINEAR: per output column a source index sx and weights (1 - fx, fx)
+// from fx = (float)((dx + 0.5) * scale - 0.5) with edge clamping (host tables, svk/preproc.py); the
+// horizontal pass forms each needed source row's value, the vertical pass blends two rows, as separate
+// f32 multiplies and adds (this file is compiled with -ffp-contract=off) like OpenCV's scalar path.
+__global__ __launch_bounds__(256) void pp_flow(const float* __restrict__ in, float* __restrict__ out,
+                                               const int* __restrict__ xo, const float* __restrict__ xa,
+                                               const int* __restrict__ yo, const float* __restrict__ ya, int B, int H,
+                                               int W, int CH, int CW, int cy0, int cx0, float su, float sv) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * CH * CW;
+  if (i >= total) return;
+  const int ox = (int)(i % CW);
+  const long r = i / CW;
+  const int oy = (int)(r % CH);
+  const int b = (int)(r / CH);
+  const int x = cx0 + ox, y = cy0 + oy;
+  const int sx = xo[x], sy = yo[y];
+  const int sx1 = min(sx + 1, W - 1), sy1 = min(sy + 1, H - 1);
+  const float a0 = xa[2 * x], a1 = xa[2 * x + 1], b0 = ya[2 * y], b1 = ya[2 * y + 1];
+  const float2* f = reinterpret_cast<const float2*>(in) + (long)b * H * W;
+  const float2 p00 = f[(long)sy * W + sx], p01 = f[(long)sy * W + sx1];
+  const float2 p10 = f[(long)sy1 * W + sx], p11 = f[(long)sy1 * W + sx1];
+  const float h0u = __fadd_rn(__fmul_rn(p00.x, a0), __fmul_rn(p01.x, a1));
+  const float h0v = __fadd_rn(__fmul_rn(p00.y, a0), __fmul_rn(p01.y, a1));
+  const float h1u = __fadd_rn(__fmul_rn(p10.x, a0), __fmul_rn(p11.x, a1));
+  const float h1v = __fadd_rn(__fmul_rn(p10.y, a0), __fmul_rn(p11.y, a1));
+  const float u = __fadd_rn(__fmul_rn(h0u, b0), __fmul_rn(h1u, b1));
+  const float v = __fadd_rn(__fmul_rn(h0v, b0), __fmul_rn(h1v, b1));
+  const long plane = (long)CH * CW;
+  float* o = out + (long)b * 2 * plane + (long)oy * CW + ox;
+  o[0] = __fmul_rn(u, su);
+  o[plane] = __fmul_rn(v, sv);
+}
+
 }  // namespace svk
 
 using namespace svk;
@@ -134,4 +170,19 @@ extern "C" int svk_frame_preproc(const void* frames, void* tmp, float* out, cons
                      out, ybounds, ycoef, ksy, B, H, CH, CW, crop_y0, mean[0], mean[1], mean[2], std[0], std[1],
                      std[2]);
   return check_launch("frame_preproc");
+}
+
+extern "C" int svk_flow_preproc(const float* flow, float* out, const int* xofs, const float* xalpha, const int* yofs,
+                                const float* yalpha, int B, int H, int W, int crop_y0, int crop_x0, int CH, int CW,
+                                float scale_u, float scale_v, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || CH <= 0 || CW <= 0 || crop_y0 < 0 || crop_x0 < 0 || !flow || !out || !xofs ||
+      !xalpha || !yofs || !yalpha || ((uintptr_t)flow & 7)) {
+    set_error("svk_flow_preproc: bad args (B=%d H=%d W=%d, flow 8-byte aligned)", B, H, W);
+    return SVK_EINVAL;
+  }
+  const long tv = (long)B * CH * CW;
+  if (tv == 0) return SVK_OK;
+  hipLaunchKernelGGL(pp_flow, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, (hipStream_t)stream, flow, out, xofs,
+                     xalpha, yofs, yalpha, B, H, W, CH, CW, crop_y0, crop_x0, scale_u, scale_v);
+  return check_launch("flow_preproc");
 }

@@ -94,3 +94,52 @@ def frame_transform(frames, size=(250, 250), crop=224, mean=CHOLEC80_MEAN, std=C
     _prof_end(t0, "frame_preproc", B * (CW * H * ksx + CH * CW * ksy) * 3 * 2, B * (H * W * 3 + 3 * CH * CW * 4),
               (B, H, W))
     return out
+
+
+def cv2_linear_table(in_size, out_size):
+    """cv2.resize INTER_LINEAR (float images) per-axis table: source index and (1 - f, f) float32 weights,
+    fx = (float)((dx + 0.5) * scale - 0.5), scale = 1 / (out / in) in double, clamped at both edges."""
+    scale = 1.0 / (float(out_size) / in_size)
+    ofs = np.zeros(out_size, np.int32)
+    alpha = np.zeros((out_size, 2), np.float32)
+    for dx in range(out_size):
+        fx = np.float32((dx + 0.5) * scale - 0.5)
+        sx = int(math.floor(fx))
+        fx = np.float32(fx - np.float32(sx))
+        if sx < 0:
+            fx, sx = np.float32(0.0), 0
+        if sx >= in_size - 1:
+            fx, sx = np.float32(0.0), in_size - 1
+        ofs[dx] = sx
+        alpha[dx] = (np.float32(1.0) - fx, fx)
+    return ofs, alpha
+
+
+_CV_CACHE = {}
+
+
+def flow_transform(flow, size=(250, 250), crop=224, out=None):
+    """flow [B, H, W, 2] f32 (the RAFT .npy fields, on the GPU) -> [B, 2, crop, crop] f32: CholecFlowDataset's
+    cv2 resize + displacement rescale (data_process.py:425-447) and the transform's CenterCrop."""
+    _chk(flow, "flow", torch.float32)
+    if flow.dim() != 4 or flow.shape[-1] != 2 or not flow.is_contiguous():
+        raise _lib.SvkError(f"svk.flow_transform: flow must be contiguous [B, H, W, 2] f32, got {tuple(flow.shape)}")
+    B, H, W, _ = flow.shape
+    OH, OW = size
+    cy0, cx0 = center_crop_offsets(OH, crop), center_crop_offsets(OW, crop)
+    key = (H, W, OH, OW, flow.device)
+    if key not in _CV_CACHE:
+        xo, xa = cv2_linear_table(W, OW)
+        yo, ya = cv2_linear_table(H, OH)
+        d = flow.device
+        _CV_CACHE[key] = tuple(torch.from_numpy(a).to(d) for a in (xo, xa, yo, ya))
+    xo, xa, yo, ya = _CV_CACHE[key]
+    if out is None:
+        out = torch.empty(B, 2, crop, crop, device=flow.device, dtype=torch.float32)
+    _chk(out, "out", torch.float32)
+    if tuple(out.shape) != (B, 2, crop, crop) or not out.is_contiguous():
+        raise _lib.SvkError("svk.flow_transform: out must be contiguous [B, 2, crop, crop] f32")
+    su, sv = float(np.float32(OW / W)), float(np.float32(OH / H))     # numpy: f32 array *= python float
+    _lib.call("svk_flow_preproc", _p(flow), _p(out), _p(xo), _p(xa), _p(yo), _p(ya), B, H, W, cy0, cx0, crop, crop,
+              su, sv, _stream())
+    return out

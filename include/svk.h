@@ -166,6 +166,14 @@ int svk_frame_preproc(const void* frames, void* tmp, float* out, const int* xbou
                       const int* ybounds, const int* ycoef, int ksy, int B, int H, int W, int crop_y0,
                       int crop_x0, int CH, int CW, const float* mean, const float* std, void* stream);
 
+/* Optical-flow transform (data_process.py:425-447 + CenterCrop): cv2.resize(INTER_LINEAR) of float32
+ * flow [B, H, W, 2] to the (OH, OW) grid, u *= scale_u (= OW / W), v *= scale_v (= OH / H), crop CH x CW at
+ * (crop_y0, crop_x0) -> out [B, 2, CH, CW] f32.  xofs/xalpha [OW] / [OW, 2] and yofs/yalpha: cv2's source
+ * index and (1 - f, f) weights per output coordinate (device arrays, svk/preproc.py).  No FMA contraction. */
+int svk_flow_preproc(const float* flow, float* out, const int* xofs, const float* xalpha, const int* yofs,
+                     const float* yalpha, int B, int H, int W, int crop_y0, int crop_x0, int CH, int CW,
+                     float scale_u, float scale_v, void* stream);
+
 /* Causal window unfold (adapter_transformer.py:336-343 as pad + unfold):
  * Y[t, i, c] = X[t - len + 1 + i, c] (0 if negative) + pos[i, c] (pos may be NULL). */
 int svk_window_unfold(int dtype, const void* X, long ldx, const float* pos, void* Y, int T, int C,

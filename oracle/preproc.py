@@ -74,3 +74,48 @@ def frame_transform(img_u8, size=(250, 250), crop=224, mean=(0.41757566, 0.26098
     m = torch.as_tensor(mean, dtype=torch.float32)[:, None, None]
     s = torch.as_tensor(std, dtype=torch.float32)[:, None, None]
     return x.sub_(m).div_(s)
+
+
+# ---- optical flow (data_process.py:425-447): cv2.resize INTER_LINEAR on float32, displacement rescale, crop ----
+# cv2 (opencv-python) is absent from this image: the restatement follows OpenCV's resizeGeneric_ for
+# INTER_LINEAR on CV_32F (HResizeLinear + VResizeLinear): fx = (float)((dx + 0.5) * scale - 0.5),
+# sx = floor(fx), fx -= sx, clamped to (0, 0) below and (size - 1, 0) above; horizontal blend per source row,
+# then vertical blend, each as f32 multiply + add.  **Parity against cv2 unpinned** (OpenCV's SIMD vertical
+# blend may use FMA, a <= 1-ulp difference); the GPU kernel is checked against this restatement.
+
+def _cv_axis(in_size, out_size):
+    scale = 1.0 / (float(out_size) / in_size)
+    i0 = np.zeros(out_size, np.int64)
+    w = np.zeros((out_size, 2), np.float32)
+    for d in range(out_size):
+        f = np.float32((d + 0.5) * scale - 0.5)
+        sidx = int(np.floor(f))
+        f = np.float32(f - np.float32(sidx))
+        if sidx < 0:
+            sidx, f = 0, np.float32(0)
+        if sidx >= in_size - 1:
+            sidx, f = in_size - 1, np.float32(0)
+        i0[d] = sidx
+        w[d] = (np.float32(1) - f, f)
+    return i0, np.minimum(i0 + 1, in_size - 1), w
+
+
+def cv2_resize_linear(img, out_hw):
+    """img [H, W, C] float32 -> [OH, OW, C] float32 (cv2.resize(img, (OW, OH), interpolation=INTER_LINEAR))."""
+    H, W, _ = img.shape
+    OH, OW = out_hw
+    x0, x1, wx = _cv_axis(W, OW)
+    y0, y1, wy = _cv_axis(H, OH)
+    hr = img[:, x0, :] * wx[None, :, 0:1] + img[:, x1, :] * wx[None, :, 1:2]      # f32 mul, f32 add
+    return (hr[y0] * wy[:, 0:1, None] + hr[y1] * wy[:, 1:2, None]).astype(np.float32)
+
+
+def flow_transform(flow, size=(250, 250), crop=224):
+    """flow [H, W, 2] float32 -> [2, crop, crop] f32 as CholecFlowDataset + CenterCrop produce it."""
+    H, W, _ = flow.shape
+    r = cv2_resize_linear(flow.astype(np.float32), size)
+    r[:, :, 0] *= size[1] / W                  # numpy 2: python float is weak -> f32 multiply
+    r[:, :, 1] *= size[0] / H
+    t = int(round((size[0] - crop) / 2.0))
+    l = int(round((size[1] - crop) / 2.0))
+    return torch.from_numpy(np.ascontiguousarray(r[t:t + crop, l:l + crop])).permute(2, 0, 1).contiguous()

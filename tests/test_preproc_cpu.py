@@ -38,3 +38,31 @@ def test_host_coefficients_match_oracle(n_in, n_out):
     assert c.shape == kk.shape
     np.testing.assert_array_equal(c, kk)
     np.testing.assert_array_equal(b[:, 0], idx[:, 0])
+
+
+def test_flow_oracle_identity_size_is_a_crop():
+    f = np.random.default_rng(0).standard_normal((250, 250, 2)).astype(np.float32)
+    out = OP.flow_transform(f)
+    assert torch.equal(out, torch.from_numpy(f[13:237, 13:237].copy()).permute(2, 0, 1))
+
+
+def test_flow_oracle_constant_and_ramp():
+    const = np.empty((480, 854, 2), np.float32)
+    const[..., 0], const[..., 1] = 3.0, -2.0
+    out = OP.flow_transform(const)
+    assert torch.allclose(out[0], torch.tensor(3.0 * 250 / 854)) and torch.allclose(out[1], torch.tensor(-2.0 * 250 / 480))
+    # a linear ramp along x is reproduced by bilinear interpolation at the half-pixel-centred sample points
+    W = 500
+    ramp = np.broadcast_to(np.arange(W, dtype=np.float32)[None, :, None], (100, W, 2)).copy()
+    r = OP.cv2_resize_linear(ramp, (250, 250))
+    expect = (np.arange(250) + 0.5) * (W / 250) - 0.5
+    np.testing.assert_allclose(r[0, :, 0], np.clip(expect, 0, W - 1), rtol=0, atol=1e-4)
+
+
+def test_host_cv2_tables_match_oracle():
+    from svk.preproc import cv2_linear_table
+    for n_in in (854, 480, 250, 200):
+        o, a = cv2_linear_table(n_in, 250)
+        i0, _, w = OP._cv_axis(n_in, 250)
+        np.testing.assert_array_equal(o, i0)
+        np.testing.assert_array_equal(a, w)

@@ -71,3 +71,16 @@ def test_frame_transform_rejects_bad_input(cuda):
         frame_transform(torch.zeros(1, 100, 100, 3, dtype=torch.float32, device=cuda))
     with pytest.raises(svk.SvkError):
         frame_transform(torch.zeros(1, 100, 100, 3, dtype=torch.uint8, device=cuda), size=(200, 200), crop=224)
+
+
+@pytest.mark.parametrize("hw", [(480, 854), (250, 250), (200, 300)])
+def test_flow_transform_vs_oracle(cuda, hw):
+    """GPU flow transform vs the cv2 INTER_LINEAR restatement (both f32 multiply + add, no FMA): bit-exact.
+    Parity against cv2 itself is unpinned (cv2 absent here; see oracle/preproc.py)."""
+    from svk.preproc import flow_transform
+    fl = (np.random.default_rng(hw[1]).standard_normal((2, *hw, 2)) * 2.0).astype(np.float32)   # N(0, 2 px)
+    out = flow_transform(torch.from_numpy(fl).to(cuda))
+    torch.cuda.synchronize()
+    ref = torch.stack([OP.flow_transform(f) for f in fl])
+    assert out.shape == (2, 2, 224, 224)
+    assert torch.equal(out.cpu(), ref), float((out.cpu() - ref).abs().max())
