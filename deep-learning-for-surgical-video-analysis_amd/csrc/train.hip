@@ -374,21 +374,31 @@ struct PackDesc {
 template <typename T>
 __global__ void pack_params_kernel(const PackDesc* __restrict__ d, int nd, long total, const float* __restrict__ src,
                                    T* __restrict__ dst) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  int lo = 0, hi = nd - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (d[mid].start <= i) lo = mid; else hi = mid - 1;
+  // one binary search per block (its first index), then each thread steps forward over the few descriptors
+  // the block spans; per-descriptor index math in 32 bits (every packed tensor has < 2^31 elements)
+  __shared__ int s_first;
+  const long blk0 = (long)blockIdx.x * blockDim.x;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = nd - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (d[mid].start <= blk0) lo = mid; else hi = mid - 1;
+    }
+    s_first = lo;
   }
+  __syncthreads();
+  const long i = blk0 + threadIdx.x;
+  if (i >= total) return;
+  int lo = s_first;
+  while (lo + 1 < nd && d[lo + 1].start <= i) ++lo;
   const PackDesc& e = d[lo];
-  long r = i - e.start;
-  if (r >= (long)e.n[0] * e.n[1] * e.n[2] * e.n[3]) return;   // alignment gap between descriptors
+  int r = (int)(i - e.start);
+  if (r >= e.n[0] * e.n[1] * e.n[2] * e.n[3]) return;          // alignment gap between descriptors
   long off = e.src;
   bool ok = true;
 #pragma unroll
   for (int k = 3; k >= 0; --k) {
-    const int idx = (int)(r % e.n[k]);
+    const int idx = r % e.n[k];
     r /= e.n[k];
     ok = ok && idx < e.lim[k];
     off += (long)idx * e.s[k];
