@@ -28,7 +28,7 @@ __device__ __forceinline__ int pp_clip8(int ss) {
 // of the HWC frame — and stages it in LDS with 16-byte loads (the range start aligned down to 16 bytes),
 // then every thread produces kept columns of those rows from LDS (taps of neighbouring output columns
 // overlap, so each input byte is read from HBM once).  Rows beyond H (last block) are skipped.
-constexpr int PP_ROWS = 4;     // 8 rows with a column-per-thread walk measured slower (358 vs 180 us)
+constexpr int PP_ROWS = 4;     // sweep (B = 256, 480x854): 2 rows 893k, 4 rows 978k, 8 rows 941k frames/s
 
 __global__ __launch_bounds__(256) void pp_resize_h(const uint8_t* __restrict__ in, uint8_t* __restrict__ tmp,
                                                    const int* __restrict__ xb, const int* __restrict__ xk, int ksx,
@@ -57,55 +57,87 @@ __global__ __launch_bounds__(256) void pp_resize_h(const uint8_t* __restrict__ i
     }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < nr * CW; e += 256) {
-    const int r = e / CW, ox = e - r * CW;
-    const int x = cx0 + ox;
-    const int xmin = xb[2 * x], n = xb[2 * x + 1];
-    const int* k = xk + (long)x * ksx;
-    const uint8_t* p = rows + lead + r * rowbytes + xmin * 3;
-    int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
-    for (int j = 0; j < n; ++j) {
-      const int c = k[j];
-      s0 += p[3 * j] * c;
-      s1 += p[3 * j + 1] * c;
-      s2 += p[3 * j + 2] * c;
+  // thread -> (row, 4 consecutive kept columns): 12 output bytes written as three 4-byte stores
+  const int CG = CW >> 2;                                      // CW % 4 == 0 (checked by the launcher)
+  for (int e = threadIdx.x; e < nr * CG; e += 256) {
+    const int r = e / CG, ox = (e - r * CG) * 4;
+    int acc[12];
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int x = cx0 + ox + px;
+      const int xmin = xb[2 * x], n = xb[2 * x + 1];
+      const int* k = xk + (long)x * ksx;
+      const uint8_t* p = rows + lead + r * rowbytes + xmin * 3;
+      int s0 = 1 << (PP_PREC - 1), s1 = s0, s2 = s0;
+      for (int j = 0; j < n; ++j) {
+        const int c = k[j];
+        s0 += p[3 * j] * c;
+        s1 += p[3 * j + 1] * c;
+        s2 += p[3 * j + 2] * c;
+      }
+      acc[3 * px] = pp_clip8(s0);
+      acc[3 * px + 1] = pp_clip8(s1);
+      acc[3 * px + 2] = pp_clip8(s2);
     }
-    uint8_t* dst = tmp + ((((long)b * H + y0 + r) * CW) + ox) * 3;
-    dst[0] = (uint8_t)pp_clip8(s0);
-    dst[1] = (uint8_t)pp_clip8(s1);
-    dst[2] = (uint8_t)pp_clip8(s2);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(tmp + ((((long)b * H + y0 + r) * CW) + ox) * 3);
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      dst[q] = (uint32_t)acc[4 * q] | ((uint32_t)acc[4 * q + 1] << 8) | ((uint32_t)acc[4 * q + 2] << 16) |
+               ((uint32_t)acc[4 * q + 3] << 24);
   }
 }
 
-// one thread per (b, kept row, kept column): vertical taps over tmp, then ToTensor + Normalize per channel
+// one thread per (b, kept row, 4 kept columns): vertical taps over tmp with 3 x 4-byte loads per tap (the 4
+// pixels' 12 bytes), then ToTensor + Normalize per channel and one 16-byte store per plane.  Needs CW % 4 == 0
+// and 4/16-byte aligned buffers (otherwise the launcher picks PX = 1, one column per thread).
+template <int PX>
 __global__ __launch_bounds__(256) void pp_resize_v_norm(const uint8_t* __restrict__ tmp, float* __restrict__ out,
                                                         const int* __restrict__ yb, const int* __restrict__ yk,
                                                         int ksy, int B, int H, int CH, int CW, int cy0, float m0,
                                                         float m1, float m2, float s0d, float s1d, float s2d) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * CH * CW;
+  const int CG = CW / PX;
+  const long total = (long)B * CH * CG;
   if (i >= total) return;
-  const int ox = (int)(i % CW);
-  const long r = i / CW;
+  const int ox = (int)(i % CG) * PX;
+  const long r = i / CG;
   const int oy = (int)(r % CH);
   const int b = (int)(r / CH);
   const int y = cy0 + oy;
   const int ymin = yb[2 * y], n = yb[2 * y + 1];
   const int* k = yk + (long)y * ksy;
   const uint8_t* src = tmp + (((long)b * H + ymin) * CW + ox) * 3;
-  int a0 = 1 << (PP_PREC - 1), a1 = a0, a2 = a0;
+  int acc[3 * PX];
+#pragma unroll
+  for (int q = 0; q < 3 * PX; ++q) acc[q] = 1 << (PP_PREC - 1);
   for (int j = 0; j < n; ++j) {
     const int c = k[j];
     const uint8_t* p = src + (long)j * CW * 3;
-    a0 += p[0] * c;
-    a1 += p[1] * c;
-    a2 += p[2] * c;
+    if (PX == 4) {
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) {
+        const uint32_t v = w[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[4 * q + e] += (int)((v >> (8 * e)) & 0xff) * c;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 3 * PX; ++q) acc[q] += p[q] * c;
+    }
   }
   const long plane = (long)CH * CW;
   float* o = out + (long)b * 3 * plane + (long)oy * CW + ox;
-  o[0] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a0), 255.f) - m0, s0d);
-  o[plane] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a1), 255.f) - m1, s1d);
-  o[2 * plane] = __fdiv_rn(__fdiv_rn((float)pp_clip8(a2), 255.f) - m2, s2d);
+  const float mm[3] = {m0, m1, m2}, ss[3] = {s0d, s1d, s2d};
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    float v[PX];
+#pragma unroll
+    for (int px = 0; px < PX; ++px)                 // acc index = pixel * 3 + channel (HWC bytes)
+      v[px] = __fdiv_rn(__fdiv_rn((float)pp_clip8(acc[3 * px + ch]), 255.f) - mm[ch], ss[ch]);
+    if (PX == 4) *reinterpret_cast<float4*>(o + ch * plane) = make_float4(v[0], v[1], v[2], v[3]);
+    else o[ch * plane] = v[0];
+  }
 }
 
 // Optical-flow transform (CholecFlowDataset, data_process.py:425-447 + the CenterCrop of the transform):
@@ -161,14 +193,24 @@ extern "C" int svk_frame_preproc(const void* frames, void* tmp, float* out, cons
   if (B == 0) return SVK_OK;
   hipStream_t s = (hipStream_t)stream;
   const long tv = (long)B * CH * CW;
+  if (CW % 4 != 0 || ((uintptr_t)tmp & 3)) {
+    set_error("svk_frame_preproc: crop width %d must be a multiple of 4 (4-byte aligned scratch)", CW);
+    return SVK_EUNSUPPORTED;
+  }
   const long lds = ((16 + (long)PP_ROWS * W * 3 + 15) / 16) * 16;
   if (lds > 64 * 1024) { set_error("svk_frame_preproc: frame width %d too large (W*3*%d > 64 KiB)", W, PP_ROWS); return SVK_EUNSUPPORTED; }
   const int bpf = (H + PP_ROWS - 1) / PP_ROWS;
   hipLaunchKernelGGL(pp_resize_h, dim3((unsigned)((long)B * bpf)), dim3(256), (size_t)lds, s, (const uint8_t*)frames,
                      (uint8_t*)tmp, xbounds, xcoef, ksx, B, H, W, CW, crop_x0);
-  hipLaunchKernelGGL(pp_resize_v_norm, dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s, (const uint8_t*)tmp,
-                     out, ybounds, ycoef, ksy, B, H, CH, CW, crop_y0, mean[0], mean[1], mean[2], std[0], std[1],
-                     std[2]);
+  const bool vec = CW % 4 == 0 && ((uintptr_t)tmp & 3) == 0 && ((uintptr_t)out & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL((pp_resize_v_norm<4>), dim3((unsigned)((tv / 4 + 255) / 256)), dim3(256), 0, s,
+                       (const uint8_t*)tmp, out, ybounds, ycoef, ksy, B, H, CH, CW, crop_y0, mean[0], mean[1], mean[2],
+                       std[0], std[1], std[2]);
+  else
+    hipLaunchKernelGGL((pp_resize_v_norm<1>), dim3((unsigned)((tv + 255) / 256)), dim3(256), 0, s,
+                       (const uint8_t*)tmp, out, ybounds, ycoef, ksy, B, H, CH, CW, crop_y0, mean[0], mean[1], mean[2],
+                       std[0], std[1], std[2]);
   return check_launch("frame_preproc");
 }
 
