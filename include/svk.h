@@ -174,6 +174,11 @@ int svk_flow_preproc(const float* flow, float* out, const int* xofs, const float
                      const float* yalpha, int B, int H, int W, int crop_y0, int crop_x0, int CH, int CW,
                      float scale_u, float scale_v, void* stream);
 
+/* Phase-anticipation targets (generate_phase_anticipation.py:10-34, generate_anticipation_gt): phases
+ * [P, T] int64 one-hot presence (row stride ldp), horizon in minutes -> out [T, P] f32; per phase a
+ * backward recurrence count = present ? 0 : min(horizon, count + 1/1500) in double, out = f32(count) / f32(horizon). */
+int svk_anticipation_gt(const long long* phases, long ldp, int P, int T, double horizon, float* out, void* stream);
+
 /* Causal window unfold (adapter_transformer.py:336-343 as pad + unfold):
  * Y[t, i, c] = X[t - len + 1 + i, c] (0 if negative) + pos[i, c] (pos may be NULL). */
 int svk_window_unfold(int dtype, const void* X, long ldx, const float* pos, void* Y, int T, int C,
