@@ -5,7 +5,8 @@ extraction (generate_evp_LFB.py's hot loop) — frames/s at 224x224 with optical
 return_features=True ([B, 2048]).  One step = one forward of a B-frame batch (default B = 256)
 whose frames, segmaps and flow are already resident in HBM.  Other workloads (``--workload``):
 ``mstcn`` (config 3: MultiStageModel_S(4,10,64,256) over 40 full-length videos), ``mamba``
-(config 3 as tecno.py instantiates it at HEAD: CausalMambaModel, the selective-scan path), ``e2e``
+(config 3 as tecno.py instantiates it at HEAD: CausalMambaModel, the selective-scan path), ``preproc``
+(generate_evp_LFB.py's eval transform on decoded 480x854 uint8 frames, Pillow-exact), ``e2e``
 (config 5: SegFormer -> MS-TCN(2,8,32,2048) -> Transformer(len 30) on 256-frame chunks) and
 ``train`` (configs 2/4: the train_evp.py stage-1 step, B = 88 per GPU, DDP over RCCL when N > 1).
 
