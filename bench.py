@@ -22,6 +22,8 @@ reference's op graph restated on torch CPU ops, fp32) on a bounded sample, rank 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,7 +35,11 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "deep-learning-for-surgical-video-analysis_amd"))
 
 METRIC = json.load(open(os.path.join(REPO, "BASELINE.json")))["metric"]
-PEAK_TFLOPS = {"bf16": 2500.0, "fp32": 157.3}     # MI355X dense MFMA (MI355X_MICROARCH.md)
+PEAK_TFLOPS = {"bf16": 2500.0, "fp16": 2500.0, "fp32": 157.3}     # MI355X dense MFMA (MI355X_MICROARCH.md)
+TORCH_DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32}
+# algorithmic work of one extraction frame: the reference formulation of MiT-b2 + flow
+# minus the dead head work that the exact resize-first rewrite removes (10.77 - 1.08)
+EXTRACT_GFLOP_PER_FRAME = 9.69
 HBM_PEAK_GBS = 8000.0                              # MI355X HBM3E
 DATA = "synthetic (seeded Cholec80-shaped frames/segmaps/flow, resident in HBM; random-init weights)"
 
@@ -53,14 +59,24 @@ def synthetic_batch(B, dev, seed):
     return x.contiguous(), y.contiguous(), flow
 
 
+def _profile_json(name):
+    """Newest committed profiles/rNN/<name> (this round's collection first)."""
+    base = os.path.join(REPO, "profiles")
+    for r in sorted((d for d in os.listdir(base) if d.startswith("r")), reverse=True) if os.path.isdir(base) else []:
+        path = os.path.join(base, r, name)
+        if os.path.exists(path):
+            return path
+    return None
+
+
 def pmc_traffic(workload, kernel):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes of this workload
     (FETCH_SIZE / WRITE_SIZE in separate passes, gfx950 FETCH correction; tools/pmc_traffic.py)."""
-    path = os.path.join(REPO, "profiles", "r01", "pmc_traffic.json")
+    path = _profile_json("pmc_traffic.json")
     try:
         with open(path) as f:
             table = json.load(f)[workload]["kernels"]
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError, KeyError, TypeError):
         return None, None
     src = os.path.relpath(path, REPO)
     if kernel in table:
@@ -72,6 +88,18 @@ def pmc_traffic(workload, kernel):
     if not n:
         return None, None
     return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in ents) / n), src + " (all instantiations)"
+
+
+def pmc_mfma_busy(workload, dtype):
+    """Whole-step MFMA busy fraction from the committed rocprofv3 counter pass (tools/pmc_mfma.py):
+    sum of SQ_VALU_MFMA_BUSY_CYCLES over the step's kernels / (SIMDs x the step's GPU-active cycles)."""
+    path = _profile_json("pmc_mfma.json")
+    try:
+        with open(path) as f:
+            rec = json.load(f)[f"{workload}_{dtype}"]
+    except (OSError, ValueError, KeyError, TypeError):
+        return None
+    return dict(rec, source=os.path.relpath(path, REPO))
 
 
 def video_lengths(n=40, seed=0):
@@ -141,6 +169,11 @@ def workload_extract(args, dev, rank, dtype):
 
     def step():
         return model(x, y, fl, return_features=True)
+
+    def set_dtype(dt):
+        model.svk_dtype = dt
+
+    step.set_dtype = set_dtype
 
     def check(out):
         assert out.shape == (args.batch, 2048) and torch.isfinite(out).all()
@@ -294,10 +327,7 @@ def workload_train(args, dev, rank, dtype):
         return tr.step(x, y, fl, lab, at)[0]
 
     def eager():
-        loss, _, _ = tr.forward_backward(x, y, fl, lab, at)
-        tr.allreduce_grads()
-        tr.optimizer_step()
-        return loss
+        return tr.train_iteration(x, y, fl, lab, at)[0]
 
     step.profile = eager
 
@@ -314,27 +344,114 @@ def workload_train(args, dev, rank, dtype):
 WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": workload_mamba, "preproc": workload_preproc, "e2e": workload_e2e, "train": workload_train}
 
 
-def main():
+def launch_ranks(args):
+    """``--gpus N`` without a torchrun environment: start N ranks under torch.distributed.run (one
+    process per GPU, rendezvous on 127.0.0.1) as a CHILD process and return its exit code.  Nothing here
+    touches the GPU (device_count only counts devices).  Mismatches fail loudly instead of silently
+    measuring one rank."""
+    world_env = os.environ.get("WORLD_SIZE")
+    # the "plumbing" workload (launcher test, gloo on CPU) runs without GPUs
+    visible = args.gpus if args.workload == "plumbing" else torch.cuda.device_count()
+    if world_env is not None:
+        if int(world_env) != args.gpus:
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+        if int(os.environ.get("LOCAL_WORLD_SIZE", world_env)) > visible:
+            sys.exit(f"bench.py: {world_env} ranks on this node but only {visible} visible GPU(s)")
+        return None
+    if args.gpus > visible:
+        sys.exit(f"bench.py: --gpus {args.gpus} but only {visible} visible GPU(s)")
+    if args.gpus <= 1:
+        return None
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def plumbing(world, rank, local):
+    """Launcher self-test (no GPU): every rank reports (rank, local rank, world) over gloo and rank 0
+    prints them with the timing barrier's max-over-ranks reduction exercised on CPU tensors."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    me = torch.tensor([rank, local, world], dtype=torch.int64)
+    got = [torch.zeros(3, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(got, me)
+        dist.barrier()
+    else:
+        got = [me]
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"workload": "plumbing", "n_gpus": world, "ranks": [g.tolist() for g in got],
+                          "max_over_ranks": t.item()}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="extract", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="extract", choices=sorted(WORKLOADS) + ["plumbing"])
     ap.add_argument("--batch", type=int, default=None, help="frames per GPU per step (256; train: 88)")
     ap.add_argument("--variant", default="mit_b2_evp")
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--dtype", default=None, choices=sorted(TORCH_DT),
+                    help="compute dtype (extract / e2e default fp16 = the reference's autocast precision; "
+                         "train default bf16 = BASELINE config 2)")
+    ap.add_argument("--other-dtypes", default=None,
+                    help="comma list of extra dtypes timed on the same inputs and reported as other_dtypes "
+                         "(extract default: bf16,fp32; 'none' to skip)")
     ap.add_argument("--no-flow", action="store_true")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-gemm", default=None, help="write per-shape GEMM timings to this file (rank 0)")
     ap.add_argument("--no-graph", action="store_true", help="train: launch kernels eagerly instead of a HIP graph")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = 88 if args.workload == "train" else 256      # train_evp.py:28 / extraction chunk
+    if args.dtype is None:
+        args.dtype = "bf16" if args.workload == "train" else "fp16"
+    if args.other_dtypes is None:
+        args.other_dtypes = "bf16,fp32" if args.workload == "extract" else "none"
+    return args
+
+
+def timed(step, steps, world):
+    """Barrier + synchronize on both sides of exactly ``steps`` steps; max over ranks."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    return out, float(dt.item())
+
+
+def main():
+    args = parse_args()
+    rc = launch_ranks(args)
+    if rc is not None:
+        sys.exit(rc)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload == "plumbing":
+        return plumbing(world, rank, local)
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
@@ -343,26 +460,15 @@ def main():
     import svk
     from svk import ops
 
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = TORCH_DT[args.dtype]
     step, units, config, check, cpu_fn = WORKLOADS[args.workload](args, dev, rank, dtype)
 
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
         records = []
         ops.set_profiler(records)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            out = step()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
+        out, elapsed = timed(step, args.steps, world)
         prof_steps = args.steps
         if not records and hasattr(step, "profile"):
             # graph-replayed steps make no host calls: time the kernels on eager iterations of the same
@@ -372,12 +478,21 @@ def main():
                 step.profile()
             torch.cuda.synchronize()
         ops.set_profiler(None)
-    check(out)
-
-    dt = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
-    elapsed = float(dt.item())
+        check(out)
+        # the same inputs at the other compute dtypes (extraction): fp32 is the precision of the
+        # reference's generate_evp_LFB.py, bf16 the narrower 16-bit format
+        other = {}
+        if hasattr(step, "set_dtype") and args.other_dtypes != "none":
+            for name in [d for d in args.other_dtypes.split(",") if d and d != args.dtype]:
+                step.set_dtype(TORCH_DT[name])
+                for _ in range(2):
+                    step()
+                o2, el2 = timed(step, max(2, args.steps // 2), world)
+                check(o2)
+                n2 = max(2, args.steps // 2)
+                other[name] = {"value": round(world * units * n2 / el2, 2), "ms_per_step": round(el2 * 1e3 / n2, 3),
+                               "steps": n2}
+            step.set_dtype(dtype)
     value = world * units * args.steps / elapsed
 
     # dominant kernel: the GEMM instantiation with the most measured device time
@@ -398,7 +513,8 @@ def main():
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
     f32_only = args.workload in ("mstcn", "mamba", "preproc")
-    peak = PEAK_TFLOPS["fp32" if f32_only else args.dtype]
+    dtype_name = "fp32" if f32_only else args.dtype
+    peak = PEAK_TFLOPS[dtype_name]
     # bound by arithmetic intensity vs the machine balance (peak FLOP/s / 8 TB/s): tall-skinny
     # token GEMMs (K or N <= 128) are HBM-bound, the head / 4096-wide GEMMs MFMA-bound
     intensity = flops / max(nbytes, 1)
@@ -416,6 +532,13 @@ def main():
                 "kernel_tflops": round(tflops, 2), "kernel_gbs": round(gbs, 1),
                 "all_gemm_tflops": round(sum(v[1] for v in per.values()) / (gemm_ms * 1e-3) / 1e12, 2),
                 "gemm_share_of_step": round(gemm_ms / prof_steps / (elapsed * 1e3 / args.steps), 3)}
+    if args.workload == "extract":
+        # whole-step MFMA utilisation: measured frames/s x algorithmic work / dense peak
+        roofline["step_mfma_util"] = round(value / world * EXTRACT_GFLOP_PER_FRAME * 1e9 / (peak * 1e12), 4)
+        roofline["step_gflop_per_frame"] = EXTRACT_GFLOP_PER_FRAME
+    busy = pmc_mfma_busy(args.workload, args.dtype)
+    if busy is not None:
+        roofline["mfma_busy_counters"] = busy
     traffic, src = pmc_traffic(args.workload, name)
     if traffic is not None:
         roofline["traffic"] = traffic
@@ -423,7 +546,8 @@ def main():
 
     if rank == 0:
         cpu = cpu_fn() if (world == 1 and not args.no_cpu_baseline) else None
-        par = (f"dp{world} (DDP: one RCCL all-reduce of the flat f32 gradient per step)" if args.workload == "train"
+        par = (f"dp{world} (DDP: RCCL all-reduce of the f32 gradient in two buckets, the head bucket overlapped "
+               f"with the backbone backward)" if args.workload == "train"
                else f"dp{world} (shards of independent units, no collective)")
         config.update({"global_units_per_step": world * units, "parallelism": par})
         if args.workload == "train":
@@ -433,8 +557,10 @@ def main():
                 "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-                "dtype": "fp32" if f32_only else args.dtype, "data": DATA, "config": config,
+                "dtype": dtype_name, "data": DATA, "config": config,
                 "roofline": roofline, "cpu_baseline": cpu, "svk": svk.version()}
+        if other:
+            line["other_dtypes"] = other
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

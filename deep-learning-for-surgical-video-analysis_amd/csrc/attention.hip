@@ -79,7 +79,7 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ Q,
 }
 
 // ---------------------------------------------------------------------------------------------
-// bf16 MFMA attention (v_mfma_f32_16x16x32_bf16).  Workgroup = 4 waves = 64 queries of one
+// 16-bit MFMA attention (v_mfma_f32_16x16x32_bf16 / _f16; T = bf16 or f16, f32 softmax state).  Workgroup = 4 waves = 64 queries of one
 // (batch, head); each wave owns 16 queries.  Keys are processed in chunks of 64 staged in LDS
 // (K row-major, V transposed), with an online softmax across chunks (one chunk for MiT's 49
 // reduced keys).
@@ -90,42 +90,43 @@ __global__ __launch_bounds__(256) void attention_kernel(const T* __restrict__ Q,
 // (across g), and the exponentiated scores feed the P.V MFMA as its A operand without leaving
 // registers: for k-step s the 8 elements of lane group g are keys {32s+4g+j} ++ {32s+16+4g+j}
 // (j < 4), a permutation of the 32 keys that the V fragment read from LDS follows exactly.
-template <int HDP>
-__global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restrict__ Q, long ldq, long sbq,
-                                                           const bf16* __restrict__ K, long ldk, long sbk,
-                                                           const bf16* __restrict__ V, long ldv, long sbv,
-                                                           bf16* __restrict__ O, long ldo, long sbo,
+template <typename T, int HDP>
+__global__ __launch_bounds__(256) void attention_mfma_bf16(const T* __restrict__ Q, long ldq, long sbq,
+                                                           const T* __restrict__ K, long ldk, long sbk,
+                                                           const T* __restrict__ V, long ldv, long sbv,
+                                                           T* __restrict__ O, long ldo, long sbo,
                                                            int Nq, int Nk, int hd, float scale_log2) {
   constexpr int KC = 64;
   constexpr int KLD = HDP + 8;   // sK row stride (elements)
   constexpr int VLD = KC + 8;    // sVt row stride (elements)
   constexpr int NKS = HDP / 32;  // k-steps over the head dim
   constexpr int NDT = HDP / 16;  // 16-wide output column tiles
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) bf16 sK[KC][KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sVt[HDP][VLD];
+  typedef v8_t<T> tx8;
+  typedef v4_t<T> tx4;
+  __shared__ __attribute__((aligned(16))) T sK[KC][KLD];
+  __shared__ __attribute__((aligned(16))) T sVt[HDP][VLD];
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const int q0 = blockIdx.x * 64 + wave * 16;
-  const bf16* Qb = Q + (long)b * sbq + (long)h * hd;
-  const bf16* Kb = K + (long)b * sbk + (long)h * hd;
-  const bf16* Vb = V + (long)b * sbv + (long)h * hd;
+  const T* Qb = Q + (long)b * sbq + (long)h * hd;
+  const T* Kb = K + (long)b * sbk + (long)h * hd;
+  const T* Vb = V + (long)b * sbv + (long)h * hd;
   const bool vec = (hd == HDP) && ((ldq | ldk | ldv) % 8 == 0) &&
                    ((((uintptr_t)Qb) | ((uintptr_t)Kb) | ((uintptr_t)Vb)) & 15) == 0;
 
-  bf16x8 qf[NKS];
+  tx8 qf[NKS];
   {
     const int qr = q0 + c;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
       const int d0 = 32 * ks + 8 * g;
       if (qr < Nq && vec) {
-        qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * ldq + d0);
+        qf[ks] = *reinterpret_cast<const tx8*>(Qb + (long)qr * ldq + d0);
       } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) qf[ks][j] = (qr < Nq && d0 + j < hd) ? Qb[(long)qr * ldq + d0 + j] : (bf16)0.f;
+        for (int j = 0; j < 8; ++j) qf[ks][j] = (qr < Nq && d0 + j < hd) ? Qb[(long)qr * ldq + d0 + j] : (T)0.f;
       }
     }
   }
@@ -140,19 +141,19 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restric
     for (int e = tid; e < KC * (HDP / 8); e += 256) {
       const int key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
       const int kg = kc0 + key;
-      bf16x8 kv, vv;
+      tx8 kv, vv;
       if (kg < Nk && vec) {
-        kv = *reinterpret_cast<const bf16x8*>(Kb + (long)kg * ldk + d0);
-        vv = *reinterpret_cast<const bf16x8*>(Vb + (long)kg * ldv + d0);
+        kv = *reinterpret_cast<const tx8*>(Kb + (long)kg * ldk + d0);
+        vv = *reinterpret_cast<const tx8*>(Vb + (long)kg * ldv + d0);
       } else {
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const bool ok = kg < Nk && d0 + j < hd;
-          kv[j] = ok ? Kb[(long)kg * ldk + d0 + j] : (bf16)0.f;
-          vv[j] = ok ? Vb[(long)kg * ldv + d0 + j] : (bf16)0.f;
+          kv[j] = ok ? Kb[(long)kg * ldk + d0 + j] : (T)0.f;
+          vv[j] = ok ? Vb[(long)kg * ldv + d0 + j] : (T)0.f;
         }
       }
-      *reinterpret_cast<bf16x8*>(&sK[key][d0]) = kv;
+      *reinterpret_cast<tx8*>(&sK[key][d0]) = kv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[j];
     }
@@ -164,8 +165,8 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restric
       s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sK[16 * t + c][32 * ks + 8 * g]);
-        s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], s[t], 0, 0, 0);
+        const tx8 a = *reinterpret_cast<const tx8*>(&sK[16 * t + c][32 * ks + 8 * g]);
+        s[t] = mfma16x16x32(a, qf[ks], s[t]);
       }
     }
     float mx = -INFINITY;
@@ -205,25 +206,25 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restric
     }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
-      bf16x8 pa;
+      tx8 pa;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        pa[j] = (bf16)s[2 * s2][j];
-        pa[4 + j] = (bf16)s[2 * s2 + 1][j];
+        pa[j] = (T)s[2 * s2][j];
+        pa[4 + j] = (T)s[2 * s2 + 1][j];
       }
 #pragma unroll
       for (int dt = 0; dt < NDT; ++dt) {
-        const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][32 * s2 + 4 * g]);
-        const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][32 * s2 + 16 + 4 * g]);
-        bf16x8 vb;
+        const tx4 v0 = *reinterpret_cast<const tx4*>(&sVt[16 * dt + c][32 * s2 + 4 * g]);
+        const tx4 v1 = *reinterpret_cast<const tx4*>(&sVt[16 * dt + c][32 * s2 + 16 + 4 * g]);
+        tx8 vb;
 #pragma unroll
         for (int j = 0; j < 4; ++j) { vb[j] = v0[j]; vb[4 + j] = v1[j]; }
-        o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+        o[dt] = mfma16x16x32(pa, vb, o[dt]);
       }
     }
   }
 
-  bf16* Ob = O + (long)b * sbo + (long)h * hd;
+  T* Ob = O + (long)b * sbo + (long)h * hd;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int qr = q0 + 4 * g + r;
@@ -232,7 +233,7 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restric
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) {
       const int d = 16 * dt + c;
-      if (d < hd) Ob[(long)qr * ldo + d] = (bf16)(o[dt][r] * inv);
+      if (d < hd) Ob[(long)qr * ldo + d] = (T)(o[dt][r] * inv);
     }
   }
 }
@@ -244,11 +245,11 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const bf16* __restric
 // computed chunk by chunk exactly as in attention_mfma_bf16.  The output tile goes through a
 // per-wave LDS patch and leaves as 16-byte row pieces (one head row = hd * 2 bytes) instead of
 // 2-byte scattered stores.
-template <int HDP, int NKC>
-__global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __restrict__ Q, long ldq, long sbq,
-                                                               const bf16* __restrict__ K, long ldk, long sbk,
-                                                               const bf16* __restrict__ V, long ldv, long sbv,
-                                                               bf16* __restrict__ O, long ldo, long sbo, int Nq,
+template <typename T, int HDP, int NKC>
+__global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restrict__ Q, long ldq, long sbq,
+                                                               const T* __restrict__ K, long ldk, long sbk,
+                                                               const T* __restrict__ V, long ldv, long sbv,
+                                                               T* __restrict__ O, long ldo, long sbo, int Nq,
                                                                int Nk, int hd, float scale_log2) {
   constexpr int KC = 64, NKP = NKC * KC;
   constexpr int KLD = HDP + 8;    // sK row stride (elements)
@@ -256,32 +257,33 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __res
   constexpr int OLD = HDP + 8;    // per-wave output patch row stride
   constexpr int NKS = HDP / 32, NDT = HDP / 16;
   constexpr int QB = 256;
-  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) bf16 sK[NKP][KLD];
-  __shared__ __attribute__((aligned(16))) bf16 sVt[HDP][VLD];
-  __shared__ __attribute__((aligned(16))) bf16 sO[4][16][OLD];
+  typedef v8_t<T> tx8;
+  typedef v4_t<T> tx4;
+  __shared__ __attribute__((aligned(16))) T sK[NKP][KLD];
+  __shared__ __attribute__((aligned(16))) T sVt[HDP][VLD];
+  __shared__ __attribute__((aligned(16))) T sO[4][16][OLD];
 
   const int b = blockIdx.z, h = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
-  const bf16* Qb = Q + (long)b * sbq + (long)h * hd;
-  const bf16* Kb = K + (long)b * sbk + (long)h * hd;
-  const bf16* Vb = V + (long)b * sbv + (long)h * hd;
-  bf16* Ob = O + (long)b * sbo + (long)h * hd;
-  const bf16 zero = (bf16)0.f;
+  const T* Qb = Q + (long)b * sbq + (long)h * hd;
+  const T* Kb = K + (long)b * sbk + (long)h * hd;
+  const T* Vb = V + (long)b * sbv + (long)h * hd;
+  T* Ob = O + (long)b * sbo + (long)h * hd;
+  const T zero = (T)0.f;
 
   // stage K [key][d] and V^T [d][key] for all keys (zeros past Nk / hd)
   for (int e = tid; e < NKP * (HDP / 8); e += 256) {
     const int key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
-    bf16x8 kv, vv;
+    tx8 kv, vv;
     if (key < Nk && d0 < hd) {
-      kv = *reinterpret_cast<const bf16x8*>(Kb + (long)key * ldk + d0);
-      vv = *reinterpret_cast<const bf16x8*>(Vb + (long)key * ldv + d0);
+      kv = *reinterpret_cast<const tx8*>(Kb + (long)key * ldk + d0);
+      vv = *reinterpret_cast<const tx8*>(Vb + (long)key * ldv + d0);
     } else {
 #pragma unroll
       for (int j = 0; j < 8; ++j) { kv[j] = zero; vv[j] = zero; }
     }
-    *reinterpret_cast<bf16x8*>(&sK[key][d0]) = kv;
+    *reinterpret_cast<tx8*>(&sK[key][d0]) = kv;
 #pragma unroll
     for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[j];
   }
@@ -291,14 +293,14 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __res
   for (int qt = wave; qt < QB / 16; qt += 4) {
     const int q0 = qbase + qt * 16;
     if (q0 >= Nq) break;
-    bf16x8 qf[NKS];
+    tx8 qf[NKS];
     {
       const int qr = q0 + c;
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const int d0 = 32 * ks + 8 * g;
         if (qr < Nq && d0 < hd) {
-          qf[ks] = *reinterpret_cast<const bf16x8*>(Qb + (long)qr * ldq + d0);
+          qf[ks] = *reinterpret_cast<const tx8*>(Qb + (long)qr * ldq + d0);
         } else {
 #pragma unroll
           for (int j = 0; j < 8; ++j) qf[ks][j] = zero;
@@ -318,8 +320,8 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __res
         s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sK[kc0 + 16 * t + c][32 * ks + 8 * g]);
-          s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, qf[ks], s[t], 0, 0, 0);
+          const tx8 a = *reinterpret_cast<const tx8*>(&sK[kc0 + 16 * t + c][32 * ks + 8 * g]);
+          s[t] = mfma16x16x32(a, qf[ks], s[t]);
         }
       }
       float mx = -INFINITY;
@@ -359,20 +361,20 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __res
       }
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
-        bf16x8 pa;
+        tx8 pa;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          pa[j] = (bf16)s[2 * s2][j];
-          pa[4 + j] = (bf16)s[2 * s2 + 1][j];
+          pa[j] = (T)s[2 * s2][j];
+          pa[4 + j] = (T)s[2 * s2 + 1][j];
         }
 #pragma unroll
         for (int dt = 0; dt < NDT; ++dt) {
-          const bf16x4 v0 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 4 * g]);
-          const bf16x4 v1 = *reinterpret_cast<const bf16x4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 16 + 4 * g]);
-          bf16x8 vb;
+          const tx4 v0 = *reinterpret_cast<const tx4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 4 * g]);
+          const tx4 v1 = *reinterpret_cast<const tx4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 16 + 4 * g]);
+          tx8 vb;
 #pragma unroll
           for (int j = 0; j < 4; ++j) { vb[j] = v0[j]; vb[4 + j] = v1[j]; }
-          o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[dt], 0, 0, 0);
+          o[dt] = mfma16x16x32(pa, vb, o[dt]);
         }
       }
     }
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const bf16* __res
     for (int r = 0; r < 4; ++r) {
       const float inv = 1.0f / __shfl(l_run, 4 * g + r, 64);
 #pragma unroll
-      for (int dt = 0; dt < NDT; ++dt) sO[wave][4 * g + r][16 * dt + c] = (bf16)(o[dt][r] * inv);
+      for (int dt = 0; dt < NDT; ++dt) sO[wave][4 * g + r][16 * dt + c] = (T)(o[dt][r] * inv);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -411,37 +413,39 @@ extern "C" int svk_attention(int dtype, const void* Q, long ldq, long sbq, const
   if (B > 65535 || heads > 65535) { set_error("svk_attention: grid too large"); return SVK_EUNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((Nq + 63) / 64, heads, B), block(256);
-  if (dtype == SVK_BF16) {
+  if (dtype == SVK_BF16 || dtype == SVK_F16) {
     const float sl2 = scale * 1.4426950408889634f;   // softmax via exp2
     const bool res_ok = hd % 8 == 0 && ((ldq | ldk | ldv | ldo | sbq | sbk | sbv | sbo) % 8) == 0 &&
                         ((((uintptr_t)Q) | ((uintptr_t)K) | ((uintptr_t)V) | ((uintptr_t)O)) & 15) == 0;
-    if (res_ok) {
-      const int nkc = (Nk + 63) / 64;
-      dim3 rgrid((Nq + 255) / 256, heads, B);
-      auto go = [&](auto hdp_c, auto nkc_c) {
-        constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
-        hipLaunchKernelGGL((attention_mfma_bf16_res<HDP, NKC>), rgrid, block, 0, st, (const bf16*)Q, ldq, sbq,
-                           (const bf16*)K, ldk, sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);
-      };
-      auto by_nkc = [&](auto hdp) {
-        switch (nkc) {
-          case 1: go(hdp, std::integral_constant<int, 1>{}); break;
-          case 2: go(hdp, std::integral_constant<int, 2>{}); break;
-          case 3: go(hdp, std::integral_constant<int, 3>{}); break;
-          default: go(hdp, std::integral_constant<int, 4>{}); break;
-        }
-      };
-      if (hd <= 32) by_nkc(std::integral_constant<int, 32>{});
-      else by_nkc(std::integral_constant<int, 64>{});
-      return check_launch("attention_mfma_bf16_res");
-    }
-    if (hd <= 32)
-      hipLaunchKernelGGL((attention_mfma_bf16<32>), grid, block, 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K, ldk,
-                         sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);
-    else
-      hipLaunchKernelGGL((attention_mfma_bf16<64>), grid, block, 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K, ldk,
-                         sbk, (const bf16*)V, ldv, sbv, (bf16*)O, ldo, sbo, Nq, Nk, hd, sl2);
-    return check_launch("attention_mfma_bf16");
+    SVK_DISPATCH_H16(dtype, T, {
+      if (res_ok) {
+        const int nkc = (Nk + 63) / 64;
+        dim3 rgrid((Nq + 255) / 256, heads, B);
+        auto go = [&](auto hdp_c, auto nkc_c) {
+          constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
+          hipLaunchKernelGGL((attention_mfma_bf16_res<T, HDP, NKC>), rgrid, block, 0, st, (const T*)Q, ldq, sbq,
+                             (const T*)K, ldk, sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
+        };
+        auto by_nkc = [&](auto hdp) {
+          switch (nkc) {
+            case 1: go(hdp, std::integral_constant<int, 1>{}); break;
+            case 2: go(hdp, std::integral_constant<int, 2>{}); break;
+            case 3: go(hdp, std::integral_constant<int, 3>{}); break;
+            default: go(hdp, std::integral_constant<int, 4>{}); break;
+          }
+        };
+        if (hd <= 32) by_nkc(std::integral_constant<int, 32>{});
+        else by_nkc(std::integral_constant<int, 64>{});
+        return check_launch("attention_mfma_bf16_res");
+      }
+      if (hd <= 32)
+        hipLaunchKernelGGL((attention_mfma_bf16<T, 32>), grid, block, 0, st, (const T*)Q, ldq, sbq, (const T*)K, ldk,
+                           sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
+      else
+        hipLaunchKernelGGL((attention_mfma_bf16<T, 64>), grid, block, 0, st, (const T*)Q, ldq, sbq, (const T*)K, ldk,
+                           sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
+      return check_launch("attention_mfma_bf16");
+    });
   }
   SVK_DISPATCH_DTYPE(dtype, T, {
     const size_t sm = (size_t)2 * Nk * hd * sizeof(float);

@@ -177,9 +177,7 @@ __device__ __forceinline__ unsigned load_col2im(const T* X, const GemmArgs& p, c
 template <typename T>
 __device__ __forceinline__ void mfma_step(const Chunk<T>& a, const Chunk<T>& b, f32x4& acc) {
   if constexpr (sizeof(T) == 2) {
-    bf16x8 av = *reinterpret_cast<const bf16x8*>(a.v);
-    bf16x8 bv = *reinterpret_cast<const bf16x8*>(b.v);
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+    acc = mfma16x16x32(*reinterpret_cast<const v8_t<T>*>(a.v), *reinterpret_cast<const v8_t<T>*>(b.v), acc);
   } else {
 #pragma unroll
     for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], acc, 0, 0, 0);
@@ -461,7 +459,7 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
               (!a.U || (aligned16(a.U) && a.ldu % vw == 0)) && (a.out_mode == 0 || a.uC % 8 == 0);
   const bool ext = a.rscale || a.U || a.out_mode;
   if constexpr (sizeof(T) == 2 && ASRC <= 1) {
-    if (vec && gemm_pk_try(a, st, ASRC) == 0) return SVK_OK;
+    if (vec && gemm_pk_try<T>(a, st, ASRC) == 0) return SVK_OK;
   }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;
@@ -470,7 +468,7 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
     static char names[2][2][96];
     char* nm = names[vec][ext];
     if (!nm[0])
-      snprintf(nm, 96, "gemm_kernel<%s, %d, %d, %s, %d, %s>", sizeof(T) == 2 ? "__bf16" : "float", BM, BN,
+      snprintf(nm, 96, "gemm_kernel<%s, %d, %d, %s, %d, %s>", type_name<T>(), BM, BN,
                vec ? "true" : "false", ASRC, ext ? "true" : "false");
     set_last_kernel(nm);
     if (ext) {
@@ -728,7 +726,7 @@ extern "C" int svk_conv2d_nhwc(int dtype, const void* X, int B, int H, int W, in
 static int conv_ln_ksplit(int dtype, long M, int N, int K, int Cin) {
   // measured (B = 256): splitting pays for the N <= 128 stages (64 x 64 tiles, 196 / 392 of them);
   // at N = 320 (490 128 x 64 tiles) the extra slab pass costs more than the occupancy gains
-  if (dtype != SVK_BF16 || K % 64 || Cin % 8 || N % 4 || N > 128) return 1;
+  if ((dtype != SVK_BF16 && dtype != SVK_F16) || K % 64 || Cin % 8 || N % 4 || N > 128) return 1;
   const int nk = K / 64;
   const long tiles = ((M + 63) / 64) * ((N + 63) / 64);
   int ks = 1;
@@ -765,11 +763,13 @@ extern "C" int svk_conv2d_ln_nhwc(int dtype, const void* X, int B, int H, int W,
     a.M = (int)M; a.N = Cout; a.K = k * k * Cin;
     a.H = H; a.Wd = W; a.Cin = Cin; a.OH = OH; a.OW = OW; a.kw = k; a.stride = stride; a.pad = pad;
     a.ksplit = ks; a.slab = static_cast<float*>(ws);
-    if (gemm_pk_conv_splitk(a, st) == 0) {
-      int rc = check_launch("conv2d_ln splitk");
-      if (rc) return rc;
-      return splitk_layernorm(a.slab, ks, bias, static_cast<bf16*>(Y), (int)M, Cout, gamma, beta, eps, st);
-    }
+    SVK_DISPATCH_H16(dtype, T, {
+      if (gemm_pk_conv_splitk<T>(a, st) == 0) {
+        int rc = check_launch("conv2d_ln splitk");
+        if (rc) return rc;
+        return splitk_layernorm<T>(a.slab, ks, bias, static_cast<T*>(Y), (int)M, Cout, gamma, beta, eps, st);
+      }
+    });
   }
   int rc = svk_conv2d_nhwc(dtype, X, B, H, W, Cin, Wt, bias, nullptr, Y, Cout, k, stride, pad, SVK_ACT_NONE, stream);
   if (rc) return rc;

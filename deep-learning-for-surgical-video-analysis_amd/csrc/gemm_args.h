@@ -27,9 +27,10 @@ struct GemmArgs {
   int ksplit; float* slab;
 };
 
-// gemm_pk.hip: persistent LDS-DMA bf16 GEMM / implicit-GEMM conv (asrc 1) for the plain-epilogue
+// gemm_pk.hip: persistent LDS-DMA bf16 / f16 GEMM / implicit-GEMM conv (asrc 1) for the plain-epilogue
 // case; returns 0 when it launched, 1 when the arguments are not eligible (caller falls back to gemm_kernel).
-int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
-int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
+// T = __bf16 or _Float16 (instantiated in gemm_pk.hip).
+template <typename T> int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
+template <typename T> int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
 
 }  // namespace svk

@@ -1,6 +1,6 @@
-// Persistent, LDS-DMA-pipelined bf16 MFMA GEMM for the token GEMMs of the MiT/SegFormer path.
+// Persistent, LDS-DMA-pipelined bf16 / f16 MFMA GEMM for the token GEMMs of the MiT/SegFormer path.
 //
-//   C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]        (bf16 in/out, f32 accumulate)
+//   C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]        (bf16 or f16 in/out, f32 accumulate)
 //
 // Why persistent: most of the path's GEMMs have a short reduction (K = 64..512, i.e. 1..8 K-steps of
 // 64), so in a one-tile-per-workgroup kernel every tile pays the full global-load latency of its
@@ -96,8 +96,9 @@ __device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current
 // SPLIT: split-K — unit u = (tile u / ks, K part u % ks) covers nk K-steps of the tile's ks * nk; the
 // epilogue stores raw f32 partial sums to slab part (p.slab + (part * M + m) * N + n) and a separate
 // reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
-template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
-__global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
+template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
+__global__ __launch_bounds__(Cfg::NT) void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
+  typedef v8_t<T> tx8;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
   __shared__ __attribute__((aligned(1024))) char smem[Cfg::LDS];
@@ -105,8 +106,8 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / Cfg::WGN, wn = wave % Cfg::WGN;
-  const bf16* A = static_cast<const bf16*>(p.A);
-  const bf16* Wt = static_cast<const bf16*>(p.W);
+  const T* A = static_cast<const T*>(p.A);
+  const T* Wt = static_cast<const T*>(p.W);
   const int G = gridDim.x;
   const int first = pk_xcd_remap(blockIdx.x, G);
   if (first >= ntiles) return;
@@ -182,15 +183,15 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int cc = ((ks * 4 + fq) ^ (fr & 7)) * 16;   // swizzled chunk of this lane's 8 k
-      bf16x8 fa[TM], fb[TN];
+      tx8 fa[TM], fb[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(sa + (wm * WM + i * 16 + fr) * 128 + cc);
+      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const tx8*>(sa + (wm * WM + i * 16 + fr) * 128 + cc);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
+      for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const tx8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
     }
   };
 
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
   // it across the last step would cost 2 VGPRs per accumulator block and halve the occupancy.
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
   float4 ebias[TN];
-  const bf16* R = static_cast<const bf16*>(p.R);
+  const T* R = static_cast<const T*>(p.R);
   auto epi_load = [&](int unit) {
     const int n0 = ((SPLIT ? unit / ks : unit) % ntn) * BN;
 #pragma unroll
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
       }
       return;
     }
-    bf16* C = static_cast<bf16*>(p.C);
+    T* C = static_cast<T*>(p.C);
     uint2 eres[TM][TN], eu[TM][TN];
     float ers[TM];
     if (R) {
@@ -243,7 +244,7 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
         }
     }
     if constexpr (EXT) {
-      const bf16* U = static_cast<const bf16*>(p.U);
+      const T* U = static_cast<const T*>(p.U);
       if (U) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -270,22 +271,24 @@ __global__ __launch_bounds__(Cfg::NT) void gemm_pk_bf16(GemmArgs p, PkConv cv, i
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], p.act) * ers[i];
           if (p.U) {
-            v[0] *= act_grad(__uint_as_float(eu[i][j].x << 16), ACT);
-            v[1] *= act_grad(__uint_as_float(eu[i][j].x & 0xFFFF0000u), ACT);
-            v[2] *= act_grad(__uint_as_float(eu[i][j].y << 16), ACT);
-            v[3] *= act_grad(__uint_as_float(eu[i][j].y & 0xFFFF0000u), ACT);
+            const f32x2 u01 = unpack2<T>(eu[i][j].x), u23 = unpack2<T>(eu[i][j].y);
+            v[0] *= act_grad(u01.x, ACT);
+            v[1] *= act_grad(u01.y, ACT);
+            v[2] *= act_grad(u23.x, ACT);
+            v[3] *= act_grad(u23.y, ACT);
           }
         } else {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
         }
         if (R) {
-          v[0] += __uint_as_float(eres[i][j].x << 16);
-          v[1] += __uint_as_float(eres[i][j].x & 0xFFFF0000u);
-          v[2] += __uint_as_float(eres[i][j].y << 16);
-          v[3] += __uint_as_float(eres[i][j].y & 0xFFFF0000u);
+          const f32x2 r01 = unpack2<T>(eres[i][j].x), r23 = unpack2<T>(eres[i][j].y);
+          v[0] += r01.x;
+          v[1] += r01.y;
+          v[2] += r23.x;
+          v[3] += r23.y;
         }
-        bf16 o[4] = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+        T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
         if constexpr (ELDS) {
           const int row = wm * WM + i * 16 + fr, col = wn * WN + j * 16 + fq * 4;
           *reinterpret_cast<uint2*>(stile + row * (BN * 2) + (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col >> 2) & 1) * 8) =
@@ -364,14 +367,14 @@ static int pk_slots(const void* fn, int nt) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
+template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
 static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.N + Cfg::BN - 1) / Cfg::BN;
   const int ks = SPLIT ? a.ksplit : 1;
   const long ntiles = (long)ntm * ntn * ks;
   const int nk = (a.K + 63) / 64 / ks;   // K-steps per unit (the caller makes ks divide them)
   static const int slots =
-      pk_slots(reinterpret_cast<const void*>(&gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), Cfg::NT);
+      pk_slots(reinterpret_cast<const void*>(&gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), Cfg::NT);
   const int grid = (int)std::min<long>(ntiles, slots);
   PkConv cv{};
   if (ASRC == 1) {
@@ -380,18 +383,18 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.cin = make_fastdiv((uint32_t)a.Cin);
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
-  hipLaunchKernelGGL((gemm_pk_bf16<Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
+  hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
                      (int)ntiles, nk, ks);
-  static char name[96];
+  static char name[112];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk_bf16<PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", Cfg::BM, Cfg::BN,
+    snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", type_name<T>(), Cfg::BM, Cfg::BN,
              Cfg::WGM, Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC,
              EXT ? "true" : "false", SPLIT ? "true" : "false");   // the demangled instantiation name
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
 
-template <class Cfg, int ASRC>
+template <typename T, class Cfg, int ASRC>
 static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   if (g_tune[TUNE_PK_ELDS] >= 0) elds = g_tune[TUNE_PK_ELDS];
@@ -402,20 +405,21 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
     // the im2col loader zero-fills the A side of a K tail itself, but the weight rows must read the
     // zero block too: the last row's tail would otherwise read past the packed weights, and 0 x a
     // NaN bit pattern found there is NaN.  No extended epilogue for convs.
-    if (elds) return tail ? launch_pk<Cfg, true, true, 1, false>(a, st) : launch_pk<Cfg, false, true, 1, false>(a, st);
-    return tail ? launch_pk<Cfg, true, false, 1, false>(a, st) : launch_pk<Cfg, false, false, 1, false>(a, st);
+    if (elds) return tail ? launch_pk<T, Cfg, true, true, 1, false>(a, st) : launch_pk<T, Cfg, false, true, 1, false>(a, st);
+    return tail ? launch_pk<T, Cfg, true, false, 1, false>(a, st) : launch_pk<T, Cfg, false, false, 1, false>(a, st);
   }
   if (ext) {
-    if (elds) return tail ? launch_pk<Cfg, true, true, 0, true>(a, st) : launch_pk<Cfg, false, true, 0, true>(a, st);
-    return tail ? launch_pk<Cfg, true, false, 0, true>(a, st) : launch_pk<Cfg, false, false, 0, true>(a, st);
+    if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, true>(a, st) : launch_pk<T, Cfg, false, true, 0, true>(a, st);
+    return tail ? launch_pk<T, Cfg, true, false, 0, true>(a, st) : launch_pk<T, Cfg, false, false, 0, true>(a, st);
   }
-  if (elds) return tail ? launch_pk<Cfg, true, true, 0, false>(a, st) : launch_pk<Cfg, false, true, 0, false>(a, st);
-  return tail ? launch_pk<Cfg, true, false, 0, false>(a, st) : launch_pk<Cfg, false, false, 0, false>(a, st);
+  if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, false>(a, st) : launch_pk<T, Cfg, false, true, 0, false>(a, st);
+  return tail ? launch_pk<T, Cfg, true, false, 0, false>(a, st) : launch_pk<T, Cfg, false, false, 0, false>(a, st);
 }
 
 // Eligible: bf16, K-contiguous operands (16-byte aligned rows, K % 8 == 0; conv: Cin % 8 == 0),
 // plain epilogue, C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when
 // not eligible.  asrc: 0 dense A, 1 implicit-GEMM conv (A = NHWC map, GemmArgs conv geometry).
+template <typename T>
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   const int force = g_tune[TUNE_PK_CFG];
   if (getenv("SVK_NO_PK")) return 1;
@@ -447,30 +451,36 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   // cfg: 0 = 128x128, 10 = 128x64, 20 = 64x128, 30 = 64x64
   if (asrc == 1) {
     switch (cfg) {
-      case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 1>(a, st, !big);
-      case 20: return launch_pk_k<PkCfg<64, 128, 2, 2, 2>, 1>(a, st, !big);
-      case 30: return launch_pk_k<PkCfg<64, 64, 2, 2, 2>, 1>(a, st, !big);
-      default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 1>(a, st, !reg_epi);
+      case 10: return launch_pk_k<T, PkCfg<128, 64, 2, 2, 2>, 1>(a, st, !big);
+      case 20: return launch_pk_k<T, PkCfg<64, 128, 2, 2, 2>, 1>(a, st, !big);
+      case 30: return launch_pk_k<T, PkCfg<64, 64, 2, 2, 2>, 1>(a, st, !big);
+      default: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 1>(a, st, !reg_epi);
     }
   }
   switch (cfg) {
-    case 10: return launch_pk_k<PkCfg<128, 64, 2, 2, 2>, 0>(a, st, !big);
-    case 20: return launch_pk_k<PkCfg<64, 128, 2, 2, 2>, 0>(a, st, !big);
-    case 30: return launch_pk_k<PkCfg<64, 64, 2, 2, 2>, 0>(a, st, !big);
-    default: return launch_pk_k<PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
+    case 10: return launch_pk_k<T, PkCfg<128, 64, 2, 2, 2>, 0>(a, st, !big);
+    case 20: return launch_pk_k<T, PkCfg<64, 128, 2, 2, 2>, 0>(a, st, !big);
+    case 30: return launch_pk_k<T, PkCfg<64, 64, 2, 2, 2>, 0>(a, st, !big);
+    default: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
   }
 }
 
 // Split-K implicit-GEMM conv into f32 partial slabs (a.ksplit parts, a.slab [ksplit][M][N]): for the
 // k = s patchify convs of the sequence reduction, whose 98-row-tile grids (B = 256) cannot fill the
 // chip with a long K (2048 / 4096).  Returns 1 when not eligible.
+template <typename T>
 int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st) {
   auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
   if (a.ksplit < 2 || !a.slab || a.K % 64 || ((a.K / 64) % a.ksplit) || a.N % 4 || a.Cin % 8 || !al(a.A, 16) ||
       !al(a.W, 16) || !al(a.slab, 16) || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)
     return 1;
-  if (a.N <= 128) return launch_pk<PkCfg<64, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
-  return launch_pk<PkCfg<128, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
+  if (a.N <= 128) return launch_pk<T, PkCfg<64, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
+  return launch_pk<T, PkCfg<128, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
 }
+
+template int gemm_pk_try<bf16>(const GemmArgs&, hipStream_t, int);
+template int gemm_pk_try<f16>(const GemmArgs&, hipStream_t, int);
+template int gemm_pk_conv_splitk<bf16>(const GemmArgs&, hipStream_t);
+template int gemm_pk_conv_splitk<f16>(const GemmArgs&, hipStream_t);
 
 }  // namespace svk

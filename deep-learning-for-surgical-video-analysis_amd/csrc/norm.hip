@@ -155,11 +155,11 @@ __global__ void mean_rows_kernel(const T* __restrict__ X, long ldx, float* __res
 }
 
 // Split-K reduction + bias + LayerNorm (svk_conv2d_ln_nhwc): Y[m, :] = LN(sum_s S[s][m][:] + bias),
-// bf16 out.  Same lane layout as layernorm_vec_kernel: LPR lanes per row, NCH 8-channel chunks per
+// 16-bit out.  Same lane layout as layernorm_vec_kernel: LPR lanes per row, NCH 8-channel chunks per
 // lane, f32 sums, two-pass mean / variance over the row held in registers.
-template <int LPR, int NCH>
+template <typename T, int LPR, int NCH>
 __global__ __launch_bounds__(256) void splitk_ln_kernel(const float* __restrict__ S, int ks, const float* __restrict__ bias,
-                                                        bf16* __restrict__ Y, const float* __restrict__ g,
+                                                        T* __restrict__ Y, const float* __restrict__ g,
                                                         const float* __restrict__ b, int M, int C, float eps) {
   constexpr int RPW = 64 / LPR;
   const int lane = threadIdx.x & 63, sub = lane % LPR;
@@ -207,21 +207,22 @@ __global__ __launch_bounds__(256) void splitk_ln_kernel(const float* __restrict_
   for (int i = 0; i < NCH; ++i) {
     const int ch = sub + LPR * i;
     if (ch >= nchunks) continue;
-    bf16 t[8];
+    T t[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) t[e] = (bf16)((v[i][e] - mean) * rstd * g[ch * 8 + e] + b[ch * 8 + e]);
+    for (int e = 0; e < 8; ++e) t[e] = (T)((v[i][e] - mean) * rstd * g[ch * 8 + e] + b[ch * 8 + e]);
     *reinterpret_cast<uint4*>(Y + row * C + ch * 8) = *reinterpret_cast<const uint4*>(t);
   }
 }
 
-int splitk_layernorm(const float* S, int ks, const float* bias, bf16* Y, int M, int C, const float* gamma,
+template <typename T>
+int splitk_layernorm(const float* S, int ks, const float* bias, T* Y, int M, int C, const float* gamma,
                      const float* beta, float eps, hipStream_t st) {
   if (C % 8 || C > 4096) { set_error("splitk_layernorm: C %% 8 != 0 or C > 4096"); return SVK_EUNSUPPORTED; }
   const int nch = C / 8;
   auto go = [&](auto lpr_c, auto nch_c) {
     constexpr int LPR = decltype(lpr_c)::value, NCH = decltype(nch_c)::value;
     constexpr int RPB = 4 * (64 / LPR);
-    hipLaunchKernelGGL((splitk_ln_kernel<LPR, NCH>), dim3((M + RPB - 1) / RPB), dim3(256), 0, st, S, ks, bias, Y, gamma,
+    hipLaunchKernelGGL((splitk_ln_kernel<T, LPR, NCH>), dim3((M + RPB - 1) / RPB), dim3(256), 0, st, S, ks, bias, Y, gamma,
                        beta, M, C, eps);
   };
   using I1 = std::integral_constant<int, 1>;
@@ -234,6 +235,10 @@ int splitk_layernorm(const float* S, int ks, const float* bias, bf16* Y, int M, 
   else go(std::integral_constant<int, 64>{}, std::integral_constant<int, 8>{});
   return check_launch("splitk_ln");
 }
+template int splitk_layernorm<bf16>(const float*, int, const float*, bf16*, int, int, const float*, const float*, float,
+                                    hipStream_t);
+template int splitk_layernorm<f16>(const float*, int, const float*, f16*, int, int, const float*, const float*, float,
+                                   hipStream_t);
 
 }  // namespace svk
 

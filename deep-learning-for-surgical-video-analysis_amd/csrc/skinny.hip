@@ -2,7 +2,7 @@
 // whose Linears are 16..128 wide over 69k..276k tokens (B = 88..256): the general 64x64/128x64 tiles
 // leave most of every tile masked and are latency-bound.
 //
-// skinny_gemm: C[M, N] = act(A[M, K] W[N, K]^T + bias) * act'(U) + R, N <= 64, K <= 128, bf16.
+// skinny_gemm: C[M, N] = act(A[M, K] W[N, K]^T + bias) * act'(U) + R, N <= 64, K <= 128, bf16 / f16.
 //   W lives in LDS for the whole workgroup; each wave streams 16-row blocks of A straight from
 //   global memory in the MFMA A-operand layout (lane: row l & 15, 8 consecutive k), so there is no
 //   LDS staging of A at all; the 16 x N tile is written back through a per-wave LDS patch as 16-byte
@@ -15,29 +15,31 @@
 
 namespace svk {
 
+template <typename T>
 struct SkinnyArgs {
-  const bf16* A; long lda;
-  const bf16* W; long ldw;
+  const T* A; long lda;
+  const T* W; long ldw;
   const float* bias;
-  const bf16* U; long ldu; int uact;
-  const bf16* R; long ldr;
-  bf16* C; long ldc;
+  const T* U; long ldu; int uact;
+  const T* R; long ldr;
+  T* C; long ldc;
   int M, N, K, act;
 };
 
-template <int NT, int KS>
-__global__ __launch_bounds__(256) void skinny_gemm(SkinnyArgs p) {
+template <typename T, int NT, int KS>
+__global__ __launch_bounds__(256) void skinny_gemm(SkinnyArgs<T> p) {
+  typedef v8_t<T> tx8;
   constexpr int NP = NT * 16, KP = KS * 32;
   constexpr int LDW = KP + 8;
   constexpr int LDO = NP + 4;
-  __shared__ __attribute__((aligned(16))) bf16 sW[NP][LDW];
+  __shared__ __attribute__((aligned(16))) T sW[NP][LDW];
   __shared__ __attribute__((aligned(16))) float sO[4][16][LDO];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
-  const bf16 z = (bf16)0.f;
+  const T z = (T)0.f;
   for (int i = tid; i < NP * (KP / 8); i += 256) {
     const int n = i / (KP / 8), k8 = (i % (KP / 8)) * 8;
-    bf16x8 v;
+    tx8 v;
     if (n < p.N && k8 < p.K) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = k8 + e < p.K ? p.W[(long)n * p.ldw + k8 + e] : z;
@@ -45,7 +47,7 @@ __global__ __launch_bounds__(256) void skinny_gemm(SkinnyArgs p) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = z;
     }
-    *reinterpret_cast<bf16x8*>(&sW[n][k8]) = v;
+    *reinterpret_cast<tx8*>(&sW[n][k8]) = v;
   }
   __syncthreads();
   const bool kvec = (p.K % 8) == 0;
@@ -54,13 +56,13 @@ __global__ __launch_bounds__(256) void skinny_gemm(SkinnyArgs p) {
     const long m0 = blk * 16;
     const long row = m0 + fr;
     const long rc = row < p.M ? row : p.M - 1;
-    bf16x8 a[KS];
+    tx8 a[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const int k = ks * 32 + fg * 8;
       const int kc = k < p.K ? k : 0;
       if (kvec) {
-        a[ks] = *reinterpret_cast<const bf16x8*>(p.A + rc * p.lda + kc);
+        a[ks] = *reinterpret_cast<const tx8*>(p.A + rc * p.lda + kc);
         if (k >= p.K) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) a[ks][e] = z;
@@ -76,8 +78,8 @@ __global__ __launch_bounds__(256) void skinny_gemm(SkinnyArgs p) {
       acc[nt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 b = *reinterpret_cast<const bf16x8*>(&sW[nt * 16 + fr][ks * 32 + fg * 8]);
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], b, acc[nt], 0, 0, 0);
+        const tx8 b = *reinterpret_cast<const tx8*>(&sW[nt * 16 + fr][ks * 32 + fg * 8]);
+        acc[nt] = mfma16x16x32(a[ks], b, acc[nt]);
       }
     }
     // C layout: col n = nt * 16 + (lane & 15), row = 4 (lane >> 4) + r  ->  per-wave LDS patch
@@ -100,25 +102,25 @@ __global__ __launch_bounds__(256) void skinny_gemm(SkinnyArgs p) {
       for (int e = 0; e < 8; ++e) v[e] = sO[w][r][c8 + e];
       if (c8 + 8 <= p.N && (p.ldc % 8) == 0 && (!p.U || p.ldu % 8 == 0) && (!p.R || p.ldr % 8 == 0)) {
         if (p.U) {
-          const bf16x8 u = *reinterpret_cast<const bf16x8*>(p.U + m * p.ldu + c8);
+          const tx8 u = *reinterpret_cast<const tx8*>(p.U + m * p.ldu + c8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= act_grad((float)u[e], p.uact);
         }
         if (p.R) {
-          const bf16x8 rr = *reinterpret_cast<const bf16x8*>(p.R + m * p.ldr + c8);
+          const tx8 rr = *reinterpret_cast<const tx8*>(p.R + m * p.ldr + c8);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += (float)rr[e];
         }
-        bf16x8 o;
+        tx8 o;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (bf16)v[e];
-        *reinterpret_cast<bf16x8*>(p.C + m * p.ldc + c8) = o;
+        for (int e = 0; e < 8; ++e) o[e] = (T)v[e];
+        *reinterpret_cast<tx8*>(p.C + m * p.ldc + c8) = o;
       } else {
         for (int e = 0; e < 8 && c8 + e < p.N; ++e) {
           float x = v[e];
           if (p.U) x *= act_grad((float)p.U[m * p.ldu + c8 + e], p.uact);
           if (p.R) x += (float)p.R[m * p.ldr + c8 + e];
-          p.C[m * p.ldc + c8 + e] = (bf16)x;
+          p.C[m * p.ldc + c8 + e] = (T)x;
         }
       }
     }
@@ -222,35 +224,37 @@ __global__ __launch_bounds__(256) void skinny_wgrad(SkinnyWgradArgs p) {
 
 using namespace svk;
 
-extern "C" int svk_gemm_skinny(const void* A, long lda, const void* W, long ldw, const float* bias, const void* U,
-                               long ldu, int uact, const void* R, long ldr, void* C, long ldc, int M, int N, int K,
-                               int act, void* stream) {
+extern "C" int svk_gemm_skinny(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias,
+                               const void* U, long ldu, int uact, const void* R, long ldr, void* C, long ldc, int M,
+                               int N, int K, int act, void* stream) {
   if (M < 0 || N <= 0 || N > 64 || K <= 0 || K > 128 || !A || !W || !C || lda < K || ldw < K || ldc < N ||
       (U && ldu < N) || (R && ldr < N) || ((uintptr_t)A & 15) || (lda % 8 && K % 8 == 0)) {
-    set_error("svk_gemm_skinny: bad args (N <= 64, K <= 128, bf16, 16-byte aligned A)"); return SVK_EINVAL;
+    set_error("svk_gemm_skinny: bad args (N <= 64, K <= 128, 16-byte aligned A)"); return SVK_EINVAL;
   }
   if (M == 0) return SVK_OK;
-  SkinnyArgs a{(const bf16*)A, lda, (const bf16*)W, ldw, bias, (const bf16*)U, ldu, uact, (const bf16*)R, ldr,
-               (bf16*)C, ldc, M, N, K, act};
   const long nblk = (M + 15) / 16;
   const int grid = (int)std::min<long>((nblk + 3) / 4, 2048);
   hipStream_t st = (hipStream_t)stream;
   const int nt = (N + 15) / 16, ks = (K + 31) / 32;
-  auto go = [&](auto ntc, auto ksc) {
-    constexpr int NT = decltype(ntc)::value, KS = decltype(ksc)::value;
-    hipLaunchKernelGGL((skinny_gemm<NT, KS>), dim3(grid), dim3(256), 0, st, a);
-  };
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using I3 = std::integral_constant<int, 3>;
-  using I4 = std::integral_constant<int, 4>;
-  auto by_ks = [&](auto ntc) {
-    switch (ks) { case 1: go(ntc, I1{}); break; case 2: go(ntc, I2{}); break; case 3: go(ntc, I3{}); break;
-                  default: go(ntc, I4{}); break; }
-  };
-  switch (nt) { case 1: by_ks(I1{}); break; case 2: by_ks(I2{}); break; case 3: by_ks(I3{}); break;
-                default: by_ks(I4{}); break; }
-  return check_launch("skinny_gemm");
+  SVK_DISPATCH_H16(dtype, T, {
+    SkinnyArgs<T> a{(const T*)A, lda, (const T*)W, ldw, bias, (const T*)U, ldu, uact, (const T*)R, ldr, (T*)C, ldc,
+                    M, N, K, act};
+    auto go = [&](auto ntc, auto ksc) {
+      constexpr int NT = decltype(ntc)::value, KS = decltype(ksc)::value;
+      hipLaunchKernelGGL((skinny_gemm<T, NT, KS>), dim3(grid), dim3(256), 0, st, a);
+    };
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using I3 = std::integral_constant<int, 3>;
+    using I4 = std::integral_constant<int, 4>;
+    auto by_ks = [&](auto ntc) {
+      switch (ks) { case 1: go(ntc, I1{}); break; case 2: go(ntc, I2{}); break; case 3: go(ntc, I3{}); break;
+                    default: go(ntc, I4{}); break; }
+    };
+    switch (nt) { case 1: by_ks(I1{}); break; case 2: by_ks(I2{}); break; case 3: by_ks(I3{}); break;
+                  default: by_ks(I4{}); break; }
+    return check_launch("skinny_gemm");
+  });
 }
 
 extern "C" int svk_wgrad_skinny(const void* dY, long ldy, const void* X, long ldx, float* dW, long lddw, float* db,

@@ -21,8 +21,6 @@ __device__ __forceinline__ void store_vec8(T* dst, const T* o) {
 // select — no branches, every load in flight at once), so each output costs 3(R+2)/R loads instead
 // of 9.  Consecutive lanes take consecutive channel groups: a wave reads whole contiguous pixel
 // rows.  bf16: products in packed f32 (v_pk_fma_f32), branch-free erf for the GELU.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
 template <typename T> struct Vec8 { uint32_t u[sizeof(T) * 2]; };
 
 template <typename T>
@@ -40,8 +38,7 @@ __device__ __forceinline__ void load8_masked(const T* p, bool ok, Vec8<T>& v) {
 template <typename T>
 __device__ __forceinline__ f32x2 pair(const Vec8<T>& v, int j) {
   if constexpr (sizeof(T) == 2) {
-    const uint32_t u = v.u[j];
-    return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+    return unpack2<T>(v.u[j]);
   } else {
     return f32x2{__uint_as_float(v.u[2 * j]), __uint_as_float(v.u[2 * j + 1])};
   }
@@ -224,17 +221,18 @@ __global__ __launch_bounds__(256) void dwconv3x3_roll_bf16(const bf16* __restric
 // padding), then runs the depthwise conv + GELU from LDS and writes G.  The hidden map H — the
 // largest tensor of the path — never goes to HBM: the unfused path writes it once and reads it
 // (through the vector caches) about 1.4 times.  The halo rows cost (R + 2) / R of the fc1 MFMA work.
-template <int KS>   // K = 32 * KS (fc1 input channels)
-__global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ XN, const bf16* __restrict__ W1,
-                                                       const float* __restrict__ b1, const float* __restrict__ taps,
-                                                       const float* __restrict__ db, bf16* __restrict__ G, int H, int W,
-                                                       int K, int HID, int R, int nstrip, int act) {
+template <typename T, int KS>   // T = bf16 / f16; K = 32 * KS (fc1 input channels)
+__global__ __launch_bounds__(256) void fc1_dwconv(const T* __restrict__ XN, const T* __restrict__ W1,
+                                                  const float* __restrict__ b1, const float* __restrict__ taps,
+                                                  const float* __restrict__ db, T* __restrict__ G, int H, int W,
+                                                  int K, int HID, int R, int nstrip, int act) {
+  typedef v8_t<T> tx8;
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
   const int WLD = K + 8;                                   // W1 chunk row stride (elements)
-  bf16* sW = reinterpret_cast<bf16*>(smem);                // [64][WLD]
+  T* sW = reinterpret_cast<T*>(smem);                      // [64][WLD]
   const int TW = W + 2;
-  char* sH = smem + 64 * WLD * 2;                          // [(R + 2)][TW][64] bf16
+  char* sH = smem + 64 * WLD * 2;                          // [(R + 2)][TW][64] T
   const int nnb = HID >> 6;
   const int nwg = gridDim.x;
   const int bid = blockIdx.x, xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -258,7 +256,7 @@ __global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ 
   // fc1 over the (R + 2) x W halo tokens: lane -> token fr of the 16-token tile, 4 channels 4fq + r of
   // each 16-channel block (W1 fragment as the A operand: the tile comes out transposed)
   const int ntok = (R + 2) * W, mt_n = (ntok + 15) >> 4;
-  const bf16* Xb = XN + (long)b * H * W * K;
+  const T* Xb = XN + (long)b * H * W * K;
   float bias4[4][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j)
@@ -266,22 +264,22 @@ __global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ 
     for (int r = 0; r < 4; ++r) bias4[j][r] = b1[nb * 64 + j * 16 + 4 * fq + r];
   // A fragments of this wave's m-tiles, software-pipelined: the next tile's K row is in flight
   // while the current tile's MFMAs run (rows clamped into the image; invalid tokens stored as zeros)
-  auto load_a = [&](int mt, bf16x8* a) {
+  auto load_a = [&](int mt, tx8* a) {
     const int t = mt * 16 + fr;
     const int hr = t / W, x = t - hr * W;
     const int y = min(max(y0 - 1 + hr, 0), H - 1);
-    const bf16* xr = Xb + ((long)y * W + min(x, W - 1)) * K + fq * 8;
+    const T* xr = Xb + ((long)y * W + min(x, W - 1)) * K + fq * 8;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(xr + ks * 32);
+    for (int ks = 0; ks < KS; ++ks) a[ks] = *reinterpret_cast<const tx8*>(xr + ks * 32);
   };
-  bf16x8 anext[KS];
+  tx8 anext[KS];
   if (wave < mt_n) load_a(wave, anext);
   for (int mt = wave; mt < mt_n; mt += 4) {
     const int t = mt * 16 + fr;
     const int hr = t / W, x = t - hr * W;
     const int y = y0 - 1 + hr;
     const bool valid = t < ntok && (unsigned)y < (unsigned)H;
-    bf16x8 a[KS];
+    tx8 a[KS];
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) a[ks] = anext[ks];
     if (mt + 4 < mt_n) load_a(mt + 4, anext);
@@ -292,16 +290,16 @@ __global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ 
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const bf16x8 w = *reinterpret_cast<const bf16x8*>(sW + (j * 16 + fr) * WLD + ks * 32 + fq * 8);
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, a[ks], acc[j], 0, 0, 0);
+        const tx8 w = *reinterpret_cast<const tx8*>(sW + (j * 16 + fr) * WLD + ks * 32 + fq * 8);
+        acc[j] = mfma16x16x32(w, a[ks], acc[j]);
       }
     if (t < ntok) {
       char* dst = sH + ((hr * TW + x + 1) * 64) * 2;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        bf16 o[4];
+        T o[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = valid ? (bf16)(acc[j][r] + bias4[j][r]) : (bf16)0.f;
+        for (int r = 0; r < 4; ++r) o[r] = valid ? (T)(acc[j][r] + bias4[j][r]) : (T)0.f;
         *reinterpret_cast<uint2*>(dst + (j * 16 + 4 * fq) * 2) = *reinterpret_cast<const uint2*>(o);
       }
     }
@@ -320,7 +318,7 @@ __global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ 
   __syncthreads();
   const uint4* tile = reinterpret_cast<const uint4*>(sH);
   const int rows = min(R, H - y0);
-  bf16* Gb = G + (long)b * H * W * HID + c0;
+  T* Gb = G + (long)b * H * W * HID + c0;
   for (int q = pl; q < rows * W; q += 32) {
     const int r = q / W, x = q - r * W;
     f32x2 acc[4];
@@ -330,17 +328,17 @@ __global__ __launch_bounds__(256) void fc1_dwconv_bf16(const bf16* __restrict__ 
     for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        Vec8<bf16> v;
+        Vec8<T> v;
         *reinterpret_cast<uint4*>(v.u) = tile[((r + dy) * TW + x + dx) * 8 + c];
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[j] = pair(v, j) * wt[dy * 3 + dx][j] + acc[j];
       }
-    bf16 o[8];
+    T o[8];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const f32x2 g = act == SVK_ACT_GELU ? gelu_fast2(acc[j]) : f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
-      o[2 * j] = (bf16)g.x;
-      o[2 * j + 1] = (bf16)g.y;
+      o[2 * j] = (T)g.x;
+      o[2 * j + 1] = (T)g.y;
     }
     store_vec8(Gb + ((long)(y0 + r) * W + x) * HID, o);
   }
@@ -638,7 +636,8 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
   SVK_DISPATCH_DTYPE(dtype, T, {
     const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 15) == 0;
     const int lds_env = g_tune[TUNE_DW_LDS], rows_env = g_tune[TUNE_DW_ROWS];   // svk_tune knobs
-    if (sizeof(T) == 2 && lds_env == 2 && C % 4 == 0 && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 7) == 0) {
+    constexpr bool is_bf16 = std::is_same<T, bf16>::value;   // the opt-in variants below are bf16-only
+    if (is_bf16 && lds_env == 2 && C % 4 == 0 && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 7) == 0) {
       constexpr int RR = 8;
       const int nstrip = (H + RR - 1) / RR;
       const long n = (long)B * nstrip * W * (C / 4);
@@ -646,7 +645,7 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
                          (bf16*)Ypre, B, H, W, C, act, nstrip);
       return check_launch("dwconv3x3_roll");
     }
-    if (sizeof(T) == 2 && vec && C % 64 == 0 && lds_env == 1) {
+    if (is_bf16 && vec && C % 64 == 0 && lds_env == 1) {
       // strip height: the tallest strip whose halo tile fits 48 KiB (3 workgroups per CU)
       int R = rows_env > 0 ? rows_env : 49152 / ((W + 2) * 128) - 2;
       R = std::max(1, std::min(R, H));
@@ -662,7 +661,7 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
       }
     }
     if (vec) {
-      constexpr int R = sizeof(T) == 2 ? 7 : 2;   // bf16: 56 / 28 / 14 / 7-row maps in whole strips
+      constexpr int R = sizeof(T) == 2 ? 7 : 2;   // 16-bit: 56 / 28 / 14 / 7-row maps in whole strips
       const int nstrip = (H + R - 1) / R;
       const long n = (long)B * nstrip * W * (C / 8);
       hipLaunchKernelGGL((dwconv3x3_strip<T, R>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B,
@@ -676,16 +675,16 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
   });
 }
 
-// fc1 + depthwise conv + activation (MixFFN front half) in one pass; see fc1_dwconv_bf16.
+// fc1 + depthwise conv + activation (MixFFN front half) in one pass; see fc1_dwconv.
 extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
                                      const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act,
                                      void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || C <= 0 || hidden <= 0 || !XN || !W1 || !b1 || !taps || !dbias || !G) {
     set_error("svk_mixffn_fc1_dwconv: bad args"); return SVK_EINVAL;
   }
-  if (dtype != SVK_BF16 || (C != 32 && C != 64 && C != 128) || hidden % 64 ||
+  if ((dtype != SVK_BF16 && dtype != SVK_F16) || (C != 32 && C != 64 && C != 128) || hidden % 64 ||
       ((((uintptr_t)XN) | ((uintptr_t)W1) | ((uintptr_t)G)) & 15)) {
-    set_error("svk_mixffn_fc1_dwconv: needs bf16, C in {32, 64, 128}, hidden %% 64 == 0, 16-byte aligned maps");
+    set_error("svk_mixffn_fc1_dwconv: needs bf16 / f16, C in {32, 64, 128}, hidden %% 64 == 0, 16-byte aligned maps");
     return SVK_EUNSUPPORTED;
   }
   if (B == 0) return SVK_OK;
@@ -699,17 +698,19 @@ extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, 
   if (lds > 160 * 1024) { set_error("svk_mixffn_fc1_dwconv: tile too large"); return SVK_EUNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   const long nwg = (long)B * nstrip * (hidden / 64);
-  auto go = [&](auto ks_c) {
-    constexpr int KS = decltype(ks_c)::value;
-    if (lds > 65536)
-      (void)hipFuncSetAttribute((const void*)fc1_dwconv_bf16<KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((fc1_dwconv_bf16<KS>), dim3((unsigned)nwg), dim3(256), lds, st, (const bf16*)XN, (const bf16*)W1,
-                       b1, taps, dbias, (bf16*)G, H, W, C, hidden, R, nstrip, act);
-  };
-  if (C == 32) go(std::integral_constant<int, 1>{});
-  else if (C == 64) go(std::integral_constant<int, 2>{});
-  else go(std::integral_constant<int, 4>{});
-  return check_launch("fc1_dwconv");
+  SVK_DISPATCH_H16(dtype, T, {
+    auto go = [&](auto ks_c) {
+      constexpr int KS = decltype(ks_c)::value;
+      if (lds > 65536)
+        (void)hipFuncSetAttribute((const void*)fc1_dwconv<T, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((fc1_dwconv<T, KS>), dim3((unsigned)nwg), dim3(256), lds, st, (const T*)XN, (const T*)W1, b1,
+                         taps, dbias, (T*)G, H, W, C, hidden, R, nstrip, act);
+    };
+    if (C == 32) go(std::integral_constant<int, 1>{});
+    else if (C == 64) go(std::integral_constant<int, 2>{});
+    else go(std::integral_constant<int, 4>{});
+    return check_launch("fc1_dwconv");
+  });
 }
 
 extern "C" int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B, int H,

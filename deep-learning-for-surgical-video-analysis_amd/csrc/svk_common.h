@@ -8,7 +8,13 @@
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 namespace svk {
 
@@ -21,7 +27,8 @@ extern int g_tune[TUNE_NKNOBS];
 // Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
 void set_last_kernel(const char* name);
 // norm.hip: Y = LN(sum of ks f32 split-K slabs [ks][M][C] + bias), bf16 out (svk_conv2d_ln_nhwc)
-int splitk_layernorm(const float* S, int ks, const float* bias, __bf16* Y, int M, int C, const float* gamma,
+template <typename T>
+int splitk_layernorm(const float* S, int ks, const float* bias, T* Y, int M, int C, const float* gamma,
                      const float* beta, float eps, hipStream_t st);
 // gemm.hip: batched split-M weight-gradient reduction dW[z] += dY[z]^T X[z] (f32 atomics)
 int wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o,
@@ -30,9 +37,39 @@ int wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, con
 
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+__device__ __forceinline__ float to_f(f16 x) { return (float)x; }
 template <typename T> __device__ __forceinline__ T from_f(float x);
 template <> __device__ __forceinline__ float from_f<float>(float x) { return x; }
 template <> __device__ __forceinline__ bf16 from_f<bf16>(float x) { return (bf16)x; }
+template <> __device__ __forceinline__ f16 from_f<f16>(float x) { return (f16)x; }
+
+// 16-bit storage types of the MFMA path: bf16 (8 significant bits) and f16 (11 significant bits,
+// the reference's torch.autocast(float16) precision, train_evp.py:493/637/760).  Both run the
+// 16x16x32 MFMA at the same rate on gfx950; accumulation is f32 either way.
+template <typename T> struct VT;
+template <> struct VT<bf16> { typedef bf16x8 x8; typedef bf16x4 x4; };
+template <> struct VT<f16> { typedef f16x8 x8; typedef f16x4 x4; };
+template <typename T> using v8_t = typename VT<T>::x8;
+template <typename T> using v4_t = typename VT<T>::x4;
+template <typename T> constexpr const char* type_name() {
+  return sizeof(T) == 4 ? "float" : (__is_same(T, bf16) ? "__bf16" : "_Float16");
+}
+
+__device__ __forceinline__ f32x4 mfma16x16x32(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16x16x32(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// The two 16-bit elements of a 32-bit word (element 0 in the low half) as f32.
+template <typename T> __device__ __forceinline__ f32x2 unpack2(uint32_t u);
+template <> __device__ __forceinline__ f32x2 unpack2<bf16>(uint32_t u) {
+  return f32x2{__uint_as_float(u << 16), __uint_as_float(u & 0xFFFF0000u)};
+}
+template <> __device__ __forceinline__ f32x2 unpack2<f16>(uint32_t u) {
+  return __builtin_convertvector(__builtin_bit_cast(f16x2, u), f32x2);
+}
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
@@ -108,5 +145,14 @@ __device__ __forceinline__ float wave_max(float v) {
   do {                                                                   \
     if ((dt) == SVK_F32) { typedef float T; __VA_ARGS__; }               \
     else if ((dt) == SVK_BF16) { typedef bf16 T; __VA_ARGS__; }          \
+    else if ((dt) == SVK_F16) { typedef f16 T; __VA_ARGS__; }            \
     else { svk::set_error("unsupported dtype %d", (int)(dt)); return SVK_EINVAL; } \
+  } while (0)
+
+// 16-bit MFMA-only paths (bf16 / f16)
+#define SVK_DISPATCH_H16(dt, T, ...)                                     \
+  do {                                                                   \
+    if ((dt) == SVK_BF16) { typedef bf16 T; __VA_ARGS__; }               \
+    else if ((dt) == SVK_F16) { typedef f16 T; __VA_ARGS__; }            \
+    else { svk::set_error("dtype %d: bf16 / f16 only", (int)(dt)); return SVK_EUNSUPPORTED; } \
   } while (0)

@@ -11,8 +11,9 @@ its GELU, and the efficient self-attention is one kernel per (frame, head, 64 qu
 The reference's NCHW round trips between stages (:376, :388, :400, :412) disappear.
 
 Compute dtype: ``model.svk_dtype`` (torch.float32 -> f32 MFMA, the parity path;
-torch.bfloat16 -> bf16 MFMA with f32 accumulation), default bf16 under CUDA autocast
-else f32.  Eval-mode forward only (see models._common.check_inference).
+torch.float16 / torch.bfloat16 -> 16-bit MFMA with f32 accumulation), default: the autocast
+dtype inside a CUDA autocast region (float16, as the reference's train_evp.py:493/637/760
+regions use), else f32 (generate_evp_LFB.py / trans_SV_output.py run fp32).  Eval-mode forward only (see models._common.check_inference).
 """
 from functools import partial
 
@@ -82,7 +83,7 @@ class Mlp(nn.Module):
         hid = self.fc1.out_features
         # measured: wins where the hidden map is largest (stages 1-2, C <= 128); at C = 320 / 512 the
         # recomputed halo fc1 work outweighs the saved traffic
-        if ops.FC1_DWCONV and x.dtype == torch.bfloat16 and C in (32, 64, 128) and hid % 64 == 0:
+        if ops.FC1_DWCONV and x.dtype in ops.H16 and C in (32, 64, 128) and hid % 64 == 0:
             # fc1 -> DWConv -> GELU in one kernel, the hidden map kept on chip (Mlp.forward :60-63)
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")

@@ -8,10 +8,12 @@ from ._lib import SvkError, load, version  # noqa: F401
 
 
 def default_dtype():
-    """Compute dtype when a caller does not pin one: bf16 under a CUDA autocast region
-    (train_evp.py:493 runs fp16 autocast; gfx950 prefers bf16), else fp32 (the
-    reference's generate_evp_LFB / trans_SV_output run fp32)."""
+    """Compute dtype when a caller does not pin one: the autocast dtype inside a CUDA autocast
+    region (the reference's train_evp.py:493/637/760 regions are torch.autocast(float16): f16
+    MFMA with f32 accumulation, same MFMA rate as bf16 on gfx950), else fp32 (the reference's
+    generate_evp_LFB / trans_SV_output run fp32)."""
     import torch
     if torch.is_autocast_enabled("cuda"):
-        return torch.bfloat16
+        dt = torch.get_autocast_dtype("cuda")
+        return dt if dt in (torch.float16, torch.bfloat16) else torch.float16
     return torch.float32

@@ -48,7 +48,7 @@ SIGNATURES = {
                     c_int, c_int, P],
     "svk_gemm_unpatchify": [c_int, P, c_long, P, c_long, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_gemm_wgrad": [c_int, P, c_long, P, c_long, P, c_long, P, c_int, c_int, c_int, P],
-    "svk_gemm_skinny": [P, c_long, P, c_long, P, P, c_long, c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, P],
+    "svk_gemm_skinny": [c_int, P, c_long, P, c_long, P, P, c_long, c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, P],
     "svk_wgrad_skinny": [P, c_long, P, c_long, P, c_long, P, c_int, c_int, c_int, P],
     "svk_conv2d_wgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, P, P, P],
     "svk_conv2d_dgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,

@@ -11,16 +11,17 @@ import torch
 
 from . import _lib
 
-F32, BF16 = 0, 1
+F32, BF16, F16 = 0, 1, 2
 ACT = {None: 0, "none": 0, "gelu": 1, "relu": 2, "tanh": 3}
-_DT = {torch.float32: F32, torch.bfloat16: BF16}
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
+H16 = (torch.bfloat16, torch.float16)     # the 16-bit MFMA storage types
 
 
 def dtype_code(dt):
     try:
         return _DT[dt]
     except KeyError:
-        raise _lib.SvkError(f"svk: unsupported dtype {dt} (float32 / bfloat16 only)") from None
+        raise _lib.SvkError(f"svk: unsupported dtype {dt} (float32 / float16 / bfloat16 only)") from None
 
 
 def _chk(t, name, dtype=None):
@@ -113,7 +114,7 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
         _, rc, ldr = _rows(residual, "residual")
         if rc != N:
             raise _lib.SvkError("svk.gemm: residual width mismatch")
-    if (SKINNY and row_scale is None and a.dtype == torch.bfloat16 and N <= 64 and K <= 128 and M >= 2048
+    if (SKINNY and row_scale is None and a.dtype in H16 and N <= 64 and K <= 128 and M >= 2048
             and a.data_ptr() % 16 == 0 and (K % 8 or lda % 8 == 0)):
         return gemm_skinny(a, w, bias, act, residual, out, N, dact, dact_src)
     t0 = _prof_begin()
@@ -147,9 +148,12 @@ SKINNY = os.environ.get("SVK_SKINNY", "1") == "1"
 
 
 def gemm_skinny(a, w, bias=None, act=None, residual=None, out=None, n=None, dact=None, dact_src=None):
-    """svk_gemm_skinny (bf16, N <= 64, K <= 128): same contract as gemm() without row_scale."""
-    _chk(a, "a", torch.bfloat16); _chk(w, "w", torch.bfloat16); _chk(bias, "bias", torch.float32)
-    _chk(residual, "residual", torch.bfloat16); _chk(dact_src, "dact_src", torch.bfloat16)
+    """svk_gemm_skinny (bf16 / f16, N <= 64, K <= 128): same contract as gemm() without row_scale."""
+    _chk(a, "a")
+    if a.dtype not in H16:
+        raise _lib.SvkError("svk.gemm_skinny: bf16 / f16 only")
+    _chk(w, "w", a.dtype); _chk(bias, "bias", torch.float32)
+    _chk(residual, "residual", a.dtype); _chk(dact_src, "dact_src", a.dtype)
     M, K, lda = _rows(a, "a")
     N = w.shape[0] if n is None else n
     if w.shape[1] != K or w.stride(1) != 1:
@@ -160,7 +164,7 @@ def gemm_skinny(a, w, bias=None, act=None, residual=None, out=None, n=None, dact
     ldr = _rows(residual, "residual")[2] if residual is not None else 0
     ldu = _rows(dact_src, "dact_src")[2] if dact_src is not None else 0
     t0 = _prof_begin()
-    _lib.call("svk_gemm_skinny", _p(a), lda, _p(w), w.stride(0), _p(bias), _p(dact_src), ldu, ACT[dact],
+    _lib.call("svk_gemm_skinny", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(dact_src), ldu, ACT[dact],
               _p(residual), ldr, _p(out), ldc, M, N, K, ACT[act], _stream())
     _prof_end(t0, "skinny_gemm", 2.0 * M * N * K,
               (M * K + N * K + M * N * (1 + (residual is not None) + (dact is not None))) * 2, (M, N, K, "skinny"))
@@ -279,9 +283,11 @@ FC1_DWCONV = os.environ.get("SVK_FC1_DWCONV", "1") == "1"
 
 
 def mixffn_fc1_dwconv(xn, w1, b1, taps, dbias, act="gelu"):
-    """act(dwconv3x3(xn @ w1.T + b1) + dbias) on an NHWC [B, H, W, C] bf16 map -> [B, H, W, hidden];
+    """act(dwconv3x3(xn @ w1.T + b1) + dbias) on an NHWC [B, H, W, C] bf16 / f16 map -> [B, H, W, hidden];
     the hidden map never leaves the chip (svk_mixffn_fc1_dwconv)."""
-    _chk(xn, "xn", torch.bfloat16); _chk(w1, "w1", torch.bfloat16)
+    _chk(xn, "xn"); _chk(w1, "w1", xn.dtype)
+    if xn.dtype not in H16:
+        raise _lib.SvkError("svk.mixffn_fc1_dwconv: bf16 / f16 only")
     for t, nm in ((b1, "b1"), (taps, "taps"), (dbias, "dbias")):
         _chk(t, nm, torch.float32)
     if not xn.is_contiguous() or xn.dim() != 4 or not w1.is_contiguous():
@@ -292,11 +298,11 @@ def mixffn_fc1_dwconv(xn, w1, b1, taps, dbias, act="gelu"):
         raise _lib.SvkError("svk.mixffn_fc1_dwconv: shape mismatch")
     out = torch.empty(B, H, W, hid, device=xn.device, dtype=xn.dtype)
     t0 = _prof_begin()
-    _lib.call("svk_mixffn_fc1_dwconv", BF16, _p(xn), _p(w1), _p(b1), _p(taps), _p(dbias), _p(out), B, H, W, C, hid,
+    _lib.call("svk_mixffn_fc1_dwconv", dtype_code(xn.dtype), _p(xn), _p(w1), _p(b1), _p(taps), _p(dbias), _p(out), B, H, W, C, hid,
               ACT[act], _stream())
     if t0 is not None:
         M = B * H * W
-        _prof_end(t0, "fc1_dwconv_bf16", 2.0 * M * C * hid, (xn.numel() + out.numel() + w1.numel()) * 2,
+        _prof_end(t0, "fc1_dwconv", 2.0 * M * C * hid, (xn.numel() + out.numel() + w1.numel()) * 2,
                   (M, hid, C, "fc1dw"))
     return out
 

@@ -110,7 +110,8 @@ class EVPTrainStep:
         self._setup_frozen()
         self._setup_packs()
         self.counter = torch.zeros(1, device=self.dev, dtype=torch.int64)   # device step count (mask RNG)
-        self.graph = None
+        self.graph = self.graph_rest = self.graph_opt = None
+        self._pending = None
 
     # ---- parameter storage ------------------------------------------------------------------
     def _setup_flat(self):
@@ -135,6 +136,11 @@ class EVPTrainStep:
                 o += k
         self.params = dict(tr)
         self.n_trainable = total
+        # the head's parameters lead the flat buffer (model construction order): its gradient bucket
+        heads = [n for n, _ in tr if n.startswith("head.")]
+        self.head_end = max((self.off[n] + self.params[n].numel() for n in heads), default=0)
+        if any(not n.startswith("head.") and self.off[n] < self.head_end for n, _ in tr):
+            self.head_end = 0                      # not a prefix: one bucket
 
     def P(self, name):
         """f32 master view of a trainable parameter."""
@@ -455,7 +461,12 @@ class EVPTrainStep:
                        None if bias_name is None else self.G(bias_name))
 
     def _backward(self, sv, dlogits, dant):
-        dt, B, pg = self.dt, sv["B"], "prompt_generator"
+        self._backward_rest(sv, self._backward_head(sv, dlogits, dant))
+
+    def _backward_head(self, sv, dlogits, dant):
+        """SegFormerHead backward: after it every head.* gradient (the first, 85 % of the flat gradient
+        buffer) is final, so DDP can all-reduce that bucket while the backbone backward runs."""
+        dt, B = self.dt, sv["B"]
         hd = sv["head"]
         # fc / fc_ant (f32)
         dfeat = None
@@ -472,7 +483,6 @@ class EVPTrainStep:
                         self.G(bn + ".weight"), self.G(bn + ".bias"), relu=True)
         ops.gemm_wgrad(dZ, hd["E"], self.G("head.linear_fuse.conv.weight").view(2048, -1))
         dE = ops.gemm(dZ, self.W("head.linear_fuse.conv.weight.T"))
-        stages = sv["stages"]
         dtok = [None] * 4
         for j, (lvl, r, H, W) in enumerate(hd["rs"]):
             dEj = dE[:, j * 2048:(j + 1) * 2048]
@@ -485,6 +495,11 @@ class EVPTrainStep:
                 acc = torch.zeros(B, H * W, dr.shape[-1], device=self.dev, dtype=torch.float32)
                 ops.resize_bilinear_bwd(dr.view(B, R, -1), H, W, 7, 7, acc)
                 dtok[lvl] = ops.cast(acc, dt)
+        return dtok
+
+    def _backward_rest(self, sv, dtok):
+        dt, B, pg = self.dt, sv["B"], "prompt_generator"
+        stages = sv["stages"]
         # cross attention (s4, s3) -> grads of backbone c3/c4 and of the flow features
         dflow = {}
         for s in (4, 3):
@@ -605,7 +620,16 @@ class EVPTrainStep:
     # ---- the step ---------------------------------------------------------------------------------
     def forward_backward(self, x, y, flow, labels, ant_targets, masks=None):
         """Zero grads, forward (train mode), loss, backward.  Returns (loss [2] f32 device tensor
-        = (CE sum, SmoothL1 sum), logits, anticipation)."""
+        = (CE sum, SmoothL1 sum), logits, anticipation).  No collective runs in here (with DDP the
+        caller syncs the BN buffers before and all-reduces the gradient buckets after, outside any
+        captured graph: train_iteration / _replay)."""
+        out = self.fb_head(x, y, flow, labels, ant_targets, masks)
+        self.fb_rest()
+        return out
+
+    def fb_head(self, x, y, flow, labels, ant_targets, masks=None):
+        """First part of forward_backward: zero grads, forward, loss, head backward (the head bucket of
+        the gradient is final afterwards)."""
         B = x.numel() // (3 * 224 * 224)
         if masks is None:
             masks = self.make_masks(B)
@@ -615,14 +639,19 @@ class EVPTrainStep:
                      "dropout2d": masks["dropout2d"].to(self.dev, torch.float32).contiguous()}
         self.grad.zero_()
         self.conv_scratch.zero_()
-        if self.group is not None and self.world > 1:
-            self._broadcast_buffers()
         sv, logits, ant = self._forward(x, y, flow, masks)
         loss, dl, da = ops.phase_loss(logits, ant, labels, ant_targets)
-        self._backward(sv, dl, da)
+        self._pending = (sv, self._backward_head(sv, dl, da))
+        return loss, logits, ant
+
+    def fb_rest(self):
+        """Second part: backbone / cross-attention / flow / prompt backward, conv-grad unpack, BN
+        running statistics."""
+        sv, dtok = self._pending
+        self._pending = None
+        self._backward_rest(sv, dtok)
         self.untab.run(self.conv_scratch, self.grad)   # packed conv weight grads -> flat grad (f32 gather)
         self._update_bn_running(sv)
-        return loss, logits, ant
 
     def _update_bn_running(self, sv):
         m = self.model
@@ -640,12 +669,48 @@ class EVPTrainStep:
             dist.broadcast(bn.running_mean, 0, group=self.group)
             dist.broadcast(bn.running_var, 0, group=self.group)
 
+    def _ddp(self):
+        return self.group is not None and self.world > 1
+
+    def sync_buffers(self):
+        """DDP's broadcast_buffers: BN running statistics from rank 0, once per step, before the forward
+        (eager, never inside a captured graph)."""
+        if self._ddp():
+            self._broadcast_buffers()
+
+    def _grad_buckets(self):
+        """Gradient all-reduce buckets, in the order backward finalises them: the head prefix of the flat
+        buffer (final after fb_head), then the rest (final after fb_rest)."""
+        h = self.head_end
+        return [self.grad[:h], self.grad[h:]] if 0 < h < self.grad.numel() else [self.grad]
+
+    def _allreduce_async(self, bucket):
+        import torch.distributed as dist
+        return dist.all_reduce(bucket, group=self.group, async_op=True)
+
     def allreduce_grads(self):
-        """DDP gradient averaging: one RCCL all-reduce over the flat f32 gradient buffer."""
-        if self.group is not None and self.world > 1:
-            import torch.distributed as dist
-            dist.all_reduce(self.grad, group=self.group)
+        """DDP gradient averaging over the flat f32 gradient (bucket by bucket; sum then / world)."""
+        if self._ddp():
+            for w in [self._allreduce_async(b) for b in self._grad_buckets()]:
+                w.wait()
             self.grad.mul_(1.0 / self.world)
+
+    def train_iteration(self, x, y, flow, labels, ant_targets, masks=None):
+        """Eager data-parallel iteration with the head bucket's all-reduce overlapped with the backbone
+        backward: buffers sync -> fb_head -> all-reduce(head) in flight -> fb_rest -> all-reduce(rest)
+        -> wait -> average -> SGD."""
+        self.sync_buffers()
+        out = self.fb_head(x, y, flow, labels, ant_targets, masks)
+        buckets = self._grad_buckets()
+        works = [self._allreduce_async(buckets[0])] if self._ddp() and len(buckets) > 1 else []
+        self.fb_rest()
+        if self._ddp():
+            works.append(self._allreduce_async(buckets[-1]))
+            for w in works:
+                w.wait()
+            self.grad.mul_(1.0 / self.world)
+        self.optimizer_step()
+        return out
 
     def _optimizer_launch(self, first):
         h = self.hp
@@ -670,18 +735,16 @@ class EVPTrainStep:
         After capture() with these same input tensors, the iteration replays as one HIP graph."""
         if self.graph is not None and masks is None and self._static == (x, y, flow, labels, ant_targets):
             return self._replay()
-        loss, logits, ant = self.forward_backward(x, y, flow, labels, ant_targets, masks)
-        self.allreduce_grads()
-        self.optimizer_step()
-        return loss, logits, ant
+        return self.train_iteration(x, y, flow, labels, ant_targets, masks)
 
     # ---- HIP graph capture ----------------------------------------------------------------------
     def capture(self, x, y, flow, labels, ant_targets):
         """Capture one full iteration (forward, backward, SGD, re-pack) over these input tensors as a
         HIP graph (torch.cuda.CUDAGraph drives hipStreamBeginCapture).  The ~700 kernel launches of a
-        step then cost one graph launch.  With DDP the gradient all-reduce stays outside the graph
-        (two graphs: forward/backward and optimizer).  Needs at least one eager step first (momentum
-        buffer initialised)."""
+        step then cost one graph launch.  With DDP no collective is captured: three graphs (fb_head,
+        fb_rest, averaging + optimizer) replay around the eager BN-buffer broadcast and the two bucket
+        all-reduces, the head bucket's overlapping fb_rest.  Needs at least one eager step first
+        (momentum buffer initialised)."""
         if self.steps == 0:
             raise SvkError("EVPTrainStep.capture: run one eager step first")
         self._static = (x, y, flow, labels, ant_targets)
@@ -698,22 +761,37 @@ class EVPTrainStep:
                 bn.running_mean.copy_(rm)
                 bn.running_var.copy_(rv)
                 bn.num_batches_tracked.copy_(nb)
+        self.graph_rest = self.graph_opt = None
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self._gout = self.forward_backward(*self._static)
-            if not ddp:
+        if not ddp:
+            with torch.cuda.graph(self.graph):
+                self._gout = self.forward_backward(*self._static)
                 self._optimizer_launch(first=False)
-        self.graph_opt = None
-        if ddp:
-            self.graph_opt = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph_opt):
-                self._optimizer_launch(first=False)
+            return self
+        pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(self.graph, pool=pool):
+            self._gout = self.fb_head(*self._static)
+        self.graph_rest = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_rest, pool=pool):
+            self.fb_rest()
+        self.graph_opt = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph_opt, pool=pool):
+            self.grad.mul_(1.0 / self.world)
+            self._optimizer_launch(first=False)
         return self
 
     def _replay(self):
-        self.graph.replay()
-        if self.graph_opt is not None:
-            self.allreduce_grads()
+        if self.graph_rest is None:
+            self.graph.replay()
+        else:
+            self.sync_buffers()
+            self.graph.replay()
+            buckets = self._grad_buckets()
+            works = [self._allreduce_async(buckets[0])] if len(buckets) > 1 else []
+            self.graph_rest.replay()
+            works.append(self._allreduce_async(buckets[-1]))
+            for w in works:
+                w.wait()
             self.graph_opt.replay()
         self._after_step()
         return self._gout

@@ -14,8 +14,11 @@
  *   - Return 0 on success, negative SVK_E* on error; svk_last_error() gives a
  *     thread-local message.  No exceptions cross the ABI.
  *   - dtype selects the storage/compute type of activations and weights:
- *     SVK_F32 (f32 MFMA, exact f32 products, parity path) or SVK_BF16 (bf16 MFMA,
- *     f32 accumulation).  Biases, norm affine terms and depthwise taps are f32.
+ *     SVK_F32 (f32 MFMA, exact f32 products, parity path), SVK_F16 (f16 MFMA, f32
+ *     accumulation: the precision of the reference's torch.autocast(float16) regions,
+ *     train_evp.py:493/637/760) or SVK_BF16 (bf16 MFMA, f32 accumulation).  Biases, norm
+ *     affine terms and depthwise taps are f32; statistics and accumulation are f32 for
+ *     every dtype.
  *   - Token layouts are row-major [rows, channels] with an explicit leading
  *     dimension; image/feature maps are NHWC (token n = h*W + w, the reference's
  *     own `flatten(2).transpose(1, 2)` order, mix_transformer_evp.py:212).
@@ -27,7 +30,7 @@
 extern "C" {
 #endif
 
-enum { SVK_F32 = 0, SVK_BF16 = 1 };
+enum { SVK_F32 = 0, SVK_BF16 = 1, SVK_F16 = 2 };
 enum { SVK_ACT_NONE = 0, SVK_ACT_GELU = 1, SVK_ACT_RELU = 2, SVK_ACT_TANH = 3 };
 enum { SVK_OK = 0, SVK_EINVAL = -1, SVK_EUNSUPPORTED = -2, SVK_ELAUNCH = -3 };
 
@@ -217,10 +220,10 @@ int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, long ldw, con
 int svk_gemm_unpatchify(int dtype, const void* A, long lda, const void* W, long ldw, const void* R, void* Y,
                         int B, int H, int Wd, int s, int C, int K, void* stream);
 
-/* Skinny bf16 GEMM for the prompt path (PromptGenerator Linears, mix_transformer_evp.py:749-815):
+/* Skinny bf16 / f16 GEMM for the prompt path (PromptGenerator Linears, mix_transformer_evp.py:749-815):
  * C = act(A W^T + bias) * uact'(U) + R with N <= 64, K <= 128 (W held in LDS, A streamed in the MFMA
  * operand layout); same semantics as svk_gemm_ex without row scale.  A 16-byte aligned. */
-int svk_gemm_skinny(const void* A, long lda, const void* W, long ldw, const float* bias, const void* U, long ldu,
+int svk_gemm_skinny(int dtype, const void* A, long lda, const void* W, long ldw, const float* bias, const void* U, long ldu,
                     int uact, const void* R, long ldr, void* C, long ldc, int M, int N, int K, int act,
                     void* stream);
 

@@ -70,8 +70,9 @@ def test_shard_range_properties():
 
 
 def _ddp_worker(rank, world, port, out):
-    """The train step's data-parallel exchange (svk.train.EVPTrainStep.allreduce_grads /
-    _broadcast_buffers) on CPU tensors: gradient averaging over ranks, BN buffers from rank 0."""
+    """The train step's data-parallel exchange (svk.train.EVPTrainStep.allreduce_grads over its two
+    gradient buckets / sync_buffers) on CPU tensors: gradient averaging over ranks, BN buffers from
+    rank 0."""
     import sys
     import types
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -89,9 +90,11 @@ def _ddp_worker(rank, world, port, out):
         bn.running_var.fill_(rank + 1.0)
     model = types.SimpleNamespace(head=types.SimpleNamespace(linear_fuse=types.SimpleNamespace(bn=bns[0])),
                                   flow_encoder=types.SimpleNamespace(**{f"bn{i}": bns[i] for i in range(1, 5)}))
-    tr = types.SimpleNamespace(group=dist.group.WORLD, world=world, grad=grad, model=model)
-    EVPTrainStep.allreduce_grads(tr)
-    EVPTrainStep._broadcast_buffers(tr)
+    tr = EVPTrainStep.__new__(EVPTrainStep)     # the exchange methods only, no GPU state
+    tr.group, tr.world, tr.grad, tr.model, tr.head_end = dist.group.WORLD, world, grad, model, 400
+    assert [b.numel() for b in tr._grad_buckets()] == [400, 600]      # head bucket, then the rest
+    tr.allreduce_grads()
+    tr.sync_buffers()
     out[rank] = (local, grad.clone(), [bn.running_mean.clone() for bn in bns], [bn.running_var.clone() for bn in bns])
     dist.destroy_process_group()
 

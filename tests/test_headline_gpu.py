@@ -1,0 +1,121 @@
+"""Parity of the BENCHED configuration (bench.py's default workload: MiT-b2-EVP + optical-flow fusion,
+B = 256 frames, return_features and logits) against the fp32 oracle on the same inputs.
+
+Bars (north star: logits within 1e-3 at fp32, argmax labels bit-exact):
+  * fp32 (the precision of the reference's generate_evp_LFB.py): features and both logit heads within
+    1e-3 absolute, phase argmax identical for all 256 frames.
+  * fp16 (the headline dtype; the precision of the reference's torch.autocast(float16) inference and
+    validation passes, train_evp.py:637/760): f16 storage, f32 accumulation / statistics.  Features
+    within FP16_FEAT_ATOL absolute, logits within FP16_LOGIT_ATOL, phase-argmax agreement >=
+    FP16_ARGMAX_MIN over the 256 frames (measured values are printed; profiles/r02/precision_b256.txt).
+  * bf16 (extra key only): features within 5e-2, logits within 2e-2.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import inputs as I, params as P, mit_evp as M, shapes as SH
+
+pytestmark = pytest.mark.gpu
+
+B = 256
+VARIANT = "mit_b2_evp"
+FP16_FEAT_ATOL = 1e-2
+FP16_LOGIT_ATOL = 5e-3
+FP16_ARGMAX_MIN = 0.99
+
+
+def _head_logits(feat, sd):
+    f = torch.nn.functional
+    y = f.linear(f.relu(f.linear(feat, sd["head.fc.0.weight"], sd["head.fc.0.bias"])), sd["head.fc.2.weight"],
+                 sd["head.fc.2.bias"])
+    ya = f.linear(f.relu(f.linear(feat, sd["head.fc_ant.0.weight"], sd["head.fc_ant.0.bias"])),
+                  sd["head.fc_ant.2.weight"], sd["head.fc_ant.2.bias"])
+    return y, ya
+
+
+@pytest.fixture(scope="module")
+def b256():
+    sd = P.make_state_dict(SH.mit_evp_shapes(VARIANT), 0)
+    x, y, fl = I.frames(B, 21), I.segmaps(B, 21), I.flow(B, 21)
+    with torch.no_grad():
+        feat = M.forward(x, y, sd, VARIANT, fl, return_features=True)
+        yl, ya = _head_logits(feat, sd)
+    return sd, (x, y, fl), feat, yl, ya
+
+
+def _run(cuda, b256, dtype):
+    from models import mix_transformer_evp as mte
+    sd, (x, y, fl), *_ = b256
+    m = getattr(mte, VARIANT)()
+    m.load_state_dict(sd)
+    m.svk_dtype = dtype
+    m = m.to(cuda).eval()
+    with torch.no_grad():
+        f = m(x.to(cuda), y.to(cuda), fl.to(cuda), return_features=True)
+        gl, ga = m(x.to(cuda), y.to(cuda), fl.to(cuda))
+    torch.cuda.synchronize()
+    return f.float().cpu(), gl.float().cpu(), ga.float().cpu()
+
+
+def _report(name, f, gl, ga, feat, yl, ya):
+    agree = (gl.argmax(1) == yl.argmax(1)).float().mean().item()
+    print(f"{name} B={B}: feat max|d| {(f - feat).abs().max():.3e} (|ref| max {feat.abs().max():.2f}), "
+          f"logits max|d| {(gl - yl).abs().max():.3e}, ant max|d| {(ga - ya).abs().max():.3e}, "
+          f"argmax agreement {agree:.4f}")
+    return agree
+
+
+def test_benched_config_fp32_b256(cuda, b256):
+    _, _, feat, yl, ya = b256
+    f, gl, ga = _run(cuda, b256, torch.float32)
+    _report("fp32", f, gl, ga, feat, yl, ya)
+    np.testing.assert_allclose(f.numpy(), feat.numpy(), rtol=0, atol=1e-3)
+    np.testing.assert_allclose(gl.numpy(), yl.numpy(), rtol=0, atol=1e-3)
+    np.testing.assert_allclose(ga.numpy(), ya.numpy(), rtol=0, atol=1e-3)
+    assert torch.equal(gl.argmax(1), yl.argmax(1))                     # argmax labels bit-exact
+
+
+def test_benched_config_fp16_b256(cuda, b256):
+    _, _, feat, yl, ya = b256
+    f, gl, ga = _run(cuda, b256, torch.float16)
+    agree = _report("fp16", f, gl, ga, feat, yl, ya)
+    assert torch.isfinite(f).all()
+    np.testing.assert_allclose(f.numpy(), feat.numpy(), rtol=0, atol=FP16_FEAT_ATOL)
+    np.testing.assert_allclose(gl.numpy(), yl.numpy(), rtol=0, atol=FP16_LOGIT_ATOL)
+    np.testing.assert_allclose(ga.numpy(), ya.numpy(), rtol=0, atol=FP16_LOGIT_ATOL)
+    assert agree >= FP16_ARGMAX_MIN
+
+
+def test_benched_config_bf16_b256(cuda, b256):
+    _, _, feat, yl, ya = b256
+    f, gl, ga = _run(cuda, b256, torch.bfloat16)
+    _report("bf16", f, gl, ga, feat, yl, ya)
+    np.testing.assert_allclose(f.numpy(), feat.numpy(), rtol=0, atol=5e-2)
+    np.testing.assert_allclose(gl.numpy(), yl.numpy(), rtol=0, atol=2e-2)
+
+
+def test_fp16_features_vs_reference_golden(cuda, golden):
+    """fp16 path against the vectors the reference itself produced (B = 2, with flow)."""
+    from models import mix_transformer_evp as mte
+    m = getattr(mte, VARIANT)()
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
+    m.svk_dtype = torch.float16
+    m = m.to(cuda).eval()
+    with torch.no_grad():
+        f = m(I.frames(2).to(cuda), I.segmaps(2).to(cuda), I.flow(2).to(cuda), return_features=True)
+        y, _ = m(I.frames(2).to(cuda), I.segmaps(2).to(cuda), I.flow(2).to(cuda))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(f.float().cpu().numpy(), golden[f"{VARIANT}_feat_flow"], rtol=0, atol=FP16_FEAT_ATOL)
+    np.testing.assert_allclose(y.float().cpu().numpy(), golden[f"{VARIANT}_logits_flow"], rtol=0, atol=FP16_LOGIT_ATOL)
+
+
+def test_autocast_fp16_region_selects_f16(cuda):
+    """Inside torch.autocast("cuda", float16) — the reference's inference/validation regions — the
+    modules compute in f16 (svk.default_dtype)."""
+    import svk
+    with torch.autocast("cuda", dtype=torch.float16):
+        assert svk.default_dtype() == torch.float16
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        assert svk.default_dtype() == torch.bfloat16
+    assert svk.default_dtype() == torch.float32

@@ -1,7 +1,7 @@
 """Per-kernel parity of the svk HIP kernels against plain torch CPU references (fp64 math on the
 same, dtype-rounded inputs).  Tolerances: f32 path (exact f32 MFMA products, f32 accumulation)
-rtol/atol 2e-5 relative to the output scale; bf16 path 1e-2 (inputs identical, outputs rounded to
-bf16 — 8 significant bits)."""
+rtol/atol 2e-5 relative to the output scale; bf16 path 1.2e-2 (inputs identical, outputs rounded to
+bf16 — 8 significant bits); f16 path 2.5e-3 (outputs rounded to f16 — 11 significant bits)."""
 import math
 
 import pytest
@@ -10,11 +10,12 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-DTS = [torch.float32, torch.bfloat16]
+DTS = [torch.float32, torch.bfloat16, torch.float16]
+H16 = [torch.bfloat16, torch.float16]
 
 
 def _tol(dt):
-    return (2e-5, 2e-5) if dt == torch.float32 else (1.2e-2, 1.2e-2)
+    return {torch.float32: (2e-5, 2e-5), torch.float16: (2.5e-3, 2.5e-3)}.get(dt, (1.2e-2, 1.2e-2))
 
 
 def _close(got, ref, dt, scale=None):
@@ -51,12 +52,12 @@ def test_gemm(cuda, dt, M, N, K, act):
                                            (3000, 136, 80, "gelu", False), (5000, 96, 200, "relu", True),
                                            (40000, 64, 256, None, True), (20001, 16, 16, None, False),
                                            (12544, 2048, 512, "tanh", False)])
-def test_gemm_persistent_bf16(cuda, M, N, K, act, res):
-    """bf16 plain-epilogue GEMMs run on the persistent LDS-DMA kernel (more tiles than resident
+@pytest.mark.parametrize("dt", H16)
+def test_gemm_persistent_16bit(cuda, M, N, K, act, res, dt):
+    """16-bit plain-epilogue GEMMs run on the persistent LDS-DMA kernel (more tiles than resident
     workgroups, K tails, M tails); checked against fp64 and against the tiled kernel (SVK_NO_PK)."""
     import os
     from svk import ops
-    dt = torch.bfloat16
     a = _rand(M, K, dt=dt, dev=cuda, seed=11)
     w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=12)
     b = _rand(N, dt=torch.float32, dev=cuda, seed=13)
@@ -106,11 +107,11 @@ def test_gemm_persistent_ext_bf16(cuda, M, N, K, uact):
 
 
 @pytest.mark.parametrize("cfg", [0, 10, 20, 30])
-def test_persistent_tile_configs(cuda, cfg):
+@pytest.mark.parametrize("dt", H16)
+def test_persistent_tile_configs(cuda, cfg, dt):
     """Every persistent-GEMM tile configuration (forced through svk_tune) on dense and implicit-GEMM
     shapes with M / N / K tails, staged and register epilogues."""
     from svk import ops
-    dt = torch.bfloat16
     try:
         ops.tune("pk_cfg", cfg)
         for M, N, K, res in ((5000, 320, 1280, True), (777, 136, 200, False), (12544, 512, 512, True)):
@@ -419,11 +420,11 @@ def test_conv2d_ln_sequence_reduction(cuda, dt, B, H, Cin, r):
 
 @pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (3, 28, 28, 128), (2, 14, 14, 128), (4, 7, 7, 64),
                                      (1, 9, 13, 32), (2, 30, 17, 64)])
-def test_mixffn_fc1_dwconv(cuda, B, H, W, C):
+@pytest.mark.parametrize("dt", H16)
+def test_mixffn_fc1_dwconv(cuda, B, H, W, C, dt):
     """fc1 -> dwconv3x3 -> GELU in one kernel (hidden kept on chip) against the unfused svk kernels
-    (fc1 GEMM, bf16 hidden, depthwise conv) and fp64 torch on the same bf16-rounded hidden."""
+    (fc1 GEMM, 16-bit hidden, depthwise conv) and fp64 torch on the same 16-bit-rounded hidden."""
     from svk import ops
-    dt = torch.bfloat16
     hid = 4 * C
     xn = _rand(B, H, W, C, dt=dt, dev=cuda, seed=81)
     w1 = _rand(hid, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=82)

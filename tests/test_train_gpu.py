@@ -491,3 +491,63 @@ def test_train_ddp_two_ranks_gloo(cuda):
     torch.testing.assert_close(a1, a0)
     torch.testing.assert_close(p1, p0)
     assert not torch.equal(l0, l1)                 # the ranks really saw different frames
+
+
+def _ddp_capture_rank(rank, world, port, out):
+    """Eager bucketed DDP iteration, then capture() + graph replay with the process group: no
+    collective is captured (BN broadcast and the two bucket all-reduces run eagerly between the three
+    graphs), so the replayed step must keep the ranks' parameters, gradients and BN buffers in sync."""
+    import os
+    import sys
+    import torch.distributed as dist
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "deep-learning-for-surgical-video-analysis_amd"), repo]
+    from models import mix_transformer_evp as mte
+    from svk.train import EVPTrainStep
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    m = mte.mit_b0_evp()
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
+    m = m.to(dev)
+    if rank == 1:
+        m.flow_encoder.bn2.running_var.mul_(3.0)
+    tr = EVPTrainStep(m, dtype=torch.bfloat16, drop=True, seed=rank, process_group=dist.group.WORLD, world_size=world)
+    assert 0 < tr.head_end < tr.n_trainable
+    x, y, fl, lab, at = (t.to(dev) for t in _train_inputs(2, 40 + rank))
+    tr.step(x, y, fl, lab, at)                     # eager: train_iteration (head bucket overlapped)
+    tr.capture(x, y, fl, lab, at)
+    assert tr.graph_rest is not None and tr.graph_opt is not None
+    flat1 = tr.flat.detach().clone()
+    loss, _, _ = tr.step(x, y, fl, lab, at)        # replay
+    loss, _, _ = tr.step(x, y, fl, lab, at)        # replay again
+    torch.cuda.synchronize()
+    v_own = m.flow_encoder.bn2.running_var.clone()  # this rank's own batch statistics went in last
+    tr.sync_buffers()                              # what the next step starts with: rank 0's buffers
+    torch.cuda.synchronize()
+    out[rank] = (flat1.cpu(), tr.flat.detach().cpu(), tr.grad.cpu(), m.flow_encoder.bn2.running_var.cpu(),
+                 loss.cpu(), tr.steps, v_own.cpu())
+    dist.destroy_process_group()
+
+
+def test_train_ddp_two_ranks_capture_replay(cuda):
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = mp.Manager().dict()
+    mp.spawn(_ddp_capture_rank, args=(2, port, out), nprocs=2, join=True)
+    (f0, p0, g0, v0, l0, n0, o0), (f1, p1, g1, v1, l1, n1, o1) = out[0], out[1]
+    assert n0 == n1 == 3
+    torch.testing.assert_close(f1, f0)
+    torch.testing.assert_close(p1, p0)             # identical parameters after two replayed steps
+    torch.testing.assert_close(g1, g0)             # averaged gradients
+    assert not torch.equal(p0, f0)                 # the replays really stepped
+    assert not torch.equal(o0, o1)                 # each rank's BN update used its own frames ...
+    torch.testing.assert_close(v1, v0)             # ... and the per-step broadcast re-syncs them from rank 0
+    torch.testing.assert_close(v0, o0)
+    assert torch.isfinite(l0).all() and not torch.equal(l0, l1)
