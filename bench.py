@@ -14,9 +14,12 @@ Multi-GPU: one process per GPU (torchrun); units shard across ranks with no data
 (SURVEY.md §8(e)): weak scaling, value = all ranks' units / the slowest rank's time.  Rank 0
 prints ONE JSON line.
 
-Roofline: the dominant kernel (the MFMA GEMM / implicit-GEMM conv instantiation with the most
-device time) is timed live with HIP events around each of its launches inside the timed region;
-achieved = its algorithmic 2*M*N*K flops / its measured time.  cpu_baseline: the oracle (the
+The extraction and train steps replay as HIP graphs (svk.graphs.GraphedForward / EVPTrainStep.capture):
+the timed region is graph launches only, no instrumentation.  Roofline: the dominant kernel (the MFMA
+GEMM / implicit-GEMM conv instantiation with the most device time) is timed with HIP events around each
+of its launches on eager iterations of the same step run right after the timed region (identical
+launches); achieved = its algorithmic flops or bytes / its measured time; the rocprofv3 summaries in
+profiles/ time the graph-replayed launches themselves.  cpu_baseline: the oracle (the
 reference's op graph restated on torch CPU ops, fp32) on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
@@ -167,11 +170,22 @@ def workload_extract(args, dev, rank, dtype):
     if args.no_flow:
         fl = None
 
-    def step():
+    def eager():
         return model(x, y, fl, return_features=True)
 
+    if args.no_graph:
+        step = eager
+    else:
+        from svk.graphs import GraphedForward
+        graphed = GraphedForward(model, x, y, fl, return_features=True)   # one graph launch per batch
+
+        def step():
+            return graphed()
+
+        step.profile = eager
+
     def set_dtype(dt):
-        model.svk_dtype = dt
+        model.svk_dtype = dt                   # GraphedForward re-captures on the next call
 
     step.set_dtype = set_dtype
 
@@ -181,7 +195,7 @@ def workload_extract(args, dev, rank, dtype):
     config = {"workload": f"generate_evp_LFB feature extraction: {args.variant} + "
                           f"{'no flow' if args.no_flow else 'optical-flow cross-attn fusion'}, "
                           f"224x224, return_features -> [B, 2048]",
-              "model": args.variant, "per_gpu_batch": args.batch}
+              "model": args.variant, "per_gpu_batch": args.batch, "hip_graph": not args.no_graph}
     return step, args.batch, config, check, (lambda: cpu_baseline_extract(args.variant, args.cpu_baseline_seconds))
 
 
@@ -410,7 +424,8 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-gemm", default=None, help="write per-shape GEMM timings to this file (rank 0)")
-    ap.add_argument("--no-graph", action="store_true", help="train: launch kernels eagerly instead of a HIP graph")
+    ap.add_argument("--no-graph", action="store_true", help="extract / train: launch kernels eagerly instead of "
+                                                           "replaying the step as a HIP graph")
     args = ap.parse_args(argv)
     if args.batch is None:
         args.batch = 88 if args.workload == "train" else 256      # train_evp.py:28 / extraction chunk
@@ -466,19 +481,17 @@ def main():
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
+        out, elapsed = timed(step, args.steps, world)      # the measured region: no instrumentation
+        check(out)
+        # roofline: HIP events around every GEMM / conv launch on separate (untimed) iterations of the
+        # same step (graph-replayed steps make no host calls: their eager twin, identical launches)
         records = []
         ops.set_profiler(records)
-        out, elapsed = timed(step, args.steps, world)
-        prof_steps = args.steps
-        if not records and hasattr(step, "profile"):
-            # graph-replayed steps make no host calls: time the kernels on eager iterations of the same
-            # step instead (identical launches, HIP events around each GEMM on its stream)
-            prof_steps = max(1, min(args.steps, 3))
-            for _ in range(prof_steps):
-                step.profile()
-            torch.cuda.synchronize()
+        prof_steps = max(1, min(args.steps, 5))
+        for _ in range(prof_steps):
+            (step.profile if hasattr(step, "profile") else step)()
+        torch.cuda.synchronize()
         ops.set_profiler(None)
-        check(out)
         # the same inputs at the other compute dtypes (extraction): fp32 is the precision of the
         # reference's generate_evp_LFB.py, bf16 the narrower 16-bit format
         other = {}

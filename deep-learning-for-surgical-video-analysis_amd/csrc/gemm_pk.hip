@@ -51,6 +51,10 @@ struct PkCfg {
   static constexpr int A_LD = A_BYTES / (NT * 16);   // DMA instructions per thread per K-step
   static constexpr int B_LD = B_BYTES / (NT * 16);
   static constexpr int LD = A_LD + B_LD;
+  // resident workgroups per CU the register budget is held to (LDS allows 3 for 128x64 / 64x128, 2 for
+  // 128x128): without the bound the f16 epilogue's conversions cost hipcc ~20-40 more VGPRs than the
+  // bf16 one and drop a workgroup per CU
+  static constexpr int OCC = BM * BN <= 64 * 64 ? 5 : (BM * BN <= 128 * 64 ? 3 : 2);
   static_assert(A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "tile must split into whole DMA rounds");
   static_assert(LD * (NSTAGE - 1) <= 63, "vmcnt range");
 };
@@ -97,7 +101,8 @@ __device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current
 // epilogue stores raw f32 partial sums to slab part (p.slab + (part * M + m) * N + n) and a separate
 // reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
 template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
-__global__ __launch_bounds__(Cfg::NT) void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
+__global__ __launch_bounds__(Cfg::NT, EXT ? (Cfg::OCC > 2 ? Cfg::OCC - 1 : 1) : Cfg::OCC)
+void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   typedef v8_t<T> tx8;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
