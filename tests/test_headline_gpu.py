@@ -6,8 +6,9 @@ Bars (north star: logits within 1e-3 at fp32, argmax labels bit-exact):
     1e-3 absolute, phase argmax identical for all 256 frames.
   * fp16 (the headline dtype; the precision of the reference's torch.autocast(float16) inference and
     validation passes, train_evp.py:637/760): f16 storage, f32 accumulation / statistics.  Features
-    within FP16_FEAT_ATOL absolute, logits within FP16_LOGIT_ATOL, phase-argmax agreement >=
-    FP16_ARGMAX_MIN over the 256 frames (measured values are printed; profiles/r02/precision_b256.txt).
+    within FP16_FEAT_ATOL absolute, both logit heads within FP16_LOGIT_ATOL = 1e-3 (the north-star bar)
+    and the phase argmax identical for all 256 frames (measured values are printed;
+    profiles/r02/precision_b256.txt).
   * bf16 (extra key only): features within 5e-2, logits within 2e-2.
 """
 import numpy as np
@@ -20,9 +21,8 @@ pytestmark = pytest.mark.gpu
 
 B = 256
 VARIANT = "mit_b2_evp"
-FP16_FEAT_ATOL = 1e-2
-FP16_LOGIT_ATOL = 5e-3
-FP16_ARGMAX_MIN = 0.99
+FP16_FEAT_ATOL = 5e-3        # measured 2.3e-3 (|features| <= 2.84)
+FP16_LOGIT_ATOL = 1e-3       # the north-star logit bar; measured 5.3e-4 (phase) / 8.2e-4 (anticipation)
 
 
 def _head_logits(feat, sd):
@@ -84,7 +84,7 @@ def test_benched_config_fp16_b256(cuda, b256):
     np.testing.assert_allclose(f.numpy(), feat.numpy(), rtol=0, atol=FP16_FEAT_ATOL)
     np.testing.assert_allclose(gl.numpy(), yl.numpy(), rtol=0, atol=FP16_LOGIT_ATOL)
     np.testing.assert_allclose(ga.numpy(), ya.numpy(), rtol=0, atol=FP16_LOGIT_ATOL)
-    assert agree >= FP16_ARGMAX_MIN
+    assert agree == 1.0 and torch.equal(gl.argmax(1), yl.argmax(1))
 
 
 def test_benched_config_bf16_b256(cuda, b256):
@@ -119,3 +119,27 @@ def test_autocast_fp16_region_selects_f16(cuda):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         assert svk.default_dtype() == torch.bfloat16
     assert svk.default_dtype() == torch.float32
+
+
+def test_graphed_forward_matches_eager_and_recaptures(cuda):
+    """svk.graphs.GraphedForward (bench.py's extraction step): graph replay == eager forward, new inputs
+    through run(), and a parameter update or dtype switch triggers a re-capture."""
+    from models import mix_transformer_evp as mte
+    from svk.graphs import GraphedForward
+    m = mte.mit_b0_evp()
+    m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
+    m.svk_dtype = torch.float16
+    m = m.to(cuda).eval()
+    x, y, fl = I.frames(4, 5).to(cuda), I.segmaps(4, 5).to(cuda), I.flow(4, 5).to(cuda)
+    gf = GraphedForward(m, x.clone(), y.clone(), fl.clone())
+    with torch.no_grad():
+        ref = m(x, y, fl, return_features=True)
+        torch.testing.assert_close(gf().clone(), ref, rtol=0, atol=0)
+        x2, y2, f2 = I.frames(4, 6).to(cuda), I.segmaps(4, 6).to(cuda), I.flow(4, 6).to(cuda)
+        torch.testing.assert_close(gf.run(x2, y2, f2).clone(), m(x2, y2, f2, return_features=True), rtol=0, atol=0)
+        g0 = gf.graph
+        m.head.linear_fuse.conv.weight.mul_(0.5)             # bumps the parameter version
+        torch.testing.assert_close(gf.run(x, y, fl).clone(), m(x, y, fl, return_features=True), rtol=0, atol=0)
+        assert gf.graph is not g0
+        m.svk_dtype = torch.float32
+        torch.testing.assert_close(gf().clone(), m(x, y, fl, return_features=True), rtol=0, atol=0)
