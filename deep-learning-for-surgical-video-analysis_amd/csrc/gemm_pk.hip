@@ -86,6 +86,18 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 __device__ __forceinline__ void barrier_mem() { asm volatile("s_barrier" ::: "memory"); }
+// Epilogue operand loads hidden from hipcc's waitcnt pass (see epi_load): completion is covered by the
+// counted wait of the tile's last step.
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gload16(f32x4& v, const char* src) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(src) : "memory");
+}
+__device__ __forceinline__ void gload8(u32x2& v, const char* src) {
+  asm volatile("global_load_dwordx2 %0, %1, off" : "=v"(v) : "v"(src) : "memory");
+}
+__device__ __forceinline__ void gload4(float& v, const char* src) {
+  asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(src) : "memory");
+}
 
 template <int LD>
 __device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current stage landed
@@ -200,18 +212,58 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
     }
   };
 
-  // The bias is loaded BEFORE the tile's last K-step so that its latency hides behind the MFMAs;
-  // the residual is loaded at the start of the epilogue (all loads first, then the math) — holding
-  // it across the last step would cost 2 VGPRs per accumulator block and halve the occupancy.
+  // Epilogue operands (bias, residual, and for EXT the activation-backward source and the row scale)
+  // are loaded BEFORE the tile's last K-step, so their latency hides behind that step's DMA wait and
+  // MFMAs.  They are issued from inline asm like the DMA: a compiler-visible global_load would make
+  // hipcc's waitcnt pass (which cannot see the asm DMA) insert s_waitcnt vmcnt(0) before the next
+  // reuse of its registers — draining the NEXT tile's prefetch at every tile.  Being older than that
+  // prefetch, they are covered by the last step's counted wait (wait_dma), after which tie_epi()
+  // hands the registers back to the compiler.  Absent operands read the zero block (no branches).
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
-  float4 ebias[TN];
+  f32x4 ebias[TN];
+  u32x2 eres[TM][TN], eu[EXT ? TM : 1][EXT ? TN : 1];
+  float ers[EXT ? TM : 1];
   const T* R = static_cast<const T*>(p.R);
   auto epi_load = [&](int unit) {
-    const int n0 = ((SPLIT ? unit / ks : unit) % ntn) * BN;
+    if constexpr (!SPLIT) {
+      const int m0 = (unit / ntn) * BM, n0 = (unit % ntn) * BN;
+      const char* zero = reinterpret_cast<const char*>(g_pk_zero);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
+        gload16(ebias[j], p.bias ? reinterpret_cast<const char*>(p.bias + n) : zero);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+          gload8(eres[i][j], R ? reinterpret_cast<const char*>(R + (long)m * p.ldr + n) : zero);
+          if constexpr (EXT) {
+            const T* U = static_cast<const T*>(p.U);
+            gload8(eu[i][j], U ? reinterpret_cast<const char*>(U + (long)m * p.ldu + n) : zero);
+          }
+        }
+      }
+      if constexpr (EXT) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+          gload4(ers[i], p.rscale ? reinterpret_cast<const char*>(p.rscale + m / p.rdiv) : zero);
+        }
+      }
+    }
+  };
+  auto tie_epi = [&]() {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
-      ebias[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+      asm volatile("" : "+v"(ebias[j]));
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        asm volatile("" : "+v"(eres[i][j]));
+        if constexpr (EXT) asm volatile("" : "+v"(eu[i][j]));
+      }
+    }
+    if constexpr (EXT) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(ers[i]));
     }
   };
   constexpr int CPR = BN / 8;            // 16-byte chunks per staged output row
@@ -236,33 +288,11 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       return;
     }
     T* C = static_cast<T*>(p.C);
-    uint2 eres[TM][TN], eu[TM][TN];
-    float ers[TM];
-    if (R) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
-          const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
-          eres[i][j] = *reinterpret_cast<const uint2*>(R + (long)m * p.ldr + n);
-        }
-    }
     if constexpr (EXT) {
-      const T* U = static_cast<const T*>(p.U);
-      if (U) {
+      if (!p.rscale) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM; ++i) {
-            const int n = min(n0 + wn * WN + j * 16 + fq * 4, p.N - 4);
-            const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
-            eu[i][j] = *reinterpret_cast<const uint2*>(U + (long)m * p.ldu + n);
-          }
+        for (int i = 0; i < TM; ++i) ers[i] = 1.f;
       }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        ers[i] = p.rscale ? p.rscale[min(m0 + wm * WM + i * 16 + fr, p.M - 1) / p.rdiv] : 1.f;
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -286,7 +316,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
         }
-        if (R) {
+        {                                  // zero block when there is no residual
           const f32x2 r01 = unpack2<T>(eres[i][j].x), r23 = unpack2<T>(eres[i][j].y);
           v[0] += r01.x;
           v[1] += r01.y;
@@ -337,9 +367,10 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   };
   // One pipeline step: top up the DMA ring (into the stage computed one step ago), wait for the
   // oldest stage `buf`, compute from it.
-  auto step = [&]() {
+  auto step = [&](bool last) {
     issue_next();
     wait_dma<Cfg::LD>(inflight - 1);   // steps in flight beyond the current one may stay outstanding
+    if (last) tie_epi();               // the epilogue loads (older than the prefetch) have landed too
     barrier_mem();
     compute(buf);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -351,9 +382,9 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) issue_next();
   for (int tile = first; tile < ntiles; tile += G) {
-    for (int kt = 0; kt < nk - 1; ++kt) step();
-    epi_load(tile);                   // bias / residual loads fly during the last step's MFMAs
-    step();
+    for (int kt = 0; kt < nk - 1; ++kt) step(false);
+    epi_load(tile);                   // epilogue operands fly during the last step's wait and MFMAs
+    step(true);
     switch (EXT ? p.uact : p.act) {
       case SVK_ACT_GELU: epilogue(tile, std::integral_constant<int, SVK_ACT_GELU>{}); break;
       case SVK_ACT_RELU: epilogue(tile, std::integral_constant<int, SVK_ACT_RELU>{}); break;

@@ -58,7 +58,8 @@ __global__ __launch_bounds__(256) void mamba_scan_kernel(const float* __restrict
                                                          const float* __restrict__ Wdt, const float* __restrict__ bdt,
                                                          const float* __restrict__ A, const float* __restrict__ Dp,
                                                          float* __restrict__ Y, float* __restrict__ HS,
-                                                         float* __restrict__ DS, int T, int Di, int R, int seg) {
+                                                         float* __restrict__ DS, int T, int Di, int R, int seg,
+                                                         float* __restrict__ Yss) {
   constexpr int CPW = 64 / NS;           // channels per wave
   constexpr int CPB = 4 * CPW;           // channels per workgroup
   constexpr int XW = MB_RMAX + 2 * NS + 1;
@@ -156,7 +157,9 @@ __global__ __launch_bounds__(256) void mamba_scan_kernel(const float* __restrict
 #pragma unroll 16
           for (int k = 0; k < NS; ++k) s += P[OUT ? wave : 0][lane][c * NS + k];
           const float zv = Z[row * ldz + d2];
-          Y[row * Di + d2] = (s + uu[wave * CPW + c][lane] * Dp[d2]) * (zv / (1.f + __expf(-zv)));
+          const float ys = s + uu[wave * CPW + c][lane] * Dp[d2];
+          Y[row * Di + d2] = ys * (zv / (1.f + __expf(-zv)));
+          if (Yss) Yss[row * Di + d2] = ys;        // training: the pre-gate output for the z-gate backward
         }
       }
     } else {
@@ -192,9 +195,9 @@ extern "C" int svk_mamba_conv_silu(const float* X, long ldx, const float* W, con
   return check_launch("mamba_conv_silu");
 }
 
-extern "C" int svk_mamba_scan(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
-                              const float* bdt, const float* A, const float* Dp, float* Y, int B, int T, int Di,
-                              int N, int R, int seg_len, float* ws, void* stream) {
+static int mamba_scan_launch(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
+                             const float* bdt, const float* A, const float* Dp, float* Y, int B, int T, int Di,
+                             int N, int R, int seg_len, float* ws, float* Yss, void* stream) {
   if (B < 0 || T < 0 || Di <= 0 || R <= 0 || R > MB_RMAX || (N != 16 && N != 32 && N != 64) ||
       ldxd < R + 2 * N || ldz < Di || !U || !XD || !Z || !Wdt || !bdt || !A || !Dp || !Y || seg_len <= 0 ||
       (seg_len < T && (seg_len % MB_TC != 0 || !ws))) {
@@ -214,15 +217,29 @@ extern "C" int svk_mamba_scan(const float* U, const float* XD, long ldxd, const 
   do {                                                                                                          \
     if (S > 1)                                                                                                  \
       hipLaunchKernelGGL((mamba_scan_kernel<NS, false>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt,  \
-                         A, Dp, Y, HS, DS, T, Di, R, seg);                                                      \
+                         A, Dp, Y, HS, DS, T, Di, R, seg, nullptr);                                             \
     hipLaunchKernelGGL((mamba_scan_kernel<NS, true>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A, \
-                       Dp, Y, HS, DS, T, Di, R, seg);                                                           \
+                       Dp, Y, HS, DS, T, Di, R, seg, Yss);                                                      \
   } while (0)
   if (N == 64) SVK_MAMBA_LAUNCH(64);
   else if (N == 32) SVK_MAMBA_LAUNCH(32);
   else SVK_MAMBA_LAUNCH(16);
 #undef SVK_MAMBA_LAUNCH
   return check_launch("mamba_scan");
+}
+
+extern "C" int svk_mamba_scan(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
+                              const float* bdt, const float* A, const float* Dp, float* Y, int B, int T, int Di,
+                              int N, int R, int seg_len, float* ws, void* stream) {
+  return mamba_scan_launch(U, XD, ldxd, Z, ldz, Wdt, bdt, A, Dp, Y, B, T, Di, N, R, seg_len, ws, nullptr, stream);
+}
+
+extern "C" int svk_mamba_scan_train(const float* U, const float* XD, long ldxd, const float* Z, long ldz,
+                                    const float* Wdt, const float* bdt, const float* A, const float* Dp, float* Y,
+                                    float* Yss, int B, int T, int Di, int N, int R, int seg_len, float* ws,
+                                    void* stream) {
+  if (!Yss) { set_error("svk_mamba_scan_train: Yss is required"); return SVK_EINVAL; }
+  return mamba_scan_launch(U, XD, ldxd, Z, ldz, Wdt, bdt, A, Dp, Y, B, T, Di, N, R, seg_len, ws, Yss, stream);
 }
 
 extern "C" long svk_mamba_scan_workspace(int B, int T, int Di, int N, int seg_len) {

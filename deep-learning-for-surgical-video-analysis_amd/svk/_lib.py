@@ -34,6 +34,14 @@ SIGNATURES = {
     "svk_mstcn_layer": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_mamba_conv_silu": [P, c_long, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_mamba_scan": [P, P, c_long, P, c_long, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P],
+    "svk_mamba_scan_train": [P, P, c_long, P, c_long, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P,
+                             P],
+    "svk_mamba_scan_bwd": [P, P, c_long, P, c_long, P, P, P, P, P, P, P, P, c_long, P, P, c_long, P, P, c_int, c_int,
+                           c_int, c_int, c_int, P, P],
+    "svk_mamba_conv_silu_bwd": [P, c_long, P, P, P, P, P, c_long, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mstcn_layer_train": [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mstcn_layer_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_softmax_rows_bwd": [P, c_long, P, c_long, P, c_long, c_int, c_int, P],
     "svk_frame_preproc": [P, P, P, P, P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
                           P],
     "svk_flow_preproc": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P],
@@ -75,7 +83,8 @@ SIGNATURES = {
 STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
 LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
               "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
-              "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int]}
+              "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int],
+              "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int]}
 
 _lib = None
 

@@ -136,6 +136,20 @@ int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C,
 int svk_mstcn_layer(const float* X, const float* Wd, const float* bd, const float* W1,
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
+/* Training (tecno.py:195-259 trains MultiStageModel_S with nn.Dropout(p = 0.5) active in every
+ * DilatedResidualLayer): Y = X + mask * (W1 relu(dilated conv) + b1) with mask values 0 or 1/keep;
+ * H [T, F] receives relu(pre) for the backward. */
+int svk_mstcn_layer_train(const float* X, const float* Wd, const float* bd, const float* W1, const float* b1,
+                          const float* mask, float* Y, float* H, int T, int F, int dilation, int causal, void* stream);
+/* Backward of svk_mstcn_layer_train: dX = dY + conv^T(dPre), dPre = relu'(H) * (mask * dY) W1 (written to
+ * the caller's dPre [T, F] scratch); dWd [3][F][F], dbd, dW1 [F][F], db1 += (f32 atomics: zero them). */
+int svk_mstcn_layer_bwd(const float* X, const float* H, const float* mask, const float* dY, const float* Wd,
+                        const float* W1, float* dPre, float* dX, float* dWd, float* dbd, float* dW1, float* db1,
+                        int T, int F, int dilation, int causal, void* stream);
+/* Backward of the inter-stage softmax (mstcn.py:126): dX = P * (dP - rowsum(P * dP)). */
+int svk_softmax_rows_bwd(const float* P, long ldp, const float* dP, long lddp, float* dX, long lddx, int M, int C,
+                         void* stream);
+
 /* CausalMambaModel (mstcn.py:282-343) block internals; the reference's Mamba is mamba_ssm's
  * `Mamba` (mamba_simple.py, imported at mstcn.py:9), absent from the reference snapshot.
  * Causal depthwise Conv1d (pad K-1, keep the first T outputs) + SiLU over B videos of T
@@ -156,6 +170,24 @@ int svk_mamba_scan(const float* U, const float* XD, long ldxd, const float* Z, l
  * segments (seg_len a multiple of 32) scanned concurrently in two passes; ws (caller-owned) holds
  * svk_mamba_scan_workspace(B, T, Di, N, seg_len) bytes of per-segment end states and delta sums. */
 long svk_mamba_scan_workspace(int B, int T, int Di, int N, int seg_len);
+/* svk_mamba_scan that also stores the pre-gate output Yss = sum_n C h + D u [B*T, Di] (training). */
+int svk_mamba_scan_train(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
+                         const float* bdt, const float* A, const float* Dp, float* Y, float* Yss, int B, int T,
+                         int Di, int N, int R, int seg_len, float* ws, void* stream);
+/* Selective-scan backward (tecno.py:256 loss.backward() through CausalMambaModel): from dOut [B*T, Di]
+ * -> dU, dZ (row stride lddz), dS = d(softplus input) [B*T, Di] (the dt projection's gradients are GEMMs
+ * on it), dXD columns R .. R+2N (dB | dC, += f32 atomics: zero them), dA (w.r.t. A = -exp(A_log)) [Di, N]
+ * and dD [Di] (+=).  ws: svk_mamba_scan_bwd_workspace() bytes (state checkpoints). */
+long svk_mamba_scan_bwd_workspace(int B, int T, int Di, int N);
+int svk_mamba_scan_bwd(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
+                       const float* bdt, const float* A, const float* Dp, const float* Yss, const float* dOut,
+                       float* dU, float* dZ, long lddz, float* dS, float* dXD, long lddxd, float* dA, float* dD,
+                       int B, int T, int Di, int N, int R, float* ws, void* stream);
+/* Backward of svk_mamba_conv_silu: dPre [B*T, Di] scratch, dX (row stride lddx) written, dW [Di, K] and
+ * db [Di] += (db may be NULL). */
+int svk_mamba_conv_silu_bwd(const float* X, long ldx, const float* W, const float* bias, const float* dY,
+                            float* dPre, float* dX, long lddx, float* dW, float* db, int B, int T, int Di, int K,
+                            void* stream);
 
 /* Frame preprocessing: generate_evp_LFB.py:243-247's Resize((OH, OW)) ->
  * CenterCrop -> ToTensor -> Normalize on decoded uint8 RGB frames [B, H, W, 3], bit-exact to Pillow's

@@ -12,9 +12,28 @@ import sys
 from collections import defaultdict
 
 
+_DEMANGLED = {}
+
+
+def demangle(name):
+    """Itanium-mangled kernel symbol -> C++ name (c++filt); unchanged when it is not mangled."""
+    if not name.startswith("_Z"):
+        return name
+    if name not in _DEMANGLED:
+        import subprocess
+        try:
+            # binutils' c++filt predates the _Float16 / __bf16 manglings: spell them as half / a vendor type
+            m = name.replace("DF16_", "Dh").replace("DF16b", "u6__bf16")
+            out = subprocess.run(["c++filt", m], capture_output=True, text=True).stdout.strip()
+            _DEMANGLED[name] = out.replace("half", "_Float16") if out and out != m else name
+        except OSError:
+            _DEMANGLED[name] = name
+    return _DEMANGLED[name]
+
+
 def kernel_key(name):
     """rocprofv3 kernel name -> the instantiation name bench.py reports (svk_last_kernel form)."""
-    n = name.strip()
+    n = demangle(name.strip())
     if n.startswith("void "):
         n = n[5:]
     n = n.replace("svk::", "")
