@@ -217,8 +217,8 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   // MFMAs.  They are issued from inline asm like the DMA: a compiler-visible global_load would make
   // hipcc's waitcnt pass (which cannot see the asm DMA) insert s_waitcnt vmcnt(0) before the next
   // reuse of its registers — draining the NEXT tile's prefetch at every tile.  Being older than that
-  // prefetch, they are covered by the last step's counted wait (wait_dma), after which tie_epi()
-  // hands the registers back to the compiler.  Absent operands read the zero block (no branches).
+  // prefetch, they are covered by the last step's counted wait (vector-memory operations, LDS-DMA
+  // included, retire in issue order), after which tie_epi() hands the registers back to the compiler.  Absent operands read the zero block (no branches).
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
   f32x4 ebias[TN];
   u32x2 eres[TM][TN], eu[EXT ? TM : 1][EXT ? TN : 1];
