@@ -123,9 +123,9 @@ __global__ __launch_bounds__(256) void mstcn_bwd_a(const float* __restrict__ X, 
       wp += pp * xs[2][k][ci];
     }
     atomicAdd(dW1 + e, w1);
-    atomicAdd(dWd + e, w0);
-    atomicAdd(dWd + F * F + e, wm);
-    atomicAdd(dWd + 2 * F * F + e, wp);
+    atomicAdd(dWd + 3 * e, w0);          // nn.Conv1d weight layout [F_out][F_in][3]
+    atomicAdd(dWd + 3 * e + 1, wm);
+    atomicAdd(dWd + 3 * e + 2, wp);
   }
   if (threadIdx.x < F) {
     const int fo = threadIdx.x;
@@ -169,14 +169,15 @@ __global__ __launch_bounds__(256) void mstcn_bwd_b(const float* __restrict__ dY,
 
 // softmax over C classes per row: backward dx = p * (dp - sum_c p dp)
 __global__ void softmax_rows_bwd_kernel(const float* __restrict__ P, long ldp, const float* __restrict__ dP, long lddp,
-                                        float* __restrict__ dX, long lddx, int M, int C) {
+                                        const float* __restrict__ R, long ldr, float* __restrict__ dX, long lddx, int M,
+                                        int C) {
   const long r = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= M) return;
   const float* p = P + r * ldp;
   const float* g = dP + r * lddp;
   float s = 0.f;
   for (int c = 0; c < C; ++c) s += p[c] * g[c];
-  for (int c = 0; c < C; ++c) dX[r * lddx + c] = p[c] * (g[c] - s);
+  for (int c = 0; c < C; ++c) dX[r * lddx + c] = p[c] * (g[c] - s) + (R ? R[r * ldr + c] : 0.f);
 }
 
 }  // namespace svk
@@ -230,13 +231,13 @@ extern "C" int svk_mstcn_layer_bwd(const float* X, const float* H, const float* 
   return check_launch("mstcn_layer_bwd");
 }
 
-extern "C" int svk_softmax_rows_bwd(const float* P, long ldp, const float* dP, long lddp, float* dX, long lddx, int M,
-                                    int C, void* stream) {
-  if (M < 0 || C <= 0 || !P || !dP || !dX || ldp < C || lddp < C || lddx < C) {
+extern "C" int svk_softmax_rows_bwd(const float* P, long ldp, const float* dP, long lddp, const float* R, long ldr,
+                                    float* dX, long lddx, int M, int C, void* stream) {
+  if (M < 0 || C <= 0 || !P || !dP || !dX || ldp < C || lddp < C || lddx < C || (R && ldr < C)) {
     set_error("svk_softmax_rows_bwd: bad args"); return SVK_EINVAL;
   }
   if (M == 0) return SVK_OK;
   hipLaunchKernelGGL(softmax_rows_bwd_kernel, dim3((M + 255) / 256), dim3(256), 0, (hipStream_t)stream, P, ldp, dP,
-                     lddp, dX, lddx, M, C);
+                     lddp, R, ldr, dX, lddx, M, C);
   return check_launch("softmax_rows_bwd");
 }

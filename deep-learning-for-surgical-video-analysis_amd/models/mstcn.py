@@ -18,7 +18,7 @@ import math
 import torch
 import torch.nn as nn
 
-from svk import ops
+from svk import ops, temporal
 from svk.pack import get_packed
 from ._common import check_inference
 
@@ -120,7 +120,10 @@ class MultiStageModel_S(nn.Module):
         return out
 
     def forward(self, x):
-        """x [B, f_dim, T] -> [stages, B, classes, T] (mstcn.py:122-130)."""
+        """x [B, f_dim, T] -> [stages, B, classes, T] (mstcn.py:122-130).  Train mode (tecno.py:195):
+        dropout active, forward/backward on the svk training kernels (svk.temporal)."""
+        if self.training:
+            return temporal.autograd_forward(self, x)
         check_inference(self, x)
         per = []
         for xb in x:                                   # batch of videos (the reference uses B = 1)
@@ -213,7 +216,9 @@ class CausalMambaModel(nn.Module):
     (``in_proj``, ``blocks.{i}`` = Mamba v1 blocks, ``dropout``, ``norm``, ``head``); the reference raises
     ImportError without ``mamba_ssm`` (mstcn.py:301-302) — this build carries its own selective-scan
     kernels instead.  Eval-mode forward: x [B, f_dim, T] -> [1, B, classes, T], all time-major f32:
-    in_proj GEMM, per block (GEMM, conv+SiLU, GEMM, scan, GEMM + residual), LayerNorm, head GEMM."""
+    in_proj GEMM, per block (GEMM, conv+SiLU, GEMM, scan, GEMM + residual), LayerNorm, head GEMM.
+    Train mode (tecno.py:153, 195): dropout after every block, forward and backward on the svk
+    training kernels (svk.temporal: selective-scan / conv+SiLU backward kernels, f32 MFMA GEMMs)."""
 
     def __init__(self, mstcn_stages, mstcn_layers, mstcn_f_maps, mstcn_f_dim, out_features, mstcn_causal_conv,
                  mamba_d_state=64, mamba_d_conv=4, mamba_expand=2, mamba_dropout=0.1):
@@ -245,6 +250,8 @@ class CausalMambaModel(nn.Module):
                     b=f(self.norm.bias), w_h=f(self.head.weight), b_h=f(self.head.bias))
 
     def forward(self, x):
+        if self.training:                                                 # tecno.py:195 (svk.temporal)
+            return temporal.autograd_forward(self, x)
         check_inference(self, x)
         B, C, T = x.shape
         p = get_packed(self, torch.float32, self._pack)

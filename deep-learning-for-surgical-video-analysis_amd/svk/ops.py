@@ -442,6 +442,122 @@ def mamba_scan(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
     return out
 
 
+# ---- temporal-model training (tecno.py:195-259) ------------------------------------------------------
+
+def mstcn_layer_train(x, wd_packed, bd, w1, b1, dilation, causal, mask, out=None, hidden=None):
+    """DilatedResidualLayer train forward: out = x + mask * (w1 relu(dilated conv) + b1); ``hidden``
+    [T, F] receives relu(pre) for the backward.  mask [T, F] f32 (0 or 1/keep)."""
+    for t, nm in ((x, "x"), (wd_packed, "wd"), (bd, "bd"), (w1, "w1"), (b1, "b1"), (mask, "mask")):
+        _chk(t, nm, torch.float32)
+    T, F = x.shape
+    if mask.numel() != T * F or not (x.is_contiguous() and mask.is_contiguous()):
+        raise _lib.SvkError("svk.mstcn_layer_train: x / mask must be contiguous [T, F]")
+    out = torch.empty_like(x) if out is None else out
+    hidden = torch.empty_like(x) if hidden is None else hidden
+    _lib.call("svk_mstcn_layer_train", _p(x), _p(wd_packed), _p(bd), _p(w1), _p(b1), _p(mask), _p(out), _p(hidden),
+              T, F, dilation, 1 if causal else 0, _stream())
+    return out, hidden
+
+
+def mstcn_layer_bwd(x, hidden, mask, dy, wd_packed, w1, dwd, dbd, dw1, db1, dilation, causal, dx=None, scratch=None):
+    """Backward of mstcn_layer_train: returns dx; dwd [F, F, 3] (nn.Conv1d layout) / dbd / dw1 [F, F] / db1 += (f32)."""
+    for t, nm in ((x, "x"), (hidden, "hidden"), (mask, "mask"), (dy, "dy"), (wd_packed, "wd"), (w1, "w1"),
+                  (dwd, "dwd"), (dbd, "dbd"), (dw1, "dw1"), (db1, "db1")):
+        _chk(t, nm, torch.float32)
+        if not t.is_contiguous():
+            raise _lib.SvkError(f"svk.mstcn_layer_bwd: {nm} must be contiguous")
+    T, F = x.shape
+    dx = torch.empty_like(x) if dx is None else dx
+    scratch = torch.empty_like(x) if scratch is None else scratch
+    _lib.call("svk_mstcn_layer_bwd", _p(x), _p(hidden), _p(mask), _p(dy), _p(wd_packed), _p(w1), _p(scratch), _p(dx),
+              _p(dwd), _p(dbd), _p(dw1), _p(db1), T, F, dilation, 1 if causal else 0, _stream())
+    return dx
+
+
+def softmax_rows_bwd(p, dp, residual=None, out=None):
+    """dX = P * (dP - rowsum(P * dP)) (+ residual) over [M, C] f32."""
+    _chk(p, "p", torch.float32); _chk(dp, "dp", torch.float32); _chk(residual, "residual", torch.float32)
+    M, C, ldp = _rows(p, "p")
+    _, _, lddp = _rows(dp, "dp")
+    ldr = _rows(residual, "residual")[2] if residual is not None else 0
+    out = torch.empty(M, C, device=p.device, dtype=torch.float32) if out is None else out
+    _, _, ldo = _rows(out, "out")
+    _lib.call("svk_softmax_rows_bwd", _p(p), ldp, _p(dp), lddp, _p(residual), ldr, _p(out), ldo, M, C, _stream())
+    return out
+
+
+def neg_exp(x, out=None):
+    _chk(x, "x", torch.float32)
+    out = torch.empty_like(x) if out is None else out
+    if not (x.is_contiguous() and out.is_contiguous()) or out.numel() != x.numel():
+        raise _lib.SvkError("svk.neg_exp: contiguous equal-size tensors required")
+    _lib.call("svk_neg_exp", _p(x), _p(out), x.numel(), _stream())
+    return out
+
+
+def mamba_scan_train(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
+    """mamba_scan that also returns the pre-gate output yss = sum_n C h + D u (for the backward)."""
+    for t, nm in ((u, "u"), (xdbl, "xdbl"), (z, "z"), (w_dt, "w_dt"), (b_dt, "b_dt"), (a_neg, "A"),
+                  (d_skip, "D")):
+        _chk(t, nm, torch.float32)
+    M, Di, ldu = _rows(u, "u")
+    Mx, W, ldxd = _rows(xdbl, "xdbl")
+    Mz, Dz, ldz = _rows(z, "z")
+    Dn, N = a_neg.shape
+    R = w_dt.shape[1]
+    if (M != B * T or Mx != M or Mz != M or Dz != Di or ldu != Di or Dn != Di or W != R + 2 * N
+            or not (w_dt.is_contiguous() and a_neg.is_contiguous())):
+        raise _lib.SvkError("svk.mamba_scan_train: shape mismatch")
+    out = torch.empty(M, Di, device=u.device, dtype=torch.float32)
+    yss = torch.empty(M, Di, device=u.device, dtype=torch.float32)
+    seg = mamba_seg_len(B, T, Di, N) if seg_len is None else int(seg_len)
+    nws = _lib.load().svk_mamba_scan_workspace(B, T, Di, N, seg)
+    ws = torch.empty(nws // 4, device=u.device, dtype=torch.float32) if nws > 0 else None
+    _lib.call("svk_mamba_scan_train", _p(u), _p(xdbl), ldxd, _p(z), ldz, _p(w_dt), _p(b_dt), _p(a_neg), _p(d_skip),
+              _p(out), _p(yss), B, T, Di, N, R, seg, _p(ws), _stream())
+    return out, yss
+
+
+def mamba_scan_bwd(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, yss, dout, dz, dxdbl, da, dd, B, T):
+    """Selective-scan backward.  Returns (du, ds) [B*T, Di]; writes dz (a [B*T, Di] view, any row stride);
+    dxdbl[:, R:] (the dB | dC columns) += and da [Di, N] / dd [Di] += (zero them first)."""
+    for t, nm in ((u, "u"), (xdbl, "xdbl"), (z, "z"), (w_dt, "w_dt"), (b_dt, "b_dt"), (a_neg, "A"),
+                  (d_skip, "D"), (yss, "yss"), (dout, "dout"), (dz, "dz"), (dxdbl, "dxdbl"), (da, "da"), (dd, "dd")):
+        _chk(t, nm, torch.float32)
+    M, Di, ldu = _rows(u, "u")
+    _, W, ldxd = _rows(xdbl, "xdbl")
+    _, _, ldz = _rows(z, "z")
+    _, _, lddz = _rows(dz, "dz")
+    _, Wd, lddxd = _rows(dxdbl, "dxdbl")
+    Dn, N = a_neg.shape
+    R = w_dt.shape[1]
+    if (M != B * T or ldu != Di or W != R + 2 * N or Wd != W or not (yss.is_contiguous() and dout.is_contiguous())
+            or yss.numel() != M * Di or dout.numel() != M * Di or not (da.is_contiguous() and dd.is_contiguous())):
+        raise _lib.SvkError("svk.mamba_scan_bwd: shape mismatch")
+    du = torch.empty(M, Di, device=u.device, dtype=torch.float32)
+    ds = torch.empty(M, Di, device=u.device, dtype=torch.float32)
+    nws = _lib.load().svk_mamba_scan_bwd_workspace(B, T, Di, N)
+    ws = torch.empty(max(nws // 4, 1), device=u.device, dtype=torch.float32)
+    _lib.call("svk_mamba_scan_bwd", _p(u), _p(xdbl), ldxd, _p(z), ldz, _p(w_dt), _p(b_dt), _p(a_neg), _p(d_skip),
+              _p(yss), _p(dout), _p(du), _p(dz), lddz, _p(ds), _p(dxdbl), lddxd, _p(da), _p(dd), B, T, Di, N, R,
+              _p(ws), _stream())
+    return du, ds
+
+
+def mamba_conv_silu_bwd(x, w, bias, dy, dx, dw, db, B, T):
+    """Backward of mamba_conv_silu: writes dx (a [B*T, Di] view, any row stride); dw [Di, K] / db += ."""
+    for t, nm in ((x, "x"), (w, "w"), (bias, "bias"), (dy, "dy"), (dx, "dx"), (dw, "dw"), (db, "db")):
+        _chk(t, nm, torch.float32)
+    M, Di, ldx = _rows(x, "x")
+    _, _, lddx = _rows(dx, "dx")
+    if M != B * T or not (dy.is_contiguous() and w.is_contiguous() and dw.is_contiguous()) or dy.numel() != M * Di:
+        raise _lib.SvkError("svk.mamba_conv_silu_bwd: shape mismatch")
+    scratch = torch.empty(M, Di, device=x.device, dtype=torch.float32)
+    _lib.call("svk_mamba_conv_silu_bwd", _p(x), ldx, _p(w), _p(bias), _p(dy), _p(scratch), _p(dx), lddx, _p(dw),
+              _p(db), B, T, Di, w.shape[1], _stream())
+    return dx
+
+
 def window_unfold(x, length, pos=None):
     """x [T, C] -> [T, length, C] causal windows (zero left-pad) + pos[length, C]."""
     _chk(x, "x"); _chk(pos, "pos", torch.float32)
@@ -687,9 +803,11 @@ def bcast_rows(df, R, dtype, scale=1.0, mask=None):
     return out
 
 
-def mul_f32(a, b):
+def mul_f32(a, b, out=None):
     _chk(a, "a", torch.float32); _chk(b, "b", torch.float32)
-    out = torch.empty_like(a)
+    out = torch.empty_like(a) if out is None else out
+    if not (a.is_contiguous() and b.is_contiguous() and out.is_contiguous()) or not (a.numel() == b.numel() == out.numel()):
+        raise _lib.SvkError("svk.mul_f32: contiguous equal-size tensors required")
     _lib.call("svk_mul_f32", _p(a), _p(b), _p(out), a.numel(), _stream())
     return out
 
@@ -723,3 +841,46 @@ def sgd(p, g, buf, lr, momentum, dampening, wd, nesterov, first):
 
 def pack_params(desc, ndesc, total, src, dst):
     _lib.call("svk_pack_params", dtype_code(dst.dtype), _p(desc), ndesc, total, _p(src), _p(dst), _stream())
+
+
+def tecno_loss(logits, labels, ant_targets, class_w=None, out=None, dlogits=None):
+    """tecno.py:237-254 loss over time-major logits [S, T, 2P] -> (loss f32 [3] = (clc, ant, #correct
+    of the last stage), dlogits [S, T, 2P] = d(clc + ant))."""
+    _chk(logits, "logits", torch.float32); _chk(labels, "labels", torch.int64)
+    _chk(ant_targets, "ant_targets", torch.float32); _chk(class_w, "class_w", torch.float32)
+    if logits.dim() != 3 or logits.stride(2) != 1:
+        raise _lib.SvkError("svk.tecno_loss: logits must be [S, T, 2P] with unit column stride")
+    S, T, C = logits.shape
+    P = C // 2
+    if C != 2 * P or labels.numel() != T or ant_targets.shape != (T, P) or not ant_targets.is_contiguous():
+        raise _lib.SvkError("svk.tecno_loss: shape mismatch")
+    out = torch.empty(3, device=logits.device, dtype=torch.float32) if out is None else out
+    dlogits = torch.empty_like(logits) if dlogits is None else dlogits
+    if dlogits.stride() != logits.stride():
+        raise _lib.SvkError("svk.tecno_loss: dlogits must share the logits layout")
+    _lib.call("svk_tecno_loss", _p(logits), logits.stride(1), logits.stride(0), S, T, P, _p(labels.contiguous()),
+              _p(ant_targets), _p(class_w), _p(out), _p(dlogits), _stream())
+    return out, dlogits
+
+
+NORM_PARTS = 256   # csrc/tecno_train.hip NORM_PARTS (svk_norm_parts())
+
+
+def grad_sqnorm(g, partials, step=None):
+    _chk(g, "g", torch.float32); _chk(partials, "partials", torch.float32); _chk(step, "step", torch.int64)
+    if partials.numel() < NORM_PARTS or not g.is_contiguous():
+        raise _lib.SvkError("svk.grad_sqnorm: partials must hold svk_norm_parts() floats, g contiguous")
+    _lib.call("svk_grad_sqnorm", _p(g), g.numel(), _p(partials), _p(step), _stream())
+
+
+def adamw(p, g, m, v, lr, step, partials=None, max_norm=0.0, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=1e-2):
+    """clip_grad_norm_(max_norm) (when partials from grad_sqnorm are given) + torch.optim.AdamW step over
+    flat f32 buffers; lr (f32 [1]) and step (int64 [1], already advanced) live on the device."""
+    for t, nm in ((p, "p"), (g, "g"), (m, "m"), (v, "v"), (lr, "lr"), (partials, "partials")):
+        _chk(t, nm, torch.float32)
+    _chk(step, "step", torch.int64)
+    n = p.numel()
+    if any(t.numel() != n or not t.is_contiguous() for t in (g, m, v)) or not p.is_contiguous():
+        raise _lib.SvkError("svk.adamw: p / g / m / v must be contiguous and equally sized")
+    _lib.call("svk_adamw", _p(p), _p(g), _p(m), _p(v), n, _p(partials), float(max_norm), _p(lr), float(beta1),
+              float(beta2), float(eps), float(weight_decay), _p(step), _stream())

@@ -1,0 +1,487 @@
+"""Training of the temporal models on the svk kernels — tecno.py:192-259 (and the MS-TCN variant it
+keeps commented at tecno.py:155).
+
+The reference trains ``CausalMambaModel`` / ``MultiStageModel_S`` one video per optimizer step: the
+video's LFB feature sequence [1, f_dim, T] -> per-stage logits, loss = mean over stages of weighted
+CrossEntropy (phase) + SmoothL1 (anticipation), backward, clip_grad_norm_(1.0), AdamW.  Here:
+
+* ``MSTCNTrainer`` / ``MambaTrainer`` own one flat f32 parameter buffer (the nn.Parameters become views
+  into it) and one flat gradient buffer, plus the derived layouts the kernels read (packed dilated-conv
+  taps, transposed weights for the data-gradient GEMMs, A = -exp(A_log)) refreshed by one gather launch
+  (``svk_pack_params``) + ``svk_neg_exp`` after every parameter update;
+* ``forward`` / ``backward`` are the explicit forward and backward over the svk kernels (time-major
+  [T, C] maps; dilated residual layers, selective scan and causal conv each with a hand-written
+  backward kernel; GEMMs and weight gradients on the f32 MFMA path); dropout masks come from the
+  counter-based ``svk_keep_mask``;
+* ``TemporalTrainStep`` chains forward, ``svk_tecno_loss``, backward, ``svk_grad_sqnorm`` and
+  ``svk_adamw`` (clip + AdamW, step count and learning rate on the device) and captures the whole
+  step in a HIP graph per sequence length (``step`` replays it);
+* the drop-in path: ``model.train(); y = model(x); loss.backward()`` in the reference's own loop runs
+  the same forward/backward through one autograd Function per model (``autograd_forward``).
+"""
+import torch
+from torch.autograd.graph import increment_version
+
+from . import ops
+from ._lib import SvkError
+from .train import _PackTable
+
+
+class _WS:
+    """Named, shape-checked device buffers (fixed addresses across calls: graph-capture friendly)."""
+
+    def __init__(self, device):
+        self.dev = device
+        self.bufs = {}
+
+    def get(self, name, shape, dtype=torch.float32, zero=False):
+        t = self.bufs.get(name)
+        if t is None or t.shape != tuple(shape) or t.dtype != dtype:
+            t = torch.empty(shape, device=self.dev, dtype=dtype)
+            self.bufs[name] = t
+        if zero:
+            t.zero_()
+        return t
+
+
+class _Flat:
+    """All parameters of ``model`` in one f32 buffer (``p.data`` re-pointed to views) + gradient buffer."""
+
+    def __init__(self, model):
+        named = list(model.named_parameters())
+        dev = named[0][1].device
+        if dev.type != "cuda":
+            raise SvkError("svk.temporal: the model must be on a GPU (there is no CPU path)")
+        self.dev = dev
+        al = lambda k: (k + 3) // 4 * 4          # every parameter starts 16-byte aligned (vector loads)
+        total = sum(al(p.numel()) for _, p in named)
+        self.flat = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=dev, dtype=torch.float32)
+        self.off, self.params = {}, {}
+        o = 0
+        with torch.no_grad():
+            for n, p in named:
+                k = p.numel()
+                self.flat[o:o + k].copy_(p.detach().reshape(-1))
+                p.data = self.flat[o:o + k].view_as(p)
+                self.off[n] = o
+                self.params[n] = p
+                o += al(k)
+        self.total = total
+        self._ptrs = {n: p.data_ptr() for n, p in self.params.items()}
+
+    def intact(self):
+        return all(p.data_ptr() == self._ptrs[n] for n, p in self.params.items())
+
+    def versions(self):
+        return tuple(p._version for p in self.params.values())
+
+    def P(self, name):
+        return self.params[name].detach()
+
+    def G(self, name):
+        p = self.params[name]
+        o = self.off[name]
+        return self.grad[o:o + p.numel()].view(p.shape)
+
+
+class _TrainerBase:
+    def __init__(self, model):
+        self.model = model
+        self.fl = _Flat(model)
+        self.dev = self.fl.dev
+        self.pt = _PackTable(torch.float32)
+        self._build_packs()
+        self.pt.finalize(self.dev)
+        self._negexp = []            # (A_log name, a_neg buffer)
+        self._post_packs()
+        self.refresh()
+
+    def _post_packs(self):
+        pass
+
+    def _T(self, name):
+        """Register a transposed [K, N] copy of the 2-D view of parameter ``name`` ([N, K, (1)])."""
+        p = self.fl.params[name]
+        N, K = p.shape[0], p.numel() // p.shape[0]
+        return self.pt.add(self.fl.off[name], (K, N), (1, K))
+
+    def refresh(self):
+        """Re-derive every packed layout from the flat parameters (after each update)."""
+        self.pt.run(self.fl.flat)
+        for name, buf in self._negexp:
+            ops.neg_exp(self.fl.P(name).reshape(-1), out=buf.view(-1))
+        self._ver = self.fl.versions()
+
+    def ensure_fresh(self):
+        if not self.fl.intact():
+            raise SvkError("svk.temporal: a parameter was re-allocated (model.to()/cuda() after the trainer was "
+                           "built); build a new trainer")
+        if self.fl.versions() != self._ver:
+            self.refresh()
+
+
+# ---------------------------------------------------------------------------------------------------
+class MSTCNTrainer(_TrainerBase):
+    """MultiStageModel_S (mstcn.py:94-130) with nn.Dropout(0.5) in every DilatedResidualLayer."""
+
+    KEEP = 0.5
+
+    def __init__(self, model):
+        self.S = model.num_stages
+        self.L = model.num_layers
+        self.F = model.num_f_maps
+        self.C = model.num_classes
+        self.causal = bool(model.causal_conv)
+        self.stage_names = ["stage1_phase"] + [f"stages.{s}" for s in range(self.S - 1)]
+        super().__init__(model)
+
+    def _build_packs(self):
+        self.k_wiT, self.k_woT, self.k_wd = [], [], []
+        F = self.F
+        for sn in self.stage_names:
+            self.k_wiT.append(self._T(f"{sn}.conv_1x1.weight"))
+            self.k_woT.append(self._T(f"{sn}.conv_out_classes.weight"))
+            ks = []
+            for l in range(self.L):
+                # conv_dilated.weight [F_out][F_in][3] -> [3][F_out][F_in]
+                ks.append(self.pt.add(self.fl.off[f"{sn}.layers.{l}.conv_dilated.weight"], (3, F, F), (1, 3 * F, 3)))
+            self.k_wd.append(ks)
+
+    def masks(self, T, seed, counter=None):
+        n = self.S * self.L * T * self.F
+        return ops.keep_mask(n, self.KEEP, seed, self.dev, counter).view(self.S, self.L, T, self.F)
+
+    def forward(self, x, masks, ws, out=None):
+        """x [T, f_dim] f32 time-major -> logits [S, T, C] (written into ``out`` if given)."""
+        P, pk = self.fl.P, self.pt.tensors
+        T = x.shape[0]
+        F, C = self.F, self.C
+        out = ws.get("out", (self.S, T, C)) if out is None else out
+        xin = x
+        self._xin = []
+        for s, sn in enumerate(self.stage_names):
+            self._xin.append(xin)
+            Din = xin.shape[1]
+            h = ops.gemm(xin, P(f"{sn}.conv_1x1.weight").view(F, Din), P(f"{sn}.conv_1x1.bias"),
+                         out=ws.get(f"h{s}_0", (T, F)))
+            for l in range(self.L):
+                lp = f"{sn}.layers.{l}"
+                h, _ = ops.mstcn_layer_train(h, pk[self.k_wd[s][l]], P(f"{lp}.conv_dilated.bias"),
+                                             P(f"{lp}.conv_1x1.weight").view(F, F), P(f"{lp}.conv_1x1.bias"), 2 ** l,
+                                             self.causal, masks[s, l], out=ws.get(f"h{s}_{l + 1}", (T, F)),
+                                             hidden=ws.get(f"H{s}_{l}", (T, F)))
+            ops.gemm(h, P(f"{sn}.conv_out_classes.weight").view(C, F), P(f"{sn}.conv_out_classes.bias"), out=out[s])
+            if s + 1 < self.S:
+                xin = ops.softmax_rows(out[s], out=ws.get(f"p{s}", (T, C)))
+        return out
+
+    def backward(self, dout, masks, ws, need_dx=False):
+        """dout [S, T, C] -> parameter gradients += into the flat gradient buffer; returns d x (or None)."""
+        P, G, pk = self.fl.P, self.fl.G, self.pt.tensors
+        S, F, C = self.S, self.F, self.C
+        T = dout.shape[1]
+        dnext = None
+        dx = None
+        for s in range(S - 1, -1, -1):
+            sn = self.stage_names[s]
+            g = dout[s]
+            if dnext is not None:
+                g = ops.softmax_rows_bwd(ws.bufs[f"p{s}"], dnext, residual=g, out=ws.get("gs", (T, C)))
+            hL = ws.bufs[f"h{s}_{self.L}"]
+            ops.gemm_wgrad(g, hL, G(f"{sn}.conv_out_classes.weight").view(C, F), G(f"{sn}.conv_out_classes.bias"))
+            dh = ops.gemm(g, pk[self.k_woT[s]], out=ws.get("dh_a", (T, F)))
+            other = "dh_b"
+            for l in range(self.L - 1, -1, -1):
+                lp = f"{sn}.layers.{l}"
+                dh = ops.mstcn_layer_bwd(ws.bufs[f"h{s}_{l}"], ws.bufs[f"H{s}_{l}"], masks[s, l], dh,
+                                         pk[self.k_wd[s][l]], P(f"{lp}.conv_1x1.weight").view(F, F),
+                                         G(f"{lp}.conv_dilated.weight"), G(f"{lp}.conv_dilated.bias"),
+                                         G(f"{lp}.conv_1x1.weight").view(F, F), G(f"{lp}.conv_1x1.bias"), 2 ** l,
+                                         self.causal, dx=ws.get(other, (T, F)), scratch=ws.get("dpre", (T, F)))
+                other = "dh_a" if other == "dh_b" else "dh_b"
+            xin = self._xin[s]
+            Din = xin.shape[1]
+            ops.gemm_wgrad(dh, xin, G(f"{sn}.conv_1x1.weight").view(F, Din), G(f"{sn}.conv_1x1.bias"))
+            if s > 0 or need_dx:
+                dnext = ops.gemm(dh, pk[self.k_wiT[s]], out=ws.get(f"dx{s}", (T, Din)))
+                if s == 0:
+                    dx = dnext
+        return dx
+
+
+# ---------------------------------------------------------------------------------------------------
+class MambaTrainer(_TrainerBase):
+    """CausalMambaModel (mstcn.py:282-343): in_proj, Mamba blocks with ``x = dropout(x + blk(x))``
+    (nn.Dropout(mamba_dropout)), LayerNorm, head."""
+
+    def __init__(self, model):
+        self.L = model.num_layers
+        self.Fm = model.num_f_maps
+        self.C = model.num_classes
+        self.keep = 1.0 - float(model.dropout.p)
+        blk = model.blocks[0] if self.L else None
+        self.Di = blk.d_inner if blk else 0
+        self.N = blk.d_state if blk else 0
+        self.R = blk.dt_rank if blk else 0
+        self.K = blk.d_conv if blk else 0
+        self.eps = float(model.norm.eps)
+        for b in model.blocks:
+            if b.in_proj.bias is not None or b.out_proj.bias is not None:
+                raise SvkError("svk.temporal: Mamba in_proj / out_proj with bias are not supported (mamba_ssm default: none)")
+        super().__init__(model)
+
+    def _build_packs(self):
+        self.k_inT = self._T("in_proj.weight")
+        self.k_headT = self._T("head.weight")
+        self.k_binT, self.k_xT, self.k_dtT, self.k_outT = [], [], [], []
+        for l in range(self.L):
+            p = f"blocks.{l}."
+            self.k_binT.append(self._T(p + "in_proj.weight"))
+            self.k_xT.append(self._T(p + "x_proj.weight"))
+            self.k_dtT.append(self._T(p + "dt_proj.weight"))
+            self.k_outT.append(self._T(p + "out_proj.weight"))
+
+    def _post_packs(self):
+        self.a_neg = []
+        for l in range(self.L):
+            buf = torch.empty(self.Di, self.N, device=self.dev, dtype=torch.float32)
+            self.a_neg.append(buf)
+            self._negexp.append((f"blocks.{l}.A_log", buf))
+
+    def masks(self, BT, seed, counter=None):
+        return ops.keep_mask(self.L * BT * self.Fm, self.keep, seed, self.dev, counter).view(self.L, BT, self.Fm)
+
+    def forward(self, x, B, T, masks, ws, out=None):
+        """x [B*T, f_dim] f32 time-major (row b*T + t) -> logits [B*T, C]."""
+        P = self.fl.P
+        BT = B * T
+        Fm, Di, N, R, K = self.Fm, self.Di, self.N, self.R, self.K
+        self._x = x
+        h = ops.gemm(x, P("in_proj.weight"), P("in_proj.bias"), out=ws.get("h0", (BT, Fm)))
+        for l in range(self.L):
+            p = f"blocks.{l}."
+            xz = ops.gemm(h, P(p + "in_proj.weight"), out=ws.get(f"xz{l}", (BT, 2 * Di)))
+            xc = ops.mamba_conv_silu(xz[:, :Di], P(p + "conv1d.weight").view(Di, K), P(p + "conv1d.bias"), B, T)
+            ws.bufs[f"xc{l}"] = xc
+            xdbl = ops.gemm(xc, P(p + "x_proj.weight"), out=ws.get(f"xdbl{l}", (BT, R + 2 * N)))
+            y, yss = ops.mamba_scan_train(xc, xdbl, xz[:, Di:], P(p + "dt_proj.weight"), P(p + "dt_proj.bias"),
+                                          self.a_neg[l], P(p + "D"), B, T)
+            ws.bufs[f"y{l}"], ws.bufs[f"yss{l}"] = y, yss
+            o = ops.gemm(y, P(p + "out_proj.weight"), residual=h, out=ws.get("o", (BT, Fm)))
+            h = ops.mul_f32(o, masks[l], out=ws.get(f"h{l + 1}", (BT, Fm)))
+        hn = ops.layernorm(h, P("norm.weight"), P("norm.bias"), self.eps, out=ws.get("hn", (BT, Fm)))
+        return ops.gemm(hn, P("head.weight"), P("head.bias"), out=ws.get("logits", (BT, self.C)) if out is None else out)
+
+    def backward(self, dlogits, B, T, masks, ws, need_dx=False):
+        P, G, pk = self.fl.P, self.fl.G, self.pt.tensors
+        BT = B * T
+        Fm, Di, N, R, K, C = self.Fm, self.Di, self.N, self.R, self.K, self.C
+        hn = ws.bufs["hn"]
+        ops.gemm_wgrad(dlogits, hn, G("head.weight"), G("head.bias"))
+        dhn = ops.gemm(dlogits, pk[self.k_headT], out=ws.get("dhn", (BT, Fm)))
+        dh = ops.layernorm_bwd(ws.bufs[f"h{self.L}"], dhn, P("norm.weight"), self.eps, out=ws.get("dh_a", (BT, Fm)),
+                               dgamma=G("norm.weight"), dbeta=G("norm.bias"))
+        other = "dh_b"
+        for l in range(self.L - 1, -1, -1):
+            p = f"blocks.{l}."
+            h_prev = ws.bufs[f"h{l}"]
+            xz, xc, xdbl = ws.bufs[f"xz{l}"], ws.bufs[f"xc{l}"], ws.bufs[f"xdbl{l}"]
+            do = ops.mul_f32(dh, masks[l], out=ws.get("do", (BT, Fm)))
+            ops.gemm_wgrad(do, ws.bufs[f"y{l}"], G(p + "out_proj.weight"))
+            dy = ops.gemm(do, pk[self.k_outT[l]], out=ws.get("dy", (BT, Di)))
+            dxz = ws.get("dxz", (BT, 2 * Di))
+            dxdbl = ws.get("dxdbl", (BT, R + 2 * N), zero=True)
+            dA = ws.get("dA", (Di, N), zero=True)
+            du, ds = ops.mamba_scan_bwd(xc, xdbl, xz[:, Di:], P(p + "dt_proj.weight"), P(p + "dt_proj.bias"),
+                                        self.a_neg[l], P(p + "D"), ws.bufs[f"yss{l}"], dy, dxz[:, Di:], dxdbl, dA,
+                                        G(p + "D"), B, T)
+            ops.mul_f32(dA, self.a_neg[l], out=G(p + "A_log"))                 # dA_log = dA * A
+            ops.gemm_wgrad(ds, xdbl[:, :R], G(p + "dt_proj.weight"), G(p + "dt_proj.bias"))
+            ops.gemm(ds, pk[self.k_dtT[l]], out=dxdbl[:, :R])
+            dxc = ops.gemm(dxdbl, pk[self.k_xT[l]], residual=du, out=ws.get("dxc", (BT, Di)))
+            ops.gemm_wgrad(dxdbl, xc, G(p + "x_proj.weight"))
+            ops.mamba_conv_silu_bwd(xz[:, :Di], P(p + "conv1d.weight").view(Di, K), P(p + "conv1d.bias"), dxc,
+                                    dxz[:, :Di], G(p + "conv1d.weight").view(Di, K), G(p + "conv1d.bias"), B, T)
+            ops.gemm_wgrad(dxz, h_prev, G(p + "in_proj.weight"))
+            dh = ops.gemm(dxz, pk[self.k_binT[l]], residual=do, out=ws.get(other, (BT, Fm)))
+            other = "dh_a" if other == "dh_b" else "dh_b"
+        ops.gemm_wgrad(dh, self._x, G("in_proj.weight"), G("in_proj.bias"))
+        if need_dx:
+            return ops.gemm(dh, pk[self.k_inT], out=ws.get("dx", (BT, self._x.shape[1])))
+        return None
+
+
+# ---------------------------------------------------------------------------------------------------
+def trainer_for(model):
+    t = model.__dict__.get("_svk_trainer")
+    if t is None or t.model is not model:
+        from models.mstcn import MultiStageModel_S, CausalMambaModel
+        if isinstance(model, MultiStageModel_S):
+            t = MSTCNTrainer(model)
+        elif isinstance(model, CausalMambaModel):
+            t = MambaTrainer(model)
+        else:
+            raise SvkError(f"svk.temporal: no trainer for {type(model).__name__}")
+        model.__dict__["_svk_trainer"] = t
+    return t
+
+
+def _seed():
+    return int(torch.randint(0, 2 ** 31 - 1, (1,)).item())
+
+
+class _TemporalFn(torch.autograd.Function):
+    """One autograd node for the whole temporal model: forward / backward on the svk kernels."""
+
+    @staticmethod
+    def forward(ctx, tr, x, *params):
+        tr.ensure_fresh()
+        ws = _WS(tr.dev)
+        B, Cin, T = x.shape
+        xt = x.transpose(1, 2).float().contiguous()                      # [B, T, f_dim] time-major
+        ctx.tr, ctx.ws, ctx.B, ctx.T, ctx.Cin = tr, ws, B, T, Cin
+        if isinstance(tr, MSTCNTrainer):
+            outs, masks = [], []
+            for b in range(B):                                             # the reference uses B = 1
+                wsb = ws if b == 0 else _WS(tr.dev)
+                m = tr.masks(T, _seed())
+                o = tr.forward(xt[b], m, wsb, out=torch.empty(tr.S, T, tr.C, device=tr.dev))
+                outs.append(o)
+                masks.append((wsb, m, tr._xin))
+            ctx.per = masks
+            tr.last_masks = [m for _, m, _ in masks]
+            out = torch.stack(outs, 1)                                     # [S, B, T, C]
+            return out.permute(0, 1, 3, 2)
+        m = tr.masks(B * T, _seed())
+        ctx.masks = m
+        tr.last_masks = m
+        logits = tr.forward(xt.view(B * T, Cin), B, T, m, ws, out=torch.empty(B * T, tr.C, device=tr.dev))
+        return logits.view(B, T, tr.C).permute(0, 2, 1).unsqueeze(0)
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gout):
+        tr = ctx.tr
+        tr.fl.grad.zero_()
+        need_dx = ctx.needs_input_grad[1]
+        dx = None
+        if isinstance(tr, MSTCNTrainer):
+            g = gout.permute(0, 1, 3, 2).float()                           # [S, B, T, C]
+            dxs = []
+            for b, (wsb, m, xin) in enumerate(ctx.per):
+                tr._xin = xin
+                d = tr.backward(g[:, b].contiguous(), m, wsb, need_dx=need_dx)
+                dxs.append(d)
+            if need_dx:
+                dx = torch.stack(dxs, 0).transpose(1, 2)
+        else:
+            B, T = ctx.B, ctx.T
+            g = gout[0].permute(0, 2, 1).float().contiguous().view(B * T, tr.C)
+            d = tr.backward(g, B, T, ctx.masks, ctx.ws, need_dx=need_dx)
+            if need_dx:
+                dx = d.view(B, T, ctx.Cin).transpose(1, 2)
+        grads = [tr.fl.G(n).clone() for n in tr.fl.params]
+        return (None, dx) + tuple(grads)
+
+
+def autograd_forward(model, x):
+    """Train-mode forward of MultiStageModel_S / CausalMambaModel through one autograd node."""
+    if not x.is_cuda:
+        raise SvkError(f"{type(model).__name__}: inputs must be on the GPU (got {x.device}); there is no CPU path")
+    tr = trainer_for(model)
+    return _TemporalFn.apply(tr, x, *tr.fl.params.values())
+
+
+# ---------------------------------------------------------------------------------------------------
+class TemporalTrainStep:
+    """One tecno.py optimizer step per call on one video (the reference's batch_size = 1):
+    forward, loss (tecno.py:237-254), backward, clip_grad_norm_(grad_clip), AdamW — all svk kernels,
+    captured into a HIP graph per sequence length T on first sight (``graphs=True``) and replayed.
+
+    Hyper-parameters default to tecno.py:100, 110-111, 162-168.  ``lr`` lives on the device
+    (``set_lr`` for ReduceLROnPlateau)."""
+
+    def __init__(self, model, class_weights=None, lr=1e-4, weight_decay=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                 grad_clip=1.0, seed=42, graphs=True):
+        model.train()
+        self.tr = trainer_for(model)
+        self.model = model
+        self.dev = self.tr.dev
+        n = self.tr.fl.total
+        self.m = torch.zeros(n, device=self.dev)
+        self.v = torch.zeros(n, device=self.dev)
+        self.lr = torch.full((1,), float(lr), device=self.dev)
+        self.step_t = torch.zeros(1, device=self.dev, dtype=torch.int64)
+        self.parts = torch.zeros(ops.NORM_PARTS, device=self.dev)
+        self.loss = torch.zeros(3, device=self.dev)
+        self.hp = dict(weight_decay=weight_decay, beta1=betas[0], beta2=betas[1], eps=eps, max_norm=grad_clip)
+        self.cw = None if class_weights is None else torch.as_tensor(class_weights, dtype=torch.float32).to(self.dev)
+        self.seed = int(seed)
+        self.graphs = graphs
+        self._g = {}        # T -> (graph, ws, static inputs)
+
+    def set_lr(self, lr):
+        self.lr.fill_(float(lr))
+
+    def _body(self, x, labels, ant, ws):
+        tr = self.tr
+        isms = isinstance(tr, MSTCNTrainer)
+        T = x.shape[0]
+        if isms:
+            masks = tr.masks(T, self.seed, self.step_t)
+            out = tr.forward(x, masks, ws)                                          # [S, T, C]
+        else:
+            masks = tr.masks(T, self.seed, self.step_t)
+            out = tr.forward(x, 1, T, masks, ws).view(1, T, tr.C)
+        _, dlog = ops.tecno_loss(out, labels, ant, self.cw, out=self.loss, dlogits=ws.get("dlogits", tuple(out.shape)))
+        tr.fl.grad.zero_()
+        if isms:
+            tr.backward(dlog, masks, ws)
+        else:
+            tr.backward(dlog.view(T, tr.C), 1, T, masks, ws)
+        ops.grad_sqnorm(tr.fl.grad, self.parts, self.step_t)
+        ops.adamw(tr.fl.flat, tr.fl.grad, self.m, self.v, self.lr, self.step_t, self.parts, **self.hp)
+        tr.refresh()
+
+    def __call__(self, x, labels, ant):
+        """x [T, f_dim] f32 (time-major LFB rows of one video), labels [T] int64, ant [T, P] f32 ->
+        device loss [3] = (clc, ant, last-stage correct count), valid until the next call."""
+        self.tr.ensure_fresh()
+        T = x.shape[0]
+        if not self.graphs:
+            ws = self._g.setdefault(("eager", T), _WS(self.dev))
+            self._body(x, labels, ant, ws)
+            self._bump()
+            return self.loss
+        ent = self._g.get(T)
+        if ent is None:
+            ws = _WS(self.dev)
+            sx = torch.empty_like(x)
+            sl = torch.empty_like(labels)
+            sa = torch.empty_like(ant)
+            sx.copy_(x); sl.copy_(labels); sa.copy_(ant)
+            # warm-up on a side stream: allocates every workspace buffer, runs one real step
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._body(sx, sl, sa, ws)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._body(sx, sl, sa, ws)
+            self._g[T] = (g, ws, sx, sl, sa)
+            self._bump()
+            return self.loss
+        g, ws, sx, sl, sa = ent
+        sx.copy_(x); sl.copy_(labels); sa.copy_(ant)
+        g.replay()
+        self._bump()
+        return self.loss
+
+    def _bump(self):
+        # the kernels updated the parameters in place: bump their version counters so every cached
+        # inference pack (svk.pack.get_packed) re-derives, then record the trainer's own view
+        for p in self.tr.fl.params.values():
+            increment_version(p)
+        self.tr._ver = self.tr.fl.versions()

@@ -142,13 +142,15 @@ int svk_mstcn_layer(const float* X, const float* Wd, const float* bd, const floa
 int svk_mstcn_layer_train(const float* X, const float* Wd, const float* bd, const float* W1, const float* b1,
                           const float* mask, float* Y, float* H, int T, int F, int dilation, int causal, void* stream);
 /* Backward of svk_mstcn_layer_train: dX = dY + conv^T(dPre), dPre = relu'(H) * (mask * dY) W1 (written to
- * the caller's dPre [T, F] scratch); dWd [3][F][F], dbd, dW1 [F][F], db1 += (f32 atomics: zero them). */
+ * the caller's dPre [T, F] scratch); dWd [F_out][F_in][3] (the nn.Conv1d weight layout; Wd itself is
+ * the packed [3][F_out][F_in] of the forward), dbd, dW1 [F][F], db1 += (f32 atomics: zero them). */
 int svk_mstcn_layer_bwd(const float* X, const float* H, const float* mask, const float* dY, const float* Wd,
                         const float* W1, float* dPre, float* dX, float* dWd, float* dbd, float* dW1, float* db1,
                         int T, int F, int dilation, int causal, void* stream);
-/* Backward of the inter-stage softmax (mstcn.py:126): dX = P * (dP - rowsum(P * dP)). */
-int svk_softmax_rows_bwd(const float* P, long ldp, const float* dP, long lddp, float* dX, long lddx, int M, int C,
-                         void* stream);
+/* Backward of the inter-stage softmax (mstcn.py:126): dX = P * (dP - rowsum(P * dP)) (+ R, may be NULL:
+ * the stage's own output gradient). */
+int svk_softmax_rows_bwd(const float* P, long ldp, const float* dP, long lddp, const float* R, long ldr, float* dX,
+                         long lddx, int M, int C, void* stream);
 
 /* CausalMambaModel (mstcn.py:282-343) block internals; the reference's Mamba is mamba_ssm's
  * `Mamba` (mamba_simple.py, imported at mstcn.py:9), absent from the reference snapshot.
@@ -188,6 +190,26 @@ int svk_mamba_scan_bwd(const float* U, const float* XD, long ldxd, const float* 
 int svk_mamba_conv_silu_bwd(const float* X, long ldx, const float* W, const float* bias, const float* dY,
                             float* dPre, float* dX, long lddx, float* dW, float* db, int B, int T, int Di, int K,
                             void* stream);
+
+/* Temporal-model training step (tecno.py:195-259).  Loss of tecno.py:237-254 over S stages of
+ * time-major logits (stage s row t at logits + s * sstride + t * ld; columns 0..P-1 phase logits,
+ * P..2P-1 anticipation regressions): loss[0] = (1/S) sum_s CrossEntropy(weight=class_w, 'mean'),
+ * loss[1] = (1/S) sum_s SmoothL1('mean'), loss[2] = correct argmax count of the last stage; dlogits
+ * (same layout) = d(loss[0] + loss[1]).  class_w may be NULL (unweighted). */
+int svk_tecno_loss(const float* logits, long ld, long sstride, int S, int T, int P, const long* labels,
+                   const float* ant_targets, const float* class_w, float* loss, float* dlogits, void* stream);
+/* clip_grad_norm_ + torch.optim.AdamW over one flat f32 buffer.  svk_grad_sqnorm writes
+ * svk_norm_parts() partial sums of squares and advances the device step counter (may be NULL when
+ * the caller counts); svk_adamw scales g by min(max_norm / (||g|| + 1e-6), 1) (partials NULL or
+ * max_norm <= 0: no clipping; the scaled g is written back), then applies AdamW with the learning
+ * rate read from device memory (*lr) and bias corrections for step *step. */
+int svk_norm_parts(void);
+int svk_grad_sqnorm(const float* g, long n, float* partials, long long* step, void* stream);
+int svk_adamw(float* p, float* g, float* m, float* v, long n, const float* partials, float max_norm,
+              const float* lr, float beta1, float beta2, float eps, float weight_decay, const long long* step,
+              void* stream);
+/* Y = -exp(X) (f32): the selective scan's A = -exp(A_log) after each optimizer step. */
+int svk_neg_exp(const float* X, float* Y, long n, void* stream);
 
 /* Frame preprocessing: generate_evp_LFB.py:243-247's Resize((OH, OW)) ->
  * CenterCrop -> ToTensor -> Normalize on decoded uint8 RGB frames [B, H, W, 3], bit-exact to Pillow's

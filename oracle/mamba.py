@@ -90,12 +90,16 @@ def mamba_block(x, sd, p, d_state, d_conv):
     return y @ sd[p + "out_proj.weight"].t()
 
 
-def causal_mamba(x, sd, layers, d_state=64, d_conv=4, dtype=torch.float64):
-    """CausalMambaModel.forward (mstcn.py:327-343), eval (dropout identity): x [B, f_dim, T] -> [1, B, classes, T]."""
+def causal_mamba(x, sd, layers, d_state=64, d_conv=4, dtype=torch.float64, masks=None):
+    """CausalMambaModel.forward (mstcn.py:327-343): x [B, f_dim, T] -> [1, B, classes, T].  Eval: dropout
+    identity; ``masks`` [L, B*T, F] (0 or 1/keep, time-major rows b*T + t): the train-mode
+    ``x = dropout(x + blk(x))`` draws (mstcn.py:335-336)."""
     sd = {k: v.to(dtype) for k, v in sd.items()}
     h = x.to(dtype).transpose(1, 2) @ sd["in_proj.weight"].t() + sd["in_proj.bias"]
     for l in range(layers):
         h = h + mamba_block(h, sd, f"blocks.{l}.", d_state, d_conv)
+        if masks is not None:
+            h = h * masks[l].to(dtype).view(h.shape)
     h = F.layer_norm(h, (h.shape[-1],), sd["norm.weight"], sd["norm.bias"], 1e-5)
     logits = h @ sd["head.weight"].t() + sd["head.bias"]
     return logits.transpose(1, 2).unsqueeze(0)

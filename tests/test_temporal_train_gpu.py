@@ -1,0 +1,253 @@
+"""Temporal-model training on the svk kernels (tecno.py:192-259) against fp64 autograd through the oracle
+restatements with the same dropout draws: MultiStageModel_S and CausalMambaModel gradients at the
+BASELINE config (4 stages / 10 layers / 64 maps / f_dim 256 / 14 outputs, causal) over a T = 1000 video,
+the tecno loss kernel, clip_grad_norm_ + AdamW against torch.optim, and the graph-captured native step
+against the eager one.
+
+Bar: every parameter gradient within 2e-3 of the fp64 reference in relative L2 norm
+(||g - g_ref|| <= 2e-3 ||g_ref||) and no element further than 1e-2 max |g_ref|; the forward logits within 2e-4 + 1e-5 |ref|
+(f32 through 4 x 10 dropout-scaled layers, logits up to ~60)."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import inputs as I, params as P, mstcn as MS, mamba as OM
+
+pytestmark = pytest.mark.gpu
+
+CW = [1.6411019141231247, 0.19090963801041133, 1.0, 0.2502662616859295, 1.9176363911137977,
+      0.9840248158200853, 2.174635818337618]        # tecno.py:124-130
+
+
+def _labels(T, seed):
+    g = torch.Generator().manual_seed(seed)
+    # phases run in contiguous segments like a surgical video
+    cuts = torch.sort(torch.randint(1, T, (6,), generator=g)).values.tolist()
+    lab = torch.zeros(T, dtype=torch.int64)
+    for k, c in enumerate(cuts):
+        lab[c:] = k + 1
+    ant = torch.rand(T, 7, generator=g) * 5
+    return lab, ant
+
+
+def _grad_close(name, g, ref, rel=2e-3, outlier=1e-2):
+    g = g.detach().double().cpu()
+    ref = ref.detach().double().cpu()
+    l2 = ((g - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+    scale = ref.abs().max().item()
+    err = (g - ref).abs().max().item()
+    assert l2 <= rel, f"{name}: relative L2 error {l2:.3e}"
+    # single elements may move further: a pre-activation within f32 rounding of 0 takes the other
+    # side of a ReLU in f32 than in f64 (one term of a 1000-step sum switches)
+    assert err <= outlier * max(scale, 1e-12), f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+
+
+def _check_grads(model, sd_ref):
+    for n, p in model.named_parameters():
+        assert p.grad is not None, n
+        _grad_close(n, p.grad, sd_ref[n].grad)
+
+
+def test_tecno_loss_kernel_vs_torch(cuda):
+    from svk import ops
+    S, T, P_ = 3, 777, 7
+    z = torch.randn(S, T, 2 * P_, dtype=torch.float64) * 2
+    lab, ant = _labels(T, 3)
+    zr = z.clone().requires_grad_(True)
+    y_all = zr.permute(0, 2, 1).unsqueeze(1)                 # [S, 1, 14, T] like the model output
+    clc, antl = MS.tecno_loss(y_all, lab, ant, torch.tensor(CW, dtype=torch.float64))
+    (clc + antl).backward()
+    loss, dz = ops.tecno_loss(z.float().to(cuda), lab.to(cuda), ant.to(cuda), torch.tensor(CW).float().to(cuda))
+    torch.cuda.synchronize()
+    assert abs(loss[0].item() - clc.item()) < 1e-5 * max(1, abs(clc.item()))
+    assert abs(loss[1].item() - antl.item()) < 1e-5 * max(1, abs(antl.item()))
+    pred = z[-1, :, :P_].argmax(-1)
+    assert int(loss[2].item()) == int((pred == lab).sum())
+    np.testing.assert_allclose(dz.cpu().double().numpy(), zr.grad.numpy(), rtol=0, atol=1e-7)
+
+
+def test_adamw_clip_vs_torch(cuda):
+    from svk import ops
+    torch.manual_seed(0)
+    n = 100_003
+    p0 = torch.randn(n, dtype=torch.float64)
+    ref = p0.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([ref], lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-3)
+    p = p0.float().to(cuda)
+    m = torch.zeros_like(p)
+    v = torch.zeros_like(p)
+    lr = torch.full((1,), 1e-3, device=cuda)
+    step = torch.zeros(1, dtype=torch.int64, device=cuda)
+    parts = torch.zeros(ops.NORM_PARTS, device=cuda)
+    for it in range(4):
+        g = torch.randn(n, dtype=torch.float64) * (0.001 if it == 2 else 0.05)   # step 2: norm < 1 (no clip)
+        ref.grad = g.clone()
+        torch.nn.utils.clip_grad_norm_([ref], max_norm=1.0)
+        opt.step()
+        gd = g.float().to(cuda)
+        ops.grad_sqnorm(gd, parts, step)
+        ops.adamw(p, gd, m, v, lr, step, parts, max_norm=1.0, weight_decay=1e-3)
+        torch.cuda.synchronize()
+        np.testing.assert_allclose(gd.cpu().double().numpy(), ref.grad.numpy(), rtol=1e-5, atol=1e-9)
+        np.testing.assert_allclose(p.cpu().double().numpy(), ref.detach().numpy(), rtol=0, atol=2e-6)
+    assert int(step.item()) == 4
+
+
+def _mstcn(cuda, seed=5):
+    from models import mstcn
+    m = mstcn.MultiStageModel_S(4, 10, 64, 256, 14, True)
+    sd = P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, seed)
+    m.load_state_dict(sd)
+    return m.to(cuda).train(), sd
+
+
+def test_mstcn_train_grads_vs_fp64_autograd(cuda):
+    m, sd = _mstcn(cuda)
+    T = 1000
+    lfb = I.lfb(T, 256, 21)                                   # [1, T, 256]
+    lab, ant = _labels(T, 4)
+    cw = torch.tensor(CW)
+    torch.manual_seed(1)
+    y_all = m.forward(lfb.to(cuda).transpose(2, 1))          # tecno.py:230
+    masks = m._svk_trainer.last_masks[0]                      # [S, L, T, F] draws of this forward
+    assert y_all.shape == (4, 1, 14, T)
+    keep = masks.float().mean().item()
+    assert 0.45 < keep / 2 < 0.55 and set(torch.unique(masks).tolist()) <= {0.0, 2.0}
+    crit_p = torch.nn.CrossEntropyLoss(weight=cw.float().to(cuda))
+    crit_r = torch.nn.SmoothL1Loss()
+    clc = sum(crit_p(y_all[j, 0, :7].transpose(1, 0), lab.to(cuda)) for j in range(4)) / 4
+    antl = sum(crit_r(y_all[j, 0, 7:].transpose(1, 0), ant.to(cuda)) for j in range(4)) / 4
+    (clc + antl).backward()                                   # tecno.py:254-256
+    torch.cuda.synchronize()
+
+    sd64 = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    ref = MS.multi_stage_s(lfb.transpose(2, 1), sd64, 4, 10, True, dtype=torch.float64, masks=masks.cpu())
+    np.testing.assert_allclose(y_all.detach().cpu().double().numpy(), ref.detach().numpy(), rtol=1e-5, atol=2e-4)
+    rc, ra = MS.tecno_loss(ref, lab, ant, cw.double())
+    (rc + ra).backward()
+    assert abs(clc.item() - rc.item()) < 1e-4 and abs(antl.item() - ra.item()) < 1e-4
+    _check_grads(m, sd64)
+
+
+def _mamba(cuda, seed=7):
+    from models import mstcn
+    m = mstcn.CausalMambaModel(4, 10, 64, 256, 14, True)
+    sd = OM.init_state_dict({k: v.shape for k, v in m.state_dict().items()}, seed)
+    m.load_state_dict(sd, strict=True)
+    return m.to(cuda).train(), sd
+
+
+def test_mamba_train_grads_vs_fp64_autograd(cuda):
+    m, sd = _mamba(cuda)
+    T = 1000
+    lfb = I.lfb(T, 256, 22)
+    lab, ant = _labels(T, 5)
+    cw = torch.tensor(CW)
+    torch.manual_seed(2)
+    y_all = m.forward(lfb.to(cuda).transpose(2, 1))
+    masks = m._svk_trainer.last_masks                         # [L, T, F]
+    assert y_all.shape == (1, 1, 14, T)
+    vals = set(np.round(torch.unique(masks).tolist(), 5))
+    assert vals <= {0.0, round(1 / 0.9, 5)}
+    crit_p = torch.nn.CrossEntropyLoss(weight=cw.float().to(cuda))
+    crit_r = torch.nn.SmoothL1Loss()
+    clc = crit_p(y_all[0, 0, :7].transpose(1, 0), lab.to(cuda))
+    antl = crit_r(y_all[0, 0, 7:].transpose(1, 0), ant.to(cuda))
+    (clc + antl).backward()
+    torch.cuda.synchronize()
+
+    sd64 = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    ref = OM.causal_mamba(lfb.transpose(2, 1), sd64, 10, masks=masks.cpu())
+    np.testing.assert_allclose(y_all.detach().cpu().double().numpy(), ref.detach().numpy(), rtol=1e-5, atol=2e-4)
+    rc, ra = MS.tecno_loss(ref, lab, ant, cw.double())
+    (rc + ra).backward()
+    _check_grads(m, sd64)
+
+
+@pytest.mark.parametrize("kind", ["mstcn", "mamba"])
+def test_native_step_matches_torch_optimizer_and_graph_replay(cuda, kind):
+    """TemporalTrainStep (svk loss + clip + AdamW, graph-captured) == the reference loop's
+    loss.backward(); clip_grad_norm_(1.0); AdamW(lr 1e-4, wd 1e-3) on the same draws; replays of the
+    captured step == eager steps."""
+    from svk.temporal import TemporalTrainStep
+    build = _mstcn if kind == "mstcn" else _mamba
+    T = 300
+    lfb = I.lfb(T, 256, 23)
+    lab, ant = _labels(T, 6)
+    x = lfb[0].to(cuda).contiguous()
+    cw = torch.tensor(CW).float()
+
+    m_ref, _ = build(cuda, 11)
+    m_eager = copy.deepcopy(m_ref)
+    m_graph = copy.deepcopy(m_ref)
+    st_e = TemporalTrainStep(m_eager, class_weights=CW, graphs=False, seed=3)
+    st_g = TemporalTrainStep(m_graph, class_weights=CW, graphs=True, seed=3)
+    opt = torch.optim.AdamW(m_ref.parameters(), lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-3)
+    crit_p = torch.nn.CrossEntropyLoss(weight=cw.to(cuda))
+    crit_r = torch.nn.SmoothL1Loss()
+    from svk import ops
+    from svk.temporal import trainer_for
+    tr = trainer_for(m_ref)
+    for it in range(3):
+        le = st_e(x, lab.to(cuda), ant.to(cuda)).clone()
+        lg = st_g(x, lab.to(cuda), ant.to(cuda)).clone()
+        # the reference loop on m_ref with the native step's dropout draws: step `it` draws with the
+        # device step counter at `it` (svk_grad_sqnorm advances it after the backward)
+        masks = tr.masks(T, 3, torch.full((1,), it, dtype=torch.int64, device=cuda))
+        opt.zero_grad()
+        y = _forward_with_masks(m_ref, x, masks)
+        S = y.shape[0]
+        clc = sum(crit_p(y[j, 0, :7].transpose(1, 0), lab.to(cuda)) for j in range(S)) / S
+        antl = sum(crit_r(y[j, 0, 7:].transpose(1, 0), ant.to(cuda)) for j in range(S)) / S
+        (clc + antl).backward()
+        torch.nn.utils.clip_grad_norm_(m_ref.parameters(), max_norm=1.0)
+        opt.step()
+        torch.cuda.synchronize()
+        assert abs(le[0].item() - clc.item()) < 1e-4 * max(1.0, clc.item())
+        assert abs(le[1].item() - antl.item()) < 1e-4 * max(1.0, antl.item())
+        np.testing.assert_allclose(lg.cpu().numpy(), le.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    # AdamW moves every element by ~lr per step whatever the gradient's size, so elements whose
+    # gradient is at rounding level may step in opposite directions: bound those few, and the rest tightly
+    for (n, pe), pg, pr in zip(m_eager.named_parameters(), m_graph.parameters(), m_ref.parameters()):
+        for a, b in ((pe, pr), (pg, pe)):
+            d = (a.detach() - b.detach()).abs()
+            assert d.max().item() <= 6e-4, n
+            assert (d > 2e-5).float().mean().item() < 2e-3, n
+
+
+def _forward_with_masks(model, x, masks):
+    """The autograd path with given draws (what model.forward(x.T[None]) does with its own draws)."""
+    import svk.temporal as TT
+    tr = TT.trainer_for(model)
+    saved = tr.masks
+    try:
+        tr.masks = lambda *a, **k: masks
+        return model.forward(x.t().unsqueeze(0))
+    finally:
+        tr.masks = saved
+
+
+@pytest.mark.parametrize("kind", ["mstcn", "mamba"])
+def test_native_step_loss_decreases(cuda, kind):
+    """30 graph-replayed steps at the reference hyper-parameters (lr 1e-4, wd 1e-3, clip 1.0) on one
+    synthetic video: the loss falls and stays finite; the eval forward sees the updated weights."""
+    from svk.temporal import TemporalTrainStep
+    m, _ = (_mstcn if kind == "mstcn" else _mamba)(cuda, 13)
+    st = TemporalTrainStep(m, class_weights=CW)
+    T = 500
+    x = I.lfb(T, 256, 24)[0].to(cuda).contiguous()
+    lab, ant = _labels(T, 7)
+    lab, ant = lab.to(cuda), ant.to(cuda)
+    first = st(x, lab, ant).clone()
+    for _ in range(30):
+        last = st(x, lab, ant)
+    torch.cuda.synchronize()
+    assert torch.isfinite(last).all()
+    drop = 0.9 if kind == "mstcn" else 0.995               # the Mamba head learns slowly at lr 1e-4
+    assert last[0].item() + last[1].item() < drop * (first[0].item() + first[1].item())
+    m.eval()
+    with torch.no_grad():
+        y = m(x.t().unsqueeze(0))
+    assert torch.isfinite(y).all() and y.shape[-1] == T
