@@ -355,7 +355,95 @@ def workload_train(args, dev, rank, dtype):
     return step, args.batch, config, check, (lambda: cpu_baseline_train(args.variant, args.cpu_baseline_seconds))
 
 
-WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": workload_mamba, "preproc": workload_preproc, "e2e": workload_e2e, "train": workload_train}
+def cpu_baseline_tecno_train(kind, budget_s, T=1500):
+    """Oracle train step (fp32 CPU autograd through the restatement, dropout draws, the tecno loss,
+    clip_grad_norm_ + AdamW) on one video of T frames, repeated within the budget."""
+    from oracle import params as P, mstcn as MS, mamba as OM, inputs as I, shapes as SH
+    if kind == "mstcn":
+        sd = P.make_state_dict(SH.mstcn_shapes(4, 10, 64, 256, 14), 1)
+    else:
+        sd = OM.init_state_dict(OM.mamba_shapes(256, 64, 10, 14), 1)
+    sd = {k: v.clone().requires_grad_(True) for k, v in sd.items()}
+    opt = torch.optim.AdamW(list(sd.values()), lr=1e-4, weight_decay=1e-3)
+    x = I.lfb(T, 256, 7).transpose(2, 1)
+    g = torch.Generator().manual_seed(0)
+    lab = torch.randint(0, 7, (T,), generator=g)
+    ant = torch.rand(T, 7, generator=g)
+    cw = torch.ones(7)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        if kind == "mstcn":
+            masks = (torch.rand(4, 10, T, 64, generator=g) < 0.5).float() * 2
+            y = MS.multi_stage_s(x, sd, 4, 10, True, masks=masks)
+        else:
+            masks = (torch.rand(10, T, 64, generator=g) < 0.9).float() / 0.9
+            y = OM.causal_mamba(x, sd, 10, dtype=torch.float32, masks=masks)
+        clc, antl = MS.tecno_loss(y, lab, ant, cw)
+        opt.zero_grad()
+        (clc + antl).backward()
+        torch.nn.utils.clip_grad_norm_(list(sd.values()), 1.0)
+        opt.step()
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n * T / dt, 2), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} optimizer steps on one {T}-frame video ({kind}, fp32 autograd through the oracle "
+                      f"restatement + AdamW) in {dt:.1f} s"}
+
+
+def workload_tecno_train(args, dev, rank, dtype):
+    """tecno.py:192-259 training epoch: one optimizer step per video over 40 full-length videos
+    (T ~ U[1000, 6000] LFB rows, f_dim 256), weighted CE + SmoothL1 over all stages, clip 1.0, AdamW —
+    every step one replay of the HIP graph captured for that video length."""
+    from models import mstcn
+    from svk.temporal import TemporalTrainStep
+    torch.manual_seed(0)
+    kind = args.temporal
+    lens = video_lengths(40, seed=rank)
+    g = torch.Generator(device=dev).manual_seed(99 + rank)
+    feats = [torch.randn(T, 256, device=dev, generator=g) for T in lens]
+    labels = [torch.randint(0, 7, (T,), device=dev, generator=g) for T in lens]
+    ants = [torch.rand(T, 7, device=dev, generator=g) * 5 for T in lens]
+    cw = [1.6411019141231247, 0.19090963801041133, 1.0, 0.2502662616859295, 1.9176363911137977,
+          0.9840248158200853, 2.174635818337618]                               # tecno.py:124-130
+
+    def build(k):
+        if k == "mstcn":
+            return mstcn.MultiStageModel_S(4, 10, 64, 256, 14, True).to(dev)
+        return mstcn.CausalMambaModel(4, 10, 64, 256, 14, True).to(dev)
+
+    model = build(kind)
+    st = TemporalTrainStep(model, class_weights=cw, graphs=not args.no_graph, seed=rank)
+
+    def step():
+        out = None
+        for x, lab, ant in zip(feats, labels, ants):
+            out = st(x, lab, ant)
+        return out
+
+    eager_st = TemporalTrainStep(model, class_weights=cw, graphs=False, seed=rank)
+
+    def eager():
+        out = None
+        for x, lab, ant in zip(feats, labels, ants):
+            out = eager_st(x, lab, ant)
+        return out
+
+    step.profile = eager
+
+    def check(out):
+        assert torch.isfinite(out).all()
+
+    name = ("MultiStageModel_S(4,10,64,256,14,True)" if kind == "mstcn" else
+            "CausalMambaModel(4,10,64,256,14,True)")
+    config = {"workload": f"tecno.py training epoch: {name}, one optimizer step per video over 40 full-length "
+                          "videos (T ~ U[1000, 6000]), train-mode dropout, weighted CE + SmoothL1 (all stages), "
+                          "clip_grad_norm_(1.0), AdamW(lr 1e-4, wd 1e-3)",
+              "model": name, "videos_per_step": 40, "hip_graph": not args.no_graph}
+    return step, sum(lens), config, check, (lambda: cpu_baseline_tecno_train(kind, args.cpu_baseline_seconds))
+
+
+WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": workload_mamba, "preproc": workload_preproc, "e2e": workload_e2e, "train": workload_train,
+             "tecno_train": workload_tecno_train}
 
 
 def launch_ranks(args):
@@ -421,6 +509,9 @@ def parse_args(argv=None):
                     help="comma list of extra dtypes timed on the same inputs and reported as other_dtypes "
                          "(extract default: bf16,fp32; 'none' to skip)")
     ap.add_argument("--no-flow", action="store_true")
+    ap.add_argument("--temporal", default="mstcn", choices=["mstcn", "mamba"],
+                    help="tecno_train: the temporal model (BASELINE config 3 names the MS-TCN; tecno.py:153 "
+                         "trains the CausalMambaModel)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-gemm", default=None, help="write per-shape GEMM timings to this file (rank 0)")
@@ -525,7 +616,7 @@ def main():
                         f"{nb / ms / 1e6:8.1f} GB/s  {shape:28s} {name}\n")
     gemm_ms = sum(v[0] for v in per.values())
     name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
-    f32_only = args.workload in ("mstcn", "mamba", "preproc")
+    f32_only = args.workload in ("mstcn", "mamba", "preproc", "tecno_train")
     dtype_name = "fp32" if f32_only else args.dtype
     peak = PEAK_TFLOPS[dtype_name]
     # bound by arithmetic intensity vs the machine balance (peak FLOP/s / 8 TB/s): tall-skinny

@@ -454,8 +454,11 @@ def mstcn_layer_train(x, wd_packed, bd, w1, b1, dilation, causal, mask, out=None
         raise _lib.SvkError("svk.mstcn_layer_train: x / mask must be contiguous [T, F]")
     out = torch.empty_like(x) if out is None else out
     hidden = torch.empty_like(x) if hidden is None else hidden
+    t0 = _prof_begin()
     _lib.call("svk_mstcn_layer_train", _p(x), _p(wd_packed), _p(bd), _p(w1), _p(b1), _p(mask), _p(out), _p(hidden),
               T, F, dilation, 1 if causal else 0, _stream())
+    # algorithmic: x, mask in; y, h out (f32); 3 dilated taps + the 1x1 conv per (t, f_out, f_in)
+    _prof_end(t0, "mstcn_layer_kernel<train>", 8.0 * T * F * F, 16 * T * F, (T, F, "mstcn_train"))
     return out, hidden
 
 
@@ -469,8 +472,12 @@ def mstcn_layer_bwd(x, hidden, mask, dy, wd_packed, w1, dwd, dbd, dw1, db1, dila
     T, F = x.shape
     dx = torch.empty_like(x) if dx is None else dx
     scratch = torch.empty_like(x) if scratch is None else scratch
+    t0 = _prof_begin()
     _lib.call("svk_mstcn_layer_bwd", _p(x), _p(hidden), _p(mask), _p(dy), _p(wd_packed), _p(w1), _p(scratch), _p(dx),
               _p(dwd), _p(dbd), _p(dw1), _p(db1), T, F, dilation, 1 if causal else 0, _stream())
+    # algorithmic: x, h, mask, dy in, dpre out (kernel A); dy, dpre in, dx out (kernel B); dh, 4 weight
+    # gradients and the 3-tap transposed conv per (t, f, f')
+    _prof_end(t0, "mstcn_bwd", 16.0 * T * F * F, 32 * T * F, (T, F, "mstcn_bwd"))
     return dx
 
 
@@ -513,8 +520,10 @@ def mamba_scan_train(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
     seg = mamba_seg_len(B, T, Di, N) if seg_len is None else int(seg_len)
     nws = _lib.load().svk_mamba_scan_workspace(B, T, Di, N, seg)
     ws = torch.empty(nws // 4, device=u.device, dtype=torch.float32) if nws > 0 else None
+    t0 = _prof_begin()
     _lib.call("svk_mamba_scan_train", _p(u), _p(xdbl), ldxd, _p(z), ldz, _p(w_dt), _p(b_dt), _p(a_neg), _p(d_skip),
               _p(out), _p(yss), B, T, Di, N, R, seg, _p(ws), _stream())
+    _prof_end(t0, f"mamba_scan_kernel<{N}, train>", M * Di * (2 * R + 6 + 6 * N), 4 * M * (4 * Di + W), (M, Di, N))
     return out, yss
 
 
@@ -538,9 +547,13 @@ def mamba_scan_bwd(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, yss, dout, dz, dxdbl, 
     ds = torch.empty(M, Di, device=u.device, dtype=torch.float32)
     nws = _lib.load().svk_mamba_scan_bwd_workspace(B, T, Di, N)
     ws = torch.empty(max(nws // 4, 1), device=u.device, dtype=torch.float32)
+    t0 = _prof_begin()
     _lib.call("svk_mamba_scan_bwd", _p(u), _p(xdbl), ldxd, _p(z), ldz, _p(w_dt), _p(b_dt), _p(a_neg), _p(d_skip),
               _p(yss), _p(dout), _p(du), _p(dz), lddz, _p(ds), _p(dxdbl), lddxd, _p(da), _p(dd), B, T, Di, N, R,
               _p(ws), _stream())
+    # algorithmic: u, z, yss, dout, dt_low|B|C in; du, dz, ds out, dB|dC accumulated (f32); the
+    # forward recurrence twice (checkpoint pass + recompute) and the reverse one, ~6 FLOP each per state
+    _prof_end(t0, f"mamba_scan_bwd_kernel<{N}>", M * Di * (2 * R + 20 + 18 * N), 4 * M * (7 * Di + 3 * W), (M, Di, N))
     return du, ds
 
 
