@@ -42,14 +42,14 @@ class DilatedResidualLayer(nn.Module):
         self.dropout = nn.Dropout()
 
     def _pack(self, dt):
-        wd = self.conv_dilated.weight.detach().float().permute(2, 0, 1).contiguous()   # [3][F_out][F_in]
+        wdT = self.conv_dilated.weight.detach().float().permute(2, 1, 0).contiguous()   # [3][F_in][F_out]
         w1, b1 = _w1x1(self.conv_1x1)
-        return dict(wd=wd, bd=self.conv_dilated.bias.detach().float().contiguous(), w1=w1, b1=b1)
+        return dict(wdT=wdT, bd=self.conv_dilated.bias.detach().float().contiguous(), w1T=w1.t().contiguous(), b1=b1)
 
     def forward_tm(self, x):
         """x [T, F] time-major f32 -> [T, F]."""
         p = get_packed(self, torch.float32, self._pack)
-        return ops.mstcn_layer(x, p["wd"], p["bd"], p["w1"], p["b1"], self.dilation, self.causal_conv)
+        return ops.mstcn_layer(x, p["wdT"], p["bd"], p["w1T"], p["b1"], self.dilation, self.causal_conv)
 
     def forward(self, x):
         """Reference signature: x [B, F, T] -> [B, F, T]."""

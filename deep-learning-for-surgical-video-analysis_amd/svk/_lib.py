@@ -40,7 +40,7 @@ SIGNATURES = {
                            c_int, c_int, c_int, P, P],
     "svk_mamba_conv_silu_bwd": [P, c_long, P, P, P, P, P, c_long, P, P, c_int, c_int, c_int, c_int, P],
     "svk_mstcn_layer_train": [P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
-    "svk_mstcn_layer_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mstcn_layer_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_softmax_rows_bwd": [P, c_long, P, c_long, P, c_long, P, c_long, c_int, c_int, P],
     "svk_neg_exp": [P, P, c_long, P],
     "svk_tecno_loss": [P, c_long, c_long, c_int, c_int, c_int, P, P, P, P, P, P],
@@ -88,7 +88,8 @@ STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
 LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
               "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int],
-              "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int]}
+              "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int],
+              "svk_mstcn_bwd_workspace": [c_int, c_int]}
 
 _lib = None
 

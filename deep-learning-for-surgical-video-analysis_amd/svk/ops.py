@@ -377,15 +377,17 @@ def softmax_rows(x, out=None):
     return out
 
 
-def mstcn_layer(x, wd_packed, bd, w1, b1, dilation, causal, out=None):
-    """x [T, F] f32 time-major; wd_packed [3, F, F]; w1 [F, F]."""
-    for t, nm in ((x, "x"), (wd_packed, "wd"), (bd, "bd"), (w1, "w1"), (b1, "b1")):
+def mstcn_layer(x, wdT, bd, w1T, b1, dilation, causal, out=None):
+    """x [T, F] f32 time-major; wdT [3, F_in, F_out]; w1T [F_in, F_out] (transposed packs)."""
+    for t, nm in ((x, "x"), (wdT, "wdT"), (bd, "bd"), (w1T, "w1T"), (b1, "b1")):
         _chk(t, nm, torch.float32)
     T, F = x.shape
     if out is None:
         out = torch.empty_like(x)
-    _lib.call("svk_mstcn_layer", _p(x), _p(wd_packed), _p(bd), _p(w1), _p(b1), _p(out), T, F, dilation,
+    t0 = _prof_begin()
+    _lib.call("svk_mstcn_layer", _p(x), _p(wdT), _p(bd), _p(w1T), _p(b1), _p(out), T, F, dilation,
               1 if causal else 0, _stream())
+    _prof_end(t0, "mstcn_layer_kernel", 8.0 * T * F * F, 8 * T * F, (T, F, "mstcn"))
     return out
 
 
@@ -444,10 +446,10 @@ def mamba_scan(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
 
 # ---- temporal-model training (tecno.py:195-259) ------------------------------------------------------
 
-def mstcn_layer_train(x, wd_packed, bd, w1, b1, dilation, causal, mask, out=None, hidden=None):
+def mstcn_layer_train(x, wdT, bd, w1T, b1, dilation, causal, mask, out=None, hidden=None):
     """DilatedResidualLayer train forward: out = x + mask * (w1 relu(dilated conv) + b1); ``hidden``
     [T, F] receives relu(pre) for the backward.  mask [T, F] f32 (0 or 1/keep)."""
-    for t, nm in ((x, "x"), (wd_packed, "wd"), (bd, "bd"), (w1, "w1"), (b1, "b1"), (mask, "mask")):
+    for t, nm in ((x, "x"), (wdT, "wdT"), (bd, "bd"), (w1T, "w1T"), (b1, "b1"), (mask, "mask")):
         _chk(t, nm, torch.float32)
     T, F = x.shape
     if mask.numel() != T * F or not (x.is_contiguous() and mask.is_contiguous()):
@@ -455,15 +457,17 @@ def mstcn_layer_train(x, wd_packed, bd, w1, b1, dilation, causal, mask, out=None
     out = torch.empty_like(x) if out is None else out
     hidden = torch.empty_like(x) if hidden is None else hidden
     t0 = _prof_begin()
-    _lib.call("svk_mstcn_layer_train", _p(x), _p(wd_packed), _p(bd), _p(w1), _p(b1), _p(mask), _p(out), _p(hidden),
+    _lib.call("svk_mstcn_layer_train", _p(x), _p(wdT), _p(bd), _p(w1T), _p(b1), _p(mask), _p(out), _p(hidden),
               T, F, dilation, 1 if causal else 0, _stream())
     # algorithmic: x, mask in; y, h out (f32); 3 dilated taps + the 1x1 conv per (t, f_out, f_in)
     _prof_end(t0, "mstcn_layer_kernel<train>", 8.0 * T * F * F, 16 * T * F, (T, F, "mstcn_train"))
     return out, hidden
 
 
-def mstcn_layer_bwd(x, hidden, mask, dy, wd_packed, w1, dwd, dbd, dw1, db1, dilation, causal, dx=None, scratch=None):
-    """Backward of mstcn_layer_train: returns dx; dwd [F, F, 3] (nn.Conv1d layout) / dbd / dw1 [F, F] / db1 += (f32)."""
+def mstcn_layer_bwd(x, hidden, mask, dy, wd_packed, w1, dwd, dbd, dw1, db1, dilation, causal, dx=None, scratch=None,
+                    ws=None):
+    """Backward of mstcn_layer_train: returns dx; dwd [F, F, 3] (nn.Conv1d layout) / dbd / dw1 [F, F] / db1 += (f32).
+    wd_packed [3, F_out, F_in]; w1 [F_out, F_in]; ws: optional scratch of svk_mstcn_bwd_workspace bytes."""
     for t, nm in ((x, "x"), (hidden, "hidden"), (mask, "mask"), (dy, "dy"), (wd_packed, "wd"), (w1, "w1"),
                   (dwd, "dwd"), (dbd, "dbd"), (dw1, "dw1"), (db1, "db1")):
         _chk(t, nm, torch.float32)
@@ -472,9 +476,12 @@ def mstcn_layer_bwd(x, hidden, mask, dy, wd_packed, w1, dwd, dbd, dw1, db1, dila
     T, F = x.shape
     dx = torch.empty_like(x) if dx is None else dx
     scratch = torch.empty_like(x) if scratch is None else scratch
+    nws = _lib.load().svk_mstcn_bwd_workspace(T, F)
+    if ws is None or ws.numel() * 4 < nws:
+        ws = torch.empty(max(nws // 4, 1), device=x.device, dtype=torch.float32)
     t0 = _prof_begin()
     _lib.call("svk_mstcn_layer_bwd", _p(x), _p(hidden), _p(mask), _p(dy), _p(wd_packed), _p(w1), _p(scratch), _p(dx),
-              _p(dwd), _p(dbd), _p(dw1), _p(db1), T, F, dilation, 1 if causal else 0, _stream())
+              _p(dwd), _p(dbd), _p(dw1), _p(db1), _p(ws), T, F, dilation, 1 if causal else 0, _stream())
     # algorithmic: x, h, mask, dy in, dpre out (kernel A); dy, dpre in, dx out (kernel B); dh, 4 weight
     # gradients and the 3-tap transposed conv per (t, f, f')
     _prof_end(t0, "mstcn_bwd", 16.0 * T * F * F, 32 * T * F, (T, F, "mstcn_bwd"))
@@ -897,3 +904,8 @@ def adamw(p, g, m, v, lr, step, partials=None, max_norm=0.0, beta1=0.9, beta2=0.
         raise _lib.SvkError("svk.adamw: p / g / m / v must be contiguous and equally sized")
     _lib.call("svk_adamw", _p(p), _p(g), _p(m), _p(v), n, _p(partials), float(max_norm), _p(lr), float(beta1),
               float(beta2), float(eps), float(weight_decay), _p(step), _stream())
+
+
+def mstcn_bwd_floats(T, F):
+    """f32 count of the svk_mstcn_layer_bwd workspace for a [T, F] layer."""
+    return _lib.load().svk_mstcn_bwd_workspace(T, F) // 4

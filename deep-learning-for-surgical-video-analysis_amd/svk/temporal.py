@@ -137,16 +137,21 @@ class MSTCNTrainer(_TrainerBase):
         super().__init__(model)
 
     def _build_packs(self):
-        self.k_wiT, self.k_woT, self.k_wd = [], [], []
+        self.k_wiT, self.k_woT, self.k_wd, self.k_wdT, self.k_w1T = [], [], [], [], []
         F = self.F
         for sn in self.stage_names:
             self.k_wiT.append(self._T(f"{sn}.conv_1x1.weight"))
             self.k_woT.append(self._T(f"{sn}.conv_out_classes.weight"))
-            ks = []
+            kd, kdT, k1T = [], [], []
             for l in range(self.L):
-                # conv_dilated.weight [F_out][F_in][3] -> [3][F_out][F_in]
-                ks.append(self.pt.add(self.fl.off[f"{sn}.layers.{l}.conv_dilated.weight"], (3, F, F), (1, 3 * F, 3)))
-            self.k_wd.append(ks)
+                o = self.fl.off[f"{sn}.layers.{l}.conv_dilated.weight"]
+                # conv_dilated.weight [F_out][F_in][3]: backward [3][F_out][F_in], forward [3][F_in][F_out]
+                kd.append(self.pt.add(o, (3, F, F), (1, 3 * F, 3)))
+                kdT.append(self.pt.add(o, (3, F, F), (1, 3, 3 * F)))
+                k1T.append(self._T(f"{sn}.layers.{l}.conv_1x1.weight"))
+            self.k_wd.append(kd)
+            self.k_wdT.append(kdT)
+            self.k_w1T.append(k1T)
 
     def masks(self, T, seed, counter=None):
         n = self.S * self.L * T * self.F
@@ -167,8 +172,8 @@ class MSTCNTrainer(_TrainerBase):
                          out=ws.get(f"h{s}_0", (T, F)))
             for l in range(self.L):
                 lp = f"{sn}.layers.{l}"
-                h, _ = ops.mstcn_layer_train(h, pk[self.k_wd[s][l]], P(f"{lp}.conv_dilated.bias"),
-                                             P(f"{lp}.conv_1x1.weight").view(F, F), P(f"{lp}.conv_1x1.bias"), 2 ** l,
+                h, _ = ops.mstcn_layer_train(h, pk[self.k_wdT[s][l]], P(f"{lp}.conv_dilated.bias"),
+                                             pk[self.k_w1T[s][l]], P(f"{lp}.conv_1x1.bias"), 2 ** l,
                                              self.causal, masks[s, l], out=ws.get(f"h{s}_{l + 1}", (T, F)),
                                              hidden=ws.get(f"H{s}_{l}", (T, F)))
             ops.gemm(h, P(f"{sn}.conv_out_classes.weight").view(C, F), P(f"{sn}.conv_out_classes.bias"), out=out[s])
@@ -198,7 +203,8 @@ class MSTCNTrainer(_TrainerBase):
                                          pk[self.k_wd[s][l]], P(f"{lp}.conv_1x1.weight").view(F, F),
                                          G(f"{lp}.conv_dilated.weight"), G(f"{lp}.conv_dilated.bias"),
                                          G(f"{lp}.conv_1x1.weight").view(F, F), G(f"{lp}.conv_1x1.bias"), 2 ** l,
-                                         self.causal, dx=ws.get(other, (T, F)), scratch=ws.get("dpre", (T, F)))
+                                         self.causal, dx=ws.get(other, (T, F)), scratch=ws.get("dpre", (T, F)),
+                                         ws=ws.get("bwd_ws", (max(ops.mstcn_bwd_floats(T, F), 1),)))
                 other = "dh_a" if other == "dh_b" else "dh_b"
             xin = self._xin[s]
             Din = xin.shape[1]

@@ -132,21 +132,24 @@ int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C,
 /* One MS-TCN DilatedResidualLayer (mstcn.py:208-214) over a time-major [T, F] f32 map:
  * h = relu(sum_j Wd[j] x[t + off_j] + bd); y[t] = x[t] + W1 h + b1;
  * causal: off = (-2d, -d, 0); else (-d, 0, +d); out-of-range taps read zero.
- * Wd packed [3][F_out][F_in], W1 [F_out][F_in]. F <= 64. */
-int svk_mstcn_layer(const float* X, const float* Wd, const float* bd, const float* W1,
+ * Weights as transposed packs: WdT [3][F_in][F_out] (WdT[j][i][o] = conv_dilated.weight[o][i][j]),
+ * W1T [F_in][F_out] (= conv_1x1.weight[:, :, 0]^T). F <= 64. */
+int svk_mstcn_layer(const float* X, const float* WdT, const float* bd, const float* W1T,
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
 /* Training (tecno.py:195-259 trains MultiStageModel_S with nn.Dropout(p = 0.5) active in every
  * DilatedResidualLayer): Y = X + mask * (W1 relu(dilated conv) + b1) with mask values 0 or 1/keep;
  * H [T, F] receives relu(pre) for the backward. */
-int svk_mstcn_layer_train(const float* X, const float* Wd, const float* bd, const float* W1, const float* b1,
+int svk_mstcn_layer_train(const float* X, const float* WdT, const float* bd, const float* W1T, const float* b1,
                           const float* mask, float* Y, float* H, int T, int F, int dilation, int causal, void* stream);
 /* Backward of svk_mstcn_layer_train: dX = dY + conv^T(dPre), dPre = relu'(H) * (mask * dY) W1 (written to
- * the caller's dPre [T, F] scratch); dWd [F_out][F_in][3] (the nn.Conv1d weight layout; Wd itself is
- * the packed [3][F_out][F_in] of the forward), dbd, dW1 [F][F], db1 += (f32 atomics: zero them). */
+ * the caller's dPre [T, F] scratch); dWd [F_out][F_in][3] (the nn.Conv1d weight layout), dbd, dW1 [F][F],
+ * db1 += (f32 atomics: zero them).  Here Wd is packed [3][F_out][F_in] and W1 is conv_1x1.weight
+ * [F_out][F_in]; ws: svk_mstcn_bwd_workspace(T, F) bytes (per-16-step-tile partial weight gradients). */
+long svk_mstcn_bwd_workspace(int T, int F);
 int svk_mstcn_layer_bwd(const float* X, const float* H, const float* mask, const float* dY, const float* Wd,
                         const float* W1, float* dPre, float* dX, float* dWd, float* dbd, float* dW1, float* db1,
-                        int T, int F, int dilation, int causal, void* stream);
+                        float* ws, int T, int F, int dilation, int causal, void* stream);
 /* Backward of the inter-stage softmax (mstcn.py:126): dX = P * (dP - rowsum(P * dP)) (+ R, may be NULL:
  * the stage's own output gradient). */
 int svk_softmax_rows_bwd(const float* P, long ldp, const float* dP, long lddp, const float* R, long ldr, float* dX,

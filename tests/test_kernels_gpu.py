@@ -358,7 +358,7 @@ def test_mstcn_layer(cuda, F_, T, d, causal):
     bd = _rand(F_, dt=torch.float32, dev=cuda, seed=24)
     w1 = _rand(F_, F_, dt=torch.float32, dev=cuda, scale=F_ ** -0.5, seed=25)
     b1 = _rand(F_, dt=torch.float32, dev=cuda, seed=26)
-    got = ops.mstcn_layer(x, wd.permute(2, 0, 1).contiguous().to(cuda), bd, w1, b1, d, causal)
+    got = ops.mstcn_layer(x, wd.permute(2, 1, 0).contiguous().to(cuda), bd, w1.t().contiguous(), b1, d, causal)
     torch.cuda.synchronize()
     xc = x.cpu().double().t()[None]
     pad = 2 * d if causal else d
@@ -367,6 +367,40 @@ def test_mstcn_layer(cuda, F_, T, d, causal):
         h = h[:, :, :-2 * d]
     ref = xc + F.conv1d(h, w1.cpu().double()[:, :, None], b1.cpu().double())
     torch.testing.assert_close(got.cpu().double(), ref[0].t(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("F_,T,d,causal", [(64, 1000, 8, True), (32, 77, 128, False), (20, 50, 2, True),
+                                           (64, 6001, 512, True)])
+def test_mstcn_layer_train_bwd(cuda, F_, T, d, causal):
+    """Train-mode layer (dropout mask) forward and its backward kernels against fp64 autograd."""
+    from svk import ops
+    x = _rand(T, F_, dt=torch.float32, dev=cuda, seed=32)
+    wd = _rand(F_, F_, 3, dt=torch.float32, dev="cpu", scale=F_ ** -0.5, seed=33)
+    bd = _rand(F_, dt=torch.float32, dev=cuda, seed=34)
+    w1 = _rand(F_, F_, dt=torch.float32, dev=cuda, scale=F_ ** -0.5, seed=35)
+    b1 = _rand(F_, dt=torch.float32, dev=cuda, seed=36)
+    mask = ops.keep_mask(T * F_, 0.5, 7, cuda).view(T, F_)
+    dy = _rand(T, F_, dt=torch.float32, dev=cuda, seed=37)
+    y, h = ops.mstcn_layer_train(x, wd.permute(2, 1, 0).contiguous().to(cuda), bd, w1.t().contiguous(), b1, d, causal,
+                                 mask)
+    dwd = torch.zeros(F_, F_, 3, device=cuda)
+    dbd, dw1, db1 = torch.zeros(F_, device=cuda), torch.zeros(F_, F_, device=cuda), torch.zeros(F_, device=cuda)
+    dx = ops.mstcn_layer_bwd(x, h, mask, dy, wd.permute(2, 0, 1).contiguous().to(cuda), w1, dwd, dbd, dw1, db1, d,
+                             causal)
+    torch.cuda.synchronize()
+    xr = x.cpu().double().t()[None].requires_grad_(True)
+    pr = [t.cpu().double().requires_grad_(True) for t in (wd, bd, w1, b1)]
+    pad = 2 * d if causal else d
+    hr = torch.relu(F.conv1d(xr, pr[0], pr[1], padding=pad, dilation=d))
+    if causal:
+        hr = hr[:, :, :-2 * d]
+    ref = xr + F.conv1d(hr, pr[2][:, :, None], pr[3]) * mask.cpu().double().t()[None]
+    torch.testing.assert_close(y.cpu().double(), ref[0].t().detach(), rtol=1e-5, atol=1e-5)
+    ref.backward(dy.cpu().double().t()[None])
+    torch.testing.assert_close(dx.cpu().double(), xr.grad[0].t(), rtol=1e-4, atol=1e-4)
+    for got, r in ((dwd, pr[0]), (dbd, pr[1]), (dw1, pr[2]), (db1, pr[3])):
+        scale = r.grad.abs().max().item()
+        assert (got.cpu().double() - r.grad).abs().max().item() <= 1e-4 * max(scale, 1.0)
 
 
 @pytest.mark.parametrize("dt", DTS)
