@@ -33,18 +33,128 @@ constexpr int MBB_RMAX = 16;
 
 __device__ __forceinline__ float softplus_bwd20(float s) { return s <= 20.f ? log1pf(__expf(s)) : s; }
 
+// Staging of one chunk of rows (shared by the segment passes): the dt_low | B | C rows into LDS, and per
+// (channel, step) delta = softplus(s), u and — mode >= 1 — g = dout * silu(z) (the gradient of yss);
+// mode 2 also writes dz and accumulates the D-skip gradient.
+template <int NS>
+struct ScanBwdSmem {
+  static constexpr int TC = MBB_TC, CPW = 64 / NS, CPB = 4 * CPW, XW = MBB_RMAX + 2 * NS + 1;
+  float xd[TC][XW];
+  float dl[CPB][TC + 1], uu[CPB][TC + 1], gy[CPB][TC + 1];
+};
+
+template <int NS>
+__device__ __forceinline__ void scan_bwd_stage(ScanBwdSmem<NS>& sm, int t0, int tn, int mode, const float* XD, long ldxd,
+                                               const float* U, const float* Z, long ldz, const float* dOut,
+                                               const float* Yss, float* dZ, long lddz, long row0, int W, int R, int Di,
+                                               int sc, int dd, const float* wdt, float bd, float& dDacc) {
+  constexpr int TC = MBB_TC, CPB = ScanBwdSmem<NS>::CPB;
+  __syncthreads();                         // earlier readers of the chunk buffers are done
+  for (int e = threadIdx.x; e < tn * W; e += 256) {
+    const int r = e / W, c = e - r * W;
+    sm.xd[r][c] = XD[(row0 + t0 + r) * ldxd + c];
+  }
+  __syncthreads();
+  for (int tl = threadIdx.x / CPB; tl < TC; tl += 256 / CPB) {
+    float dv = 0.f, uv = 0.f, g = 0.f;
+    if (tl < tn && dd < Di) {
+      const long row = row0 + t0 + tl;
+      float s = bd;
+#pragma unroll
+      for (int r = 0; r < MBB_RMAX; ++r)
+        if (r < R) s += wdt[r] * sm.xd[tl][r];
+      dv = softplus_bwd20(s);
+      uv = U[row * Di + dd];
+      if (mode >= 1) {
+        const float zv = Z[row * ldz + dd], go = dOut[row * Di + dd];
+        const float sg = 1.f / (1.f + __expf(-zv));
+        g = go * zv * sg;                                                 // d yss = dout * silu(z)
+        if (mode == 2) {
+          dZ[row * lddz + dd] = go * Yss[row * Di + dd] * sg * (1.f + zv * (1.f - sg));
+          dDacc += g * uv;
+        }
+      }
+    }
+    sm.dl[sc][tl] = dv;
+    sm.uu[sc][tl] = uv;
+    sm.gy[sc][tl] = g;
+  }
+  __syncthreads();
+}
+
+// Time is split into segments of seg_len steps (a multiple of the 16-step chunk), one workgroup per
+// (channel group, segment, video), so a single video's backward spreads over the chip:
+//   pass S (mamba_scan_bwd_seg): per segment, the forward recurrence from a zero state gives the local
+//     end state E and the decay product P = prod a = exp(A sum delta); the reverse recurrence from a zero
+//     carry gives the local carry-out M = a_first gh_first.  Stored per (video, segment, channel, state);
+//   main pass: the segment's true start state H_k = sum_{j<k} (prod_{j<i<k} P_i) E_j and its true carry-in
+//     G_k = M_{k+1} + P_{k+1} G_{k+1} (both linear recurrences over the segment summaries, folded by every
+//     workgroup in a short loop), then the exact per-segment backward below.
+template <int NS>
+__global__ __launch_bounds__(256) void mamba_scan_bwd_seg(
+    const float* __restrict__ U, const float* __restrict__ XD, long ldxd, const float* __restrict__ Z, long ldz,
+    const float* __restrict__ Wdt, const float* __restrict__ bdt, const float* __restrict__ A,
+    const float* __restrict__ dOut, float* __restrict__ SE, float* __restrict__ SP, float* __restrict__ SM, int T,
+    int Di, int R, int seg_len) {
+  using SM_ = ScanBwdSmem<NS>;
+  constexpr int TC = MBB_TC, CPW = SM_::CPW, CPB = SM_::CPB;
+  __shared__ SM_ sm;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cl = lane / NS, n = lane - cl * NS;
+  const int cw = wave * CPW + cl;
+  const int c0 = blockIdx.x * CPB, d = c0 + cw;
+  const int k = blockIdx.y, nseg = gridDim.y, b = blockIdx.z;
+  const long row0 = (long)b * T;
+  const float a_ = d < Di ? A[(long)d * NS + n] : 0.f;
+  const int W = R + 2 * NS;
+  const int sc = threadIdx.x % CPB, dd = c0 + sc;
+  float wdt[MBB_RMAX];
+#pragma unroll
+  for (int r = 0; r < MBB_RMAX; ++r) wdt[r] = (r < R && dd < Di) ? Wdt[(long)dd * R + r] : 0.f;
+  const float bd = dd < Di ? bdt[dd] : 0.f;
+  float unused = 0.f;
+  const int ts = k * seg_len, te = min(T, ts + seg_len);
+  float h = 0.f, ssum = 0.f;
+  for (int t0 = ts; t0 < te; t0 += TC) {
+    const int tn = min(TC, te - t0);
+    scan_bwd_stage<NS>(sm, t0, tn, 0, XD, ldxd, U, Z, ldz, dOut, nullptr, nullptr, 0, row0, W, R, Di, sc, dd, wdt, bd,
+                       unused);
+    for (int tl = 0; tl < tn; ++tl) {
+      const float dv = sm.dl[cw][tl];
+      h = __expf(dv * a_) * h + dv * sm.xd[tl][R + n] * sm.uu[cw][tl];
+      ssum += dv;
+    }
+  }
+  float carry = 0.f;
+  const int nch = (te - ts + TC - 1) / TC;
+  for (int c = nch - 1; c >= 0; --c) {
+    const int t0 = ts + c * TC, tn = min(TC, te - t0);
+    scan_bwd_stage<NS>(sm, t0, tn, 1, XD, ldxd, U, Z, ldz, dOut, nullptr, nullptr, 0, row0, W, R, Di, sc, dd, wdt, bd,
+                       unused);
+    for (int tl = tn - 1; tl >= 0; --tl) {
+      const float dv = sm.dl[cw][tl];
+      carry = __expf(dv * a_) * (sm.xd[tl][R + NS + n] * sm.gy[cw][tl] + carry);
+    }
+  }
+  if (d < Di) {
+    const long o = (((long)b * nseg + k) * Di + d) * NS + n;
+    SE[o] = h;
+    SP[o] = __expf(a_ * ssum);
+    SM[o] = carry;
+  }
+}
+
 template <int NS>
 __global__ __launch_bounds__(256) void mamba_scan_bwd_kernel(
     const float* __restrict__ U, const float* __restrict__ XD, long ldxd, const float* __restrict__ Z, long ldz,
     const float* __restrict__ Wdt, const float* __restrict__ bdt, const float* __restrict__ A,
     const float* __restrict__ Dp, const float* __restrict__ Yss, const float* __restrict__ dOut,
     float* __restrict__ dU, float* __restrict__ dZ, long lddz, float* __restrict__ dS, float* __restrict__ dXD,
-    long lddxd, float* __restrict__ dA, float* __restrict__ dD, float* __restrict__ HCK, int T, int Di, int R) {
-  constexpr int TC = MBB_TC;
-  constexpr int CPW = 64 / NS, CPB = 4 * CPW;
-  constexpr int XW = MBB_RMAX + 2 * NS + 1;
-  __shared__ float xd[TC][XW];
-  __shared__ float dl[CPB][TC + 1], uu[CPB][TC + 1], gy[CPB][TC + 1];
+    long lddxd, float* __restrict__ dA, float* __restrict__ dD, float* __restrict__ HCK, const float* __restrict__ SE,
+    const float* __restrict__ SP, const float* __restrict__ SMv, int T, int Di, int R, int seg_len) {
+  using SM_ = ScanBwdSmem<NS>;
+  constexpr int TC = MBB_TC, CPW = SM_::CPW, CPB = SM_::CPB;
+  __shared__ SM_ sm;
   __shared__ float P1[4][TC][65], P2[4][TC][65], Q1[4][TC][65], Q2[4][TC][65];
 
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -52,12 +162,13 @@ __global__ __launch_bounds__(256) void mamba_scan_bwd_kernel(
   const int cw = wave * CPW + cl;
   const int c0 = blockIdx.x * CPB;
   const int d = c0 + cw;
-  const int b = blockIdx.y;
+  const int k = blockIdx.y, nseg = gridDim.y, b = blockIdx.z;
   const long row0 = (long)b * T;
   const float a_ = d < Di ? A[(long)d * NS + n] : 0.f;
   const int W = R + 2 * NS;
   const int nchunk = (T + TC - 1) / TC;
-  // staging: thread -> fixed channel sc, time steps tl = threadIdx.x / CPB + k * (256 / CPB)
+  const int ts = k * seg_len, te = min(T, ts + seg_len);
+  const int cs = ts / TC, ce = (te + TC - 1) / TC;       // this segment's chunks
   const int sc = threadIdx.x % CPB, dd = c0 + sc;
   float wdt[MBB_RMAX];
 #pragma unroll
@@ -65,72 +176,47 @@ __global__ __launch_bounds__(256) void mamba_scan_bwd_kernel(
   const float bd = dd < Di ? bdt[dd] : 0.f;
   float dDacc = 0.f;
 
-  auto stage = [&](int t0, int tn, bool grads) {
-    __syncthreads();                       // earlier readers of the chunk buffers are done
-    for (int e = threadIdx.x; e < tn * W; e += 256) {
-      const int r = e / W, c = e - r * W;
-      xd[r][c] = XD[(row0 + t0 + r) * ldxd + c];
-    }
-    __syncthreads();
-    for (int tl = threadIdx.x / CPB; tl < TC; tl += 256 / CPB) {
-      float dv = 0.f, uv = 0.f, g = 0.f;
-      if (tl < tn && dd < Di) {
-        const long row = row0 + t0 + tl;
-        float s = bd;
-#pragma unroll
-        for (int r = 0; r < MBB_RMAX; ++r)
-          if (r < R) s += wdt[r] * xd[tl][r];
-        dv = softplus_bwd20(s);
-        uv = U[row * Di + dd];
-        if (grads) {
-          const float zv = Z[row * ldz + dd], go = dOut[row * Di + dd];
-          const float sg = 1.f / (1.f + __expf(-zv));
-          g = go * zv * sg;                                               // d yss = dout * silu(z)
-          dZ[row * lddz + dd] = go * Yss[row * Di + dd] * sg * (1.f + zv * (1.f - sg));
-          dDacc += g * uv;
-        }
-      }
-      dl[sc][tl] = dv;
-      uu[sc][tl] = uv;
-      gy[sc][tl] = g;
-    }
-    __syncthreads();
-  };
+  // the segment's true start state and carry-in from the segment summaries
+  float h = 0.f, carry = 0.f;
+  if (nseg > 1 && d < Di) {
+    const long base = (long)b * nseg * Di * NS + (long)d * NS + n, step = (long)Di * NS;
+    for (int j = 0; j < k; ++j) h = SP[base + j * step] * h + SE[base + j * step];
+    for (int j = nseg - 1; j > k; --j) carry = SMv[base + j * step] + SP[base + j * step] * carry;
+  }
 
-  // pass 1: forward recurrence, h checkpoint at each chunk start
-  float h = 0.f;
-  for (int c = 0; c < nchunk; ++c) {
-    const int t0 = c * TC, tn = min(TC, T - t0);
+  // pass 1: forward recurrence over the segment, h checkpoint at each chunk start
+  for (int c = cs; c < ce; ++c) {
+    const int t0 = c * TC, tn = min(TC, te - t0);
     if (d < Di) HCK[(((long)b * nchunk + c) * Di + d) * NS + n] = h;
-    stage(t0, tn, false);
+    scan_bwd_stage<NS>(sm, t0, tn, 0, XD, ldxd, U, Z, ldz, dOut, Yss, dZ, lddz, row0, W, R, Di, sc, dd, wdt, bd, dDacc);
     for (int tl = 0; tl < tn; ++tl) {
-      const float dv = dl[cw][tl];
-      h = __expf(dv * a_) * h + dv * xd[tl][R + n] * uu[cw][tl];
+      const float dv = sm.dl[cw][tl];
+      h = __expf(dv * a_) * h + dv * sm.xd[tl][R + n] * sm.uu[cw][tl];
     }
   }
   __threadfence_block();
 
-  // pass 2: chunks backwards
-  float carry = 0.f, dAacc = 0.f;
-  for (int c = nchunk - 1; c >= 0; --c) {
-    const int t0 = c * TC, tn = min(TC, T - t0);
+  // pass 2: the segment's chunks backwards
+  float dAacc = 0.f;
+  for (int c = ce - 1; c >= cs; --c) {
+    const int t0 = c * TC, tn = min(TC, te - t0);
     const float hstart = d < Di ? HCK[(((long)b * nchunk + c) * Di + d) * NS + n] : 0.f;
-    stage(t0, tn, true);
+    scan_bwd_stage<NS>(sm, t0, tn, 2, XD, ldxd, U, Z, ldz, dOut, Yss, dZ, lddz, row0, W, R, Di, sc, dd, wdt, bd, dDacc);
     float hh[TC];
     float hc = hstart;
 #pragma unroll
     for (int tl = 0; tl < TC; ++tl) {
       if (tl < tn) {
-        const float dv = dl[cw][tl];
-        hc = __expf(dv * a_) * hc + dv * xd[tl][R + n] * uu[cw][tl];
+        const float dv = sm.dl[cw][tl];
+        hc = __expf(dv * a_) * hc + dv * sm.xd[tl][R + n] * sm.uu[cw][tl];
       }
       hh[tl] = hc;
     }
 #pragma unroll
     for (int tl = TC - 1; tl >= 0; --tl) {
       if (tl < tn) {
-        const float dv = dl[cw][tl], uv = uu[cw][tl], g = gy[cw][tl];
-        const float Bn = xd[tl][R + n], Cn = xd[tl][R + NS + n];
+        const float dv = sm.dl[cw][tl], uv = sm.uu[cw][tl], g = sm.gy[cw][tl];
+        const float Bn = sm.xd[tl][R + n], Cn = sm.xd[tl][R + NS + n];
         const float at = __expf(dv * a_);
         const float hp = tl > 0 ? hh[tl - 1] : hstart;
         const float gh = Cn * g + carry;
@@ -151,18 +237,18 @@ __global__ __launch_bounds__(256) void mamba_scan_bwd_kernel(
       const int w2 = cw2 / CPW, cl2 = cw2 - w2 * CPW;
       float sd = 0.f, su = 0.f;
 #pragma unroll 8
-      for (int k = 0; k < NS; ++k) {
-        sd += P1[w2][tl][cl2 * NS + k];
-        su += P2[w2][tl][cl2 * NS + k];
+      for (int q = 0; q < NS; ++q) {
+        sd += P1[w2][tl][cl2 * NS + q];
+        su += P2[w2][tl][cl2 * NS + q];
       }
       const long row = row0 + t0 + tl;
-      const float dv = dl[cw2][tl];
+      const float dv = sm.dl[cw2][tl];
       dS[row * Di + d2] = sd * (1.f - __expf(-dv));                       // sigmoid(s) = 1 - exp(-softplus(s))
-      dU[row * Di + d2] = su + gy[cw2][tl] * Dp[d2];
+      dU[row * Di + d2] = su + sm.gy[cw2][tl] * Dp[d2];
     }
     // per (t, state): dB and dC summed over the workgroup's channels
     for (int e = threadIdx.x; e < TC * NS; e += 256) {
-      const int tl = e / NS, k = e - tl * NS;
+      const int tl = e / NS, q = e - tl * NS;
       if (tl >= tn) continue;
       float sb = 0.f, scc = 0.f;
 #pragma unroll
@@ -170,13 +256,13 @@ __global__ __launch_bounds__(256) void mamba_scan_bwd_kernel(
 #pragma unroll
         for (int cl2 = 0; cl2 < CPW; ++cl2) {
           if (c0 + w2 * CPW + cl2 < Di) {
-            sb += Q1[w2][tl][cl2 * NS + k];
-            scc += Q2[w2][tl][cl2 * NS + k];
+            sb += Q1[w2][tl][cl2 * NS + q];
+            scc += Q2[w2][tl][cl2 * NS + q];
           }
         }
       const long row = row0 + t0 + tl;
-      atomicAdd(dXD + row * lddxd + R + k, sb);
-      atomicAdd(dXD + row * lddxd + R + NS + k, scc);
+      atomicAdd(dXD + row * lddxd + R + q, sb);
+      atomicAdd(dXD + row * lddxd + R + NS + q, scc);
     }
   }
   if (d < Di) atomicAdd(dA + (long)d * NS + n, dAacc);
@@ -261,9 +347,20 @@ __global__ __launch_bounds__(256) void mamba_conv_silu_bwd_x(const float* __rest
 
 using namespace svk;
 
+// segment length for the backward: enough (channel group, segment, video) workgroups to fill the chip
+static int scan_bwd_seg_len(int B, int T, int Di, int N) {
+  const int groups = B * ((Di + 4 * (64 / N) - 1) / (4 * (64 / N)));
+  int nseg = std::max(1, std::min(512 / std::max(groups, 1), (T + 63) / 64));
+  int seg = (T + nseg - 1) / nseg;
+  return (seg + MBB_TC - 1) / MBB_TC * MBB_TC;
+}
+
 extern "C" long svk_mamba_scan_bwd_workspace(int B, int T, int Di, int N) {
   if (B <= 0 || T <= 0 || Di <= 0 || N <= 0) return 0;
-  return (long)B * ((T + MBB_TC - 1) / MBB_TC) * Di * N * (long)sizeof(float);
+  const int seg = scan_bwd_seg_len(B, T, Di, N), nseg = (T + seg - 1) / seg;
+  const long hck = (long)B * ((T + MBB_TC - 1) / MBB_TC) * Di * N;
+  const long sums = nseg > 1 ? 3L * B * nseg * Di * N : 0;
+  return (hck + sums) * (long)sizeof(float);
 }
 
 extern "C" int svk_mamba_scan_bwd(const float* U, const float* XD, long ldxd, const float* Z, long ldz,
@@ -279,11 +376,20 @@ extern "C" int svk_mamba_scan_bwd(const float* U, const float* XD, long ldxd, co
   }
   if ((long)B * T == 0) return SVK_OK;
   const int cpb = 4 * (64 / N);
-  dim3 grid((Di + cpb - 1) / cpb, B);
+  const int seg = scan_bwd_seg_len(B, T, Di, N), nseg = (T + seg - 1) / seg;
+  dim3 grid((Di + cpb - 1) / cpb, nseg, B);
   hipStream_t s = (hipStream_t)stream;
-#define SVK_MAMBA_BWD(NS)                                                                                     \
-  hipLaunchKernelGGL((mamba_scan_bwd_kernel<NS>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A, Dp, \
-                     Yss, dOut, dU, dZ, lddz, dS, dXD, lddxd, dA, dD, ws, T, Di, R)
+  float* hck = ws;
+  const long nh = (long)B * ((T + MBB_TC - 1) / MBB_TC) * Di * N;
+  float *SE = ws + nh, *SP = SE + (long)B * nseg * Di * N, *SMv = SP + (long)B * nseg * Di * N;
+#define SVK_MAMBA_BWD(NS)                                                                                       \
+  do {                                                                                                          \
+    if (nseg > 1)                                                                                               \
+      hipLaunchKernelGGL((mamba_scan_bwd_seg<NS>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A, dOut, \
+                         SE, SP, SMv, T, Di, R, seg);                                                           \
+    hipLaunchKernelGGL((mamba_scan_bwd_kernel<NS>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A, Dp,  \
+                       Yss, dOut, dU, dZ, lddz, dS, dXD, lddxd, dA, dD, hck, SE, SP, SMv, T, Di, R, seg);        \
+  } while (0)
   if (N == 64) SVK_MAMBA_BWD(64);
   else if (N == 32) SVK_MAMBA_BWD(32);
   else SVK_MAMBA_BWD(16);
