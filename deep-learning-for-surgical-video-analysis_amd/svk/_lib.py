@@ -43,6 +43,7 @@ SIGNATURES = {
     "svk_mstcn_layer_bwd": [P, P, P, P, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_softmax_rows_bwd": [P, c_long, P, c_long, P, c_long, P, c_long, c_int, c_int, P],
     "svk_neg_exp": [P, P, c_long, P],
+    "svk_phase_metrics": [P, P, P, c_int, c_int, c_int, P, P],
     "svk_tecno_loss": [P, c_long, c_long, c_int, c_int, c_int, P, P, P, P, P, P],
     "svk_grad_sqnorm": [P, c_long, P, P, P],
     "svk_adamw": [P, P, P, P, c_long, P, c_float, P, c_float, c_float, c_float, c_float, P, P],

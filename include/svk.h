@@ -214,6 +214,13 @@ int svk_adamw(float* p, float* g, float* m, float* v, long n, const float* parti
 /* Y = -exp(X) (f32): the selective scan's A = -exp(A_log) after each optimizer step. */
 int svk_neg_exp(const float* X, float* Y, long n, void* stream);
 
+/* Relaxed-boundary phase metrics (eval_and_vis.py:35-161) over V videos of int64
+ * labels concatenated in gt / pred with offsets [V + 1]: counts [V][2 + 4P] = (T, #forgiven-diff-zero,
+ * then per phase (TP over the gt|pred union, |union|, #pred, #gt)); exact integers, the caller forms the
+ * reference's ratios.  P <= 16, one workgroup per video. */
+int svk_phase_metrics(const long long* gt, const long long* pred, const long long* offsets, int V, int P,
+                      int tolerance, long long* counts, void* stream);
+
 /* Frame preprocessing: generate_evp_LFB.py:243-247's Resize((OH, OW)) ->
  * CenterCrop -> ToTensor -> Normalize on decoded uint8 RGB frames [B, H, W, 3], bit-exact to Pillow's
  * 8-bit bilinear resampling (libImaging/Resample.c: horizontal then vertical pass, 22-bit fixed-point
