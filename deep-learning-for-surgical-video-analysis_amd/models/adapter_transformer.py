@@ -11,7 +11,7 @@ epilogue applies the tanh.
 import torch
 import torch.nn as nn
 
-from svk import ops
+from svk import ops, temporal
 from svk.pack import get_packed, lin_w
 from ._common import check_inference
 from .transformer2_3_1 import Transformer2_3_1
@@ -34,7 +34,10 @@ class Transformer(nn.Module):
         self.fc = nn.Linear(mstcn_f_dim, out_features, bias=False)
 
     def original_forward(self, x, long_feature):
-        """x [1, classes, T] (MS-TCN last stage), long_feature [1, T, f_dim] -> [T, 1, classes]."""
+        """x [1, classes, T] (MS-TCN last stage), long_feature [1, T, f_dim] -> [T, 1, classes].
+        Train mode (tecno_trans.py:226-292): forward and backward on svk kernels (svk.temporal)."""
+        if self.training:
+            return temporal.transformer_autograd_forward(self, x, long_feature)
         check_inference(self, x, long_feature)
         xt = x[0].t()                                   # [T, classes]
         if xt.dtype != torch.float32 or xt.stride(1) != 1:

@@ -46,6 +46,7 @@ SIGNATURES = {
     "svk_phase_metrics": [P, P, P, c_int, c_int, c_int, P, P],
     "svk_tecno_loss": [P, c_long, c_long, c_int, c_int, c_int, P, P, P, P, P, P],
     "svk_grad_sqnorm": [P, c_long, P, P, P],
+    "svk_norm_parts": [],
     "svk_adamw": [P, P, P, P, c_long, P, c_float, P, c_float, c_float, c_float, c_float, P, P],
     "svk_frame_preproc": [P, P, P, P, P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
                           P],

@@ -491,3 +491,174 @@ class TemporalTrainStep:
         for p in self.tr.fl.params.values():
             increment_version(p)
         self.tr._ver = self.tr.fl.versions()
+
+
+# ---------------------------------------------------------------------------------------------------
+class TransformerTrainer(_TrainerBase):
+    """adapter_transformer.Transformer.original_forward in train mode (tecno_trans.py:226-292):
+    feas = tanh(fc(lfb)) and the build's Transformer2_3_1 (post-LN encoder over the 30-frame window,
+    decoder self- then cross-attention, ReLU FFNs; no dropout layers), forward and backward on svk
+    kernels (f32 GEMMs / weight gradients, the f32 attention forward and backward, LayerNorm backward)."""
+
+    def __init__(self, model):
+        t = model.transformer
+        self.len_q = model.len_q
+        self.C = model.num_classes
+        self.heads = t.encoder.layers[0].self_attn.n_heads if len(t.encoder.layers) else 4
+        mha = t.decoder.self_attn
+        self.dk, self.dv, self.H = mha.d_k, mha.d_v, mha.n_heads
+        self.n_layers = len(t.encoder.layers)
+        self.eps = float(mha.layer_norm.eps)
+        super().__init__(model)
+
+    def _lin_names(self):
+        names = ["fc.weight"]
+        mhas = [f"transformer.encoder.layers.{l}.self_attn" for l in range(self.n_layers)]
+        mhas += ["transformer.decoder.self_attn", "transformer.decoder.cross_attn"]
+        ffns = [f"transformer.encoder.layers.{l}.ffn" for l in range(self.n_layers)] + ["transformer.decoder.ffn"]
+        for m in mhas:
+            names += [f"{m}.{w}.weight" for w in ("W_Q", "W_K", "W_V", "fc")]
+        for f in ffns:
+            names += [f"{f}.fc1.weight", f"{f}.fc2.weight"]
+        return names
+
+    def _build_packs(self):
+        self.kT = {n: self._T(n) for n in self._lin_names()}
+
+    def WT(self, name):
+        return self.pt.tensors[self.kT[name + ".weight"]]
+
+    # ---- building blocks: forward saves what the backward needs into ``sv`` ----
+    def _lin(self, x, name, act=None, residual=None, out=None):
+        P = self.fl.P
+        b = self.fl.params.get(name + ".bias")
+        return ops.gemm(x, P(name + ".weight"), None if b is None else b.detach(), act=act, residual=residual, out=out)
+
+    def _mha_fwd(self, q_in, kv_in, p, sv):
+        P = self.fl.P
+        q = self._lin(q_in, p + ".W_Q")
+        k = self._lin(kv_in, p + ".W_K")
+        v = self._lin(kv_in, p + ".W_V")
+        o = ops.attention(q, k, v, self.H, 1.0 / (self.dk ** 0.5))
+        pre = self._lin(o, p + ".fc", residual=q_in)
+        y = ops.layernorm(pre, P(p + ".layer_norm.weight"), P(p + ".layer_norm.bias"), self.eps)
+        sv[p] = (q_in, kv_in, q, k, v, o, pre)
+        return y
+
+    def _ffn_fwd(self, x, p, sv):
+        P = self.fl.P
+        h = self._lin(x, p + ".fc1", act="relu")
+        pre = self._lin(h, p + ".fc2", residual=x)
+        y = ops.layernorm(pre, P(p + ".layer_norm.weight"), P(p + ".layer_norm.bias"), self.eps)
+        sv[p] = (x, h, pre)
+        return y
+
+    def forward(self, xt, lf, sv):
+        """xt [T, C] (MS-TCN last stage, time-major), lf [T, f_dim] -> [T, 1, C]."""
+        P = self.fl.P
+        T = xt.shape[0]
+        tr = self.model.transformer
+        pos = tr.pos_table if self.len_q == tr.len_q else None
+        x = ops.window_unfold(xt, self.len_q, pos=pos)
+        if pos is None:
+            x = ops.add_bcast(x, tr.pos_table)
+        pre_f = ops.gemm(lf, P("fc.weight"))                                    # [T, C]
+        feas = ops.gemm(lf, P("fc.weight"), act="tanh").view(T, 1, self.C)
+        sv["fc"] = (lf, pre_f)
+        for l in range(self.n_layers):
+            x = self._mha_fwd(x, x, f"transformer.encoder.layers.{l}.self_attn", sv)
+            x = self._ffn_fwd(x, f"transformer.encoder.layers.{l}.ffn", sv)
+        d = self._mha_fwd(feas, feas, "transformer.decoder.self_attn", sv)
+        d = self._mha_fwd(d, x, "transformer.decoder.cross_attn", sv)
+        return self._ffn_fwd(d, "transformer.decoder.ffn", sv)
+
+    def _lin_bwd(self, dy, x, name, residual=None, need_dx=True):
+        G = self.fl.G
+        b = self.fl.params.get(name + ".bias")
+        ops.gemm_wgrad(dy, x, G(name + ".weight"), None if b is None else G(name + ".bias"))
+        if need_dx:
+            return ops.gemm(dy, self.WT(name), residual=residual)
+        return None
+
+    def _ln_bwd(self, pre, dy, p):
+        return ops.layernorm_bwd(pre, dy, self.fl.P(p + ".layer_norm.weight"), self.eps,
+                                 dgamma=self.fl.G(p + ".layer_norm.weight"), dbeta=self.fl.G(p + ".layer_norm.bias"))
+
+    def _mha_bwd(self, dy, p, sv, self_attn):
+        q_in, kv_in, q, k, v, o, pre = sv[p]
+        dpre = self._ln_bwd(pre, dy, p)
+        do = self._lin_bwd(dpre, o, p + ".fc")
+        dq, dk, dv = ops.attention_bwd(q, k, v, o, do, self.H, 1.0 / (self.dk ** 0.5))
+        dq_in = self._lin_bwd(dq, q_in, p + ".W_Q", residual=dpre)
+        if self_attn:
+            d = self._lin_bwd(dk, kv_in, p + ".W_K", residual=dq_in)
+            return self._lin_bwd(dv, kv_in, p + ".W_V", residual=d), None
+        dkv = self._lin_bwd(dk, kv_in, p + ".W_K")
+        dkv = self._lin_bwd(dv, kv_in, p + ".W_V", residual=dkv)
+        return dq_in, dkv
+
+    def _ffn_bwd(self, dy, p, sv):
+        x, h, pre = sv[p]
+        G = self.fl.G
+        dpre = self._ln_bwd(pre, dy, p)
+        ops.gemm_wgrad(dpre, h, G(p + ".fc2.weight"), G(p + ".fc2.bias"))
+        dh = ops.gemm(dpre, self.WT(p + ".fc2"), dact="relu", dact_src=h)   # relu'(pre) = [h > 0]
+        return self._lin_bwd(dh, x, p + ".fc1", residual=dpre)
+
+    def backward(self, dout, sv):
+        """dout [T, 1, C] -> parameter gradients into the flat buffer (the window input is detached at
+        tecno_trans.py:271 and the LFB is data: no input gradients)."""
+        dd = self._ffn_bwd(dout.contiguous(), "transformer.decoder.ffn", sv)
+        dd, denc = self._mha_bwd(dd, "transformer.decoder.cross_attn", sv, self_attn=False)
+        dfeas, _ = self._mha_bwd(dd, "transformer.decoder.self_attn", sv, self_attn=True)
+        dx = denc
+        for l in range(self.n_layers - 1, -1, -1):
+            dx = self._ffn_bwd(dx, f"transformer.encoder.layers.{l}.ffn", sv)
+            if l > 0:
+                dx, _ = self._mha_bwd(dx, f"transformer.encoder.layers.{l}.self_attn", sv, self_attn=True)
+            else:                                   # the first layer's input is the (detached) window
+                p = f"transformer.encoder.layers.{l}.self_attn"
+                q_in, kv_in, q, k, v, o, pre = sv[p]
+                dpre = self._ln_bwd(pre, dx, p)
+                do = self._lin_bwd(dpre, o, p + ".fc")
+                dq, dk, dv = ops.attention_bwd(q, k, v, o, do, self.H, 1.0 / (self.dk ** 0.5))
+                for dz, nm in ((dq, ".W_Q"), (dk, ".W_K"), (dv, ".W_V")):
+                    self._lin_bwd(dz, q_in, p + nm, need_dx=False)
+        lf, pre_f = sv["fc"]
+        dpre_f = ops.act_bwd(pre_f, dfeas.reshape(pre_f.shape).contiguous(), "tanh")
+        ops.gemm_wgrad(dpre_f, lf, self.fl.G("fc.weight"))
+
+
+class _TransformerFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tr, x, lf, *params):
+        tr.ensure_fresh()
+        xt = x[0].t().float().contiguous()
+        l2 = lf[0].float().contiguous()
+        sv = {}
+        out = tr.forward(xt, l2, sv)
+        ctx.tr, ctx.sv = tr, sv
+        return out
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, gout):
+        tr = ctx.tr
+        tr.fl.grad.zero_()
+        tr.backward(gout.float().contiguous(), ctx.sv)
+        grads = [tr.fl.G(n).clone() for n in tr.fl.params]
+        return (None, None, None) + tuple(grads)
+
+
+def transformer_autograd_forward(model, x, long_feature):
+    """Train-mode Transformer.original_forward(x [1, C, T], long_feature [1, T, f_dim]) -> [T, 1, C]."""
+    if not (x.is_cuda and long_feature.is_cuda):
+        raise SvkError("Transformer: inputs must be on the GPU; there is no CPU path")
+    if x.requires_grad or long_feature.requires_grad:
+        raise SvkError("Transformer train mode: input gradients are not built (tecno_trans.py detaches the "
+                       "MS-TCN output and the LFB is data)")
+    t = model.__dict__.get("_svk_trainer")
+    if t is None or t.model is not model:
+        t = TransformerTrainer(model)
+        model.__dict__["_svk_trainer"] = t
+    return _TransformerFn.apply(t, x, long_feature, *t.fl.params.values())

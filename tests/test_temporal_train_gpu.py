@@ -32,16 +32,19 @@ def _labels(T, seed):
     return lab, ant
 
 
-def _grad_close(name, g, ref, rel=2e-3, outlier=1e-2):
+def _grad_close(name, g, ref, rel=2e-3, outlier=1e-2, floor=1e-6):
+    """floor: absolute L2 floor for gradients that vanish analytically (e.g. the attention key bias:
+    a shift common to all keys leaves the softmax unchanged, so its exact gradient is 0 and f32 leaves
+    ~1e-9 of rounding)."""
     g = g.detach().double().cpu()
     ref = ref.detach().double().cpu()
-    l2 = ((g - ref).norm() / ref.norm().clamp_min(1e-30)).item()
+    l2 = ((g - ref).norm() / max(ref.norm().item(), floor / rel)).item()
     scale = ref.abs().max().item()
     err = (g - ref).abs().max().item()
     assert l2 <= rel, f"{name}: relative L2 error {l2:.3e}"
     # single elements may move further: a pre-activation within f32 rounding of 0 takes the other
     # side of a ReLU in f32 than in f64 (one term of a 1000-step sum switches)
-    assert err <= outlier * max(scale, 1e-12), f"{name}: max err {err:.3e} vs scale {scale:.3e}"
+    assert err <= outlier * max(scale, floor), f"{name}: max err {err:.3e} vs scale {scale:.3e}"
 
 
 def _check_grads(model, sd_ref):
@@ -251,3 +254,38 @@ def test_native_step_loss_decreases(cuda, kind):
     with torch.no_grad():
         y = m(x.t().unsqueeze(0))
     assert torch.isfinite(y).all() and y.shape[-1] == T
+
+
+def test_transformer_train_grads_vs_fp64_autograd(cuda):
+    """tecno_trans.py:226-292: model1.train(); p_all = model1.original_forward(out_features.detach(), lfb);
+    loss = 0.5 CE + SmoothL1; backward — every Transformer parameter gradient vs fp64 autograd through the
+    oracle restatement (Transformer2_3_1 itself is build-defined: parity of its definition unpinned)."""
+    from models.adapter_transformer import Transformer
+    from oracle import trans_sv as TS
+    m = Transformer(64, 2048, 14, 30)
+    sd = P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 17)
+    m.load_state_dict(sd)
+    m = m.to(cuda).train()
+    T = 300
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 14, T, generator=g) * 3
+    lfb = I.lfb(T, 2048, 25)
+    lab, ant = _labels(T, 8)
+    p_all = m.original_forward(x.to(cuda), lfb.to(cuda))
+    assert p_all.shape == (T, 1, 14)
+    clc = torch.nn.functional.cross_entropy(p_all[:, :, :7].squeeze(), lab.to(cuda))
+    antl = torch.nn.functional.smooth_l1_loss(p_all[:, :, 7:].squeeze(), ant.to(cuda))
+    (0.5 * clc + antl).backward()
+    torch.cuda.synchronize()
+    sd64 = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    ref = TS.original_forward(x.double(), lfb.double(), sd64, 64, dtype=torch.float64)
+    np.testing.assert_allclose(p_all.detach().cpu().double().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-4)
+    rc = torch.nn.functional.cross_entropy(ref[:, :, :7].squeeze(), lab)
+    ra = torch.nn.functional.smooth_l1_loss(ref[:, :, 7:].squeeze(), ant.double())
+    (0.5 * rc + ra).backward()
+    _check_grads(m, sd64)
+    # the eval forward still works after training-mode use
+    m.eval()
+    with torch.no_grad():
+        e = m.original_forward(x.to(cuda), lfb.to(cuda))
+    np.testing.assert_allclose(e.cpu().double().numpy(), ref.detach().numpy(), rtol=1e-5, atol=1e-4)
