@@ -484,7 +484,8 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     }
   }
   const bool reg_epi = cfg == 0 && (big || a.M < 32768);
-  // cfg: 0 = 128x128, 10 = 128x64, 20 = 64x128, 30 = 64x64
+  // cfg: 0 = 128x128, 10 = 128x64, 20 = 64x128, 30 = 64x64, 40 = 128x160 (N % 160 == 0), 50 = 256x128 (8 waves)
+  if (cfg == 40 && a.N % 160 != 0) cfg = 10;
   if (asrc == 1) {
     switch (cfg) {
       case 10: return launch_pk_k<T, PkCfg<128, 64, 2, 2, 2>, 1>(a, st, !big);
@@ -497,6 +498,8 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 10: return launch_pk_k<T, PkCfg<128, 64, 2, 2, 2>, 0>(a, st, !big);
     case 20: return launch_pk_k<T, PkCfg<64, 128, 2, 2, 2>, 0>(a, st, !big);
     case 30: return launch_pk_k<T, PkCfg<64, 64, 2, 2, 2>, 0>(a, st, !big);
+    case 40: return launch_pk_k<T, PkCfg<128, 160, 2, 2, 2>, 0>(a, st, false);
+    case 50: return launch_pk_k<T, PkCfg<256, 128, 4, 2, 2>, 0>(a, st, false);
     default: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
   }
 }

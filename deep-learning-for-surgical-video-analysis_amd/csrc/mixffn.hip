@@ -1,304 +1,457 @@
-// Fused MixFFN for bf16 (mix_transformer_evp.py:32-67 + DWConv :19-30 + the Block residual :169):
+// Whole MixFFN + Block residual in one kernel, f16 / bf16 (mix_transformer_evp.py:32-67, DWConv
+// :19-30, Block :169), optionally followed by the stage LayerNorm (:370-412):
 //
-//   Y = X + fc2( GELU( dwconv3x3( fc1(XN) ) ) )         XN = LN2(X), all maps NHWC [B, H, W, C]
+//   Y  = X + fc2( GELU( dwconv3x3( fc1(XN) ) ) )          all maps NHWC [B, H, W, C], hidden 4C
+//   Yn = LN(Y)                                            (when gamma != nullptr; Y may then be null)
 //
-// The unfused path writes and re-reads the 4C-wide hidden map three times (fc1 out, dwconv in/out,
-// fc2 in): 1.6 GB per stage-1 block at B = 256.  Here a workgroup owns a TH x TW tile of output
-// tokens of one frame and keeps the hidden on chip: it stages XN for the tile plus a 1-token halo
-// in LDS once, then for each 64-channel hidden chunk
-//   (1) fc1 over the (TH+2)(TW+2) halo tokens      -> sH   (MFMA 16x16x32, out-of-image rows = 0,
-//                                                          which is the dwconv's zero padding)
-//   (2) depthwise 3x3 + bias + GELU over the tile    -> sG   (VALU, 16-byte LDS reads)
-//   (3) fc2 partial sums, accumulated in registers across chunks (MFMA)
-// and finally adds b2 + the residual and writes Y through an LDS-staged 16-byte epilogue.
-// HBM traffic per block: read XN (+halo re-reads from L2), read X, write Y.
+// The unfused path moves the 4C-wide hidden map through HBM (stage 1 at B = 256: 411 MB written by
+// fc1+dwconv, 411 MB read by fc2).  Here the hidden never leaves the chip.  Work unit: a strip of R
+// image rows x the full width W of one frame, its hidden channels walked in chunks of HC:
+//   fc1(c)    (R + 2) x W halo tokens x HC hidden (MFMA 16x16x32; A = XN fragments held in registers
+//             for the whole strip, B = the chunk's W1 rows from LDS) -> sH as TOKEN PAIRS: dword
+//             (row, pair p, channel) = the hidden values of pixels (2p, 2p + 1).  Out-of-image rows
+//             and the two border pair columns are zeros (the conv's zero padding).
+//   dwconv(c) depthwise 3x3 + bias + GELU -> sG [token][HC].  The pair layout turns the 3 horizontal
+//             taps of two outputs into 4 v_dot2_f32_{f16,bf16} (f32 accumulate):
+//             out[x] = (h[x], h[x+1]).(w1, w2) + (h[x-2], h[x-1]).(0, w0), likewise for x + 1 — 6
+//             instructions per output; taps pre-packed in that form (svk.ops.mixffn_pack_taps).
+//   fc2(c)    partial sums of the chunk (MFMA, transposed: a lane ends with 4 consecutive output
+//             channels of one token), accumulated in registers over the strip's chunks.
+// The dwconv + GELU is VALU work (~25 instructions per hidden element) and dominates; the two GEMMs
+// are short MFMA phases.  So the workgroup is WAVE-SPECIALISED and software-pipelined: 4 producer
+// waves (one per SIMD) run fc1(s) and fc2(s - 2), and 8 dwconv waves (one channel quad each, so their
+// taps are wave-uniform broadcast reads, prefetched a step ahead) run dwconv(s - 1) — concurrently in
+// pipeline step s, one workgroup barrier per step (sH and sG double-buffered by step parity).  The
+// workgroup is persistent (one per CU): W1, W2, the biases and the packed taps stay resident in LDS for
+// the whole kernel (no weight traffic per strip), and the pipeline runs across strips without draining
+// (the next strip's XN fragments are fetched after the current strip's last fc1; each strip's residual
+// rows go global -> LDS by LDS-DMA when its fc2 starts, NCH steps before its epilogue needs them).
+// Epilogue (producer waves, per finished strip): + b2 + residual, 8-byte row-piece stores, optional
+// LayerNorm reduced over the 4 lanes that hold a token's row.
+// HBM traffic per token: XN (+ halo re-reads from L2), X, Y (or Yn) — 3 x 2C bytes.
+// Measured (B = 256, stage 1, f16): 372 us vs 463 us for fc1+dwconv kernel + fc2 GEMM; the per-step
+// critical path is the dwconv waves' LDS + VALU latency (s_memtime trace: ~3.4k cycles per step).
 //
-// Weights: the fc1 B fragments are read straight from global memory (L2-resident, shared by every
-// workgroup); the fc2 weight chunk is staged in LDS with a one-chunk register prefetch.
+// Taps and the MFMA operands are in the storage dtype (the reference's autocast casts the conv weight
+// to f16 too); accumulation, bias, GELU and LayerNorm statistics in f32.
 #include "svk_common.h"
 
 namespace svk {
-
 namespace ffn {
 
-constexpr int HC = 64;      // hidden channels per chunk
-constexpr int HLD = HC + 8; // sH / sG / sW2 row stride (elements): 144 B rows, conflict-free b128 reads
-
-template <int C, int TH, int TW>
+template <int C_, int W_, int R_, int RV_, int HC_>
 struct Cfg {
-  static constexpr int HW_ = TW + 2, HH = TH + 2;
-  static constexpr int NH = HH * HW_;               // halo tokens
-  static constexpr int MTH = (NH + 15) / 16;        // fc1 M-tiles
-  static constexpr int NO = TH * TW;                // output tokens
-  static constexpr int MTO = (NO + 15) / 16;        // fc2 M-tiles
-  static constexpr int XLD = C + 8;                 // sXN row stride
-  static constexpr int KS1 = C / 32;                // fc1 k-steps
-  static constexpr int NT2 = C / 16;                // fc2 n-tiles
-  static constexpr int HID = 4 * C;
-  static constexpr int NCH = HID / HC;
-  static constexpr int I1 = (MTH + 3) / 4;          // fc1 M-tiles per wave (max)
-  static constexpr int I2 = (MTO + 3) / 4;          // fc2 M-tiles per wave (max)
-  static constexpr int SX = MTH * 16 * XLD * 2;     // bytes
-  static constexpr int SH = MTH * 16 * HLD * 2;
-  static constexpr int SG = MTO * 16 * HLD * 2;
-  static constexpr int SW2 = C * HLD * 2;
-  static constexpr int STP = 10 * HC * 4;           // taps [9][64] + dwconv bias [64], f32
-  static constexpr int SOUT = NO * (C + 4) * 4;     // f32 epilogue tile (aliases sXN.. region)
-  static constexpr int MAIN = SX + SH + SG + SW2 + STP;
-  static constexpr int BYTES = MAIN > SOUT ? MAIN : SOUT;
-  static constexpr int W2CH = C * HC / 8;           // 16-byte chunks of one W2 chunk
-  static constexpr int W2PT = (W2CH + 255) / 256;   // per thread
+  static constexpr int C = C_, W = W_, R = R_, RV = RV_, HC = HC_;
+  static constexpr int HID = 4 * C, NCH = HID / HC;     // HC-channel hidden chunks = pipeline steps per strip
+  static constexpr int KS = C / 32;                     // fc1 k-steps
+  static constexpr int NT1 = HC / 16;                   // fc1 n-tiles (hidden channels of a chunk)
+  static constexpr int KS2 = HC / 32;                   // fc2 k-steps per chunk
+  static constexpr int NT2 = C / 16;                    // fc2 n-tiles (output channels)
+  static constexpr int NPC = W / 2 + 2;                 // pair columns incl. the two zero borders
+  static constexpr int HR = R + 2;                      // halo rows
+  static constexpr int NH = HR * W, MTH = (NH + 15) / 16;
+  static constexpr int NO = R * W, MTO = (NO + 15) / 16;
+  static constexpr int NQ = HC / 4;                     // channel quads per chunk = dwconv waves
+  static constexpr int NPW = 4, NDW = NQ, NWV = NPW + NDW, NT = 64 * NWV;   // producer / dwconv waves
+  static constexpr int I1 = (MTH + NPW - 1) / NPW, I2 = (MTO + NPW - 1) / NPW;
+  static constexpr int NPAIR = W / 2, NITEM = NPAIR * (R / RV);   // dwconv lanes per wave
+  static constexpr int CS = HC + 4;                     // dwords per pair column (conflict-free 16-byte reads)
+  static constexpr int SH = HR * NPC * CS * 4;          // bytes, per parity
+  static constexpr int GROW = HC * 2;                   // sG row bytes
+  static constexpr int SG = MTO * 16 * GROW;            // per parity
+  // resident weights: W1, W2 (swizzled rows), the fc1 bias (the packed taps are read by the scalar unit)
+  static constexpr int SW1 = HID * C * 2, SW2 = C * HID * 2, SB1 = HID * 4, SEP = 3 * C * 4;   // + b2, gamma, beta
+  static constexpr int WTS = SW1 + SW2 + SB1 + SEP;
+  static constexpr int SXR = NPW * I2 * 16 * C * 2;    // producer waves' residual rows (LDS-DMA target)
+  static constexpr int STP = HID / 4 * 13 * 16;        // packed taps (svk.ops.mixffn_pack_taps layout)
+  static constexpr int LDS = WTS + 2 * (SH + SG) + SXR + STP;
+  static_assert(W % 4 == 0 && C % 32 == 0 && HC == 32 && R % RV == 0 && HID % HC == 0, "shape");
+  static_assert(NITEM <= 64, "one dwconv item per lane");
+  static_assert(LDS <= 160 * 1024, "LDS");
 };
 
-template <int C, int TH, int TW>
-__global__ __launch_bounds__(256) void mixffn_bf16(const bf16* __restrict__ XN, const bf16* __restrict__ X,
-                                                   const bf16* __restrict__ W1, const float* __restrict__ b1,
-                                                   const float* __restrict__ taps, const float* __restrict__ db,
-                                                   const bf16* __restrict__ W2, const float* __restrict__ b2,
-                                                   bf16* __restrict__ Y, int H, int W, int tiles_x, int tiles_y) {
-  using K = Cfg<C, TH, TW>;
-  __shared__ __attribute__((aligned(16))) char smem[K::BYTES];
-  bf16 (*sX)[K::XLD] = reinterpret_cast<bf16 (*)[K::XLD]>(smem);
-  bf16 (*sH)[HLD] = reinterpret_cast<bf16 (*)[HLD]>(smem + K::SX);
-  bf16 (*sG)[HLD] = reinterpret_cast<bf16 (*)[HLD]>(smem + K::SX + K::SH);
-  bf16 (*sW2)[HLD] = reinterpret_cast<bf16 (*)[HLD]>(smem + K::SX + K::SH + K::SG);
-  float (*sT)[HC] = reinterpret_cast<float (*)[HC]>(smem + K::SX + K::SH + K::SG + K::SW2);   // [10][64]
-  float (*sO)[C + 4] = reinterpret_cast<float (*)[C + 4]>(smem);
+// 16-byte chunk c of row r of an LDS matrix with `cpr` chunks per row sits at c ^ (r & (cpr - 1)) (cpr <= 16):
+// conflict-free MFMA fragment reads (16 rows x one chunk column per 16-lane group).
+template <int CPRW>
+__device__ __forceinline__ int swz(int r, int c) { return r * CPRW + (c ^ (r & (CPRW - 1))); }
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int fr = lane & 15, fk = (lane >> 4) * 8;
-  int bid = blockIdx.x;
-  const int tx = bid % tiles_x; bid /= tiles_x;
-  const int ty = bid % tiles_y;
-  const int b = bid / tiles_y;
-  const int y0 = ty * TH, x0 = tx * TW;
-  const long img = (long)b * H * W;
+// sG rows are 64 bytes (4 chunks of 8 hidden channels); chunk c of token row o sits at c ^ gsw(o):
+// conflict-free ds_read_b128 fragment reads (16 rows x one chunk column per 16-lane group).
+__device__ __forceinline__ int gsw(int o) { return (-(o >> 2)) & 3; }
 
-  // ---- stage XN halo tile: halo token r -> (hy, hx) = (r / HW_, r % HW_), image (y0-1+hy, x0-1+hx)
-  {
-    // all loads issued before any store (a load -> select -> store loop would serialise one HBM
-    // round trip per iteration)
-    constexpr int CPR = C / 8;
-    constexpr int NIT = (K::MTH * 16 * CPR + 255) / 256;
-    uint4 v[NIT];
-    bool okv[NIT];
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = min(tid + 256 * it, K::MTH * 16 * CPR - 1);
-      const int r = e / CPR, c8 = (e % CPR) * 8;
-      const int hy = r / K::HW_, hx = r - hy * K::HW_;
-      const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-      okv[it] = r < K::NH && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      const int iyc = min(max(iy, 0), H - 1), ixc = min(max(ix, 0), W - 1);
-      v[it] = *reinterpret_cast<const uint4*>(XN + (img + (long)iyc * W + ixc) * C + c8);
-    }
-#pragma unroll
-    for (int it = 0; it < NIT; ++it) {
-      const int e = tid + 256 * it;
-      if (e < K::MTH * 16 * CPR) {
-        const int r = e / CPR, c8 = (e % CPR) * 8;
-        *reinterpret_cast<uint4*>(&sX[r][c8]) = okv[it] ? v[it] : make_uint4(0, 0, 0, 0);
-      }
-    }
+template <typename T> struct P2;
+template <> struct P2<f16> {
+  typedef _Float16 v2 __attribute__((ext_vector_type(2)));
+  static __device__ __forceinline__ float dot(uint32_t a, uint32_t b, float c) {
+    return __builtin_amdgcn_fdot2(__builtin_bit_cast(v2, a), __builtin_bit_cast(v2, b), c, false);
   }
-  // W2 chunk loader (register prefetch): W2 [C][HID], chunk hc -> sW2[n][k] = W2[n][hc*64 + k]
-  uint4 w2r[K::W2PT];
-  float4 tpr;                                   // taps/bias chunk: 160 float4 -> threads 0..159
-  auto w2_fetch = [&](int hc) {
-#pragma unroll
-    for (int i = 0; i < K::W2PT; ++i) {
-      const int e = tid + 256 * i;
-      const int ec = e < K::W2CH ? e : K::W2CH - 1;
-      const int n = ec / (HC / 8), k8 = (ec % (HC / 8)) * 8;
-      w2r[i] = *reinterpret_cast<const uint4*>(W2 + (long)n * K::HID + hc * HC + k8);
-    }
-    const int tt = min(tid, 159), row = tt / 16, c4 = (tt % 16) * 4;
-    tpr = *reinterpret_cast<const float4*>((row < 9 ? taps + row * K::HID : db) + hc * HC + c4);
+};
+template <> struct P2<bf16> {
+  typedef __bf16 v2 __attribute__((ext_vector_type(2)));
+  static __device__ __forceinline__ float dot(uint32_t a, uint32_t b, float c) {
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(v2, a), __builtin_bit_cast(v2, b), c, false);
+  }
+};
+template <typename T> __device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  T v[2] = {(T)lo, (T)hi};
+  return *reinterpret_cast<const uint32_t*>(v);
+}
+
+// gelu(x) = 0.5 x (1 + erf(x / sqrt2)) with the erf of erf_fast (A&S 7.1.26), rearranged as
+// relu(x) - 0.5 |x| t p(t) exp(-x^2 / 2): 11 VALU + 2 transcendental, no select on the sign.
+__device__ __forceinline__ float gelu_dw(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
+  float q = fmaf(-0.5f * 1.061405429f, t, -0.5f * -1.453152027f);
+  q = fmaf(q, t, -0.5f * 1.421413741f);
+  q = fmaf(q, t, -0.5f * -0.284496736f);
+  q = fmaf(q, t, -0.5f * 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);   // exp(-x^2 / 2)
+  return fmaf(ax * t * q, e, fmaxf(x, 0.f));
+}
+
+// 16-byte global -> LDS copy without a VGPR round trip (global_load_lds_dwordx4: lane l of the wave
+// writes bytes [lds_dst + 16 l, + 16)); issued from asm, completion counted by the caller (vmcnt).
+typedef __attribute__((address_space(3))) void* las_ptr;
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(las_ptr)p; }
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <typename T, class K>
+__global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, const T* __restrict__ X,
+                                                     const T* __restrict__ W1, const float* __restrict__ b1,
+                                                     const uint4* __restrict__ tpk, const T* __restrict__ W2,
+                                                     const float* __restrict__ b2, T* __restrict__ Y,
+                                                     T* __restrict__ Yn, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, int H,
+                                                     int nstrip, int total) {
+  typedef v8_t<T> tx8;
+  constexpr int W = K::W, C = K::C, HC = K::HC, HID = K::HID, NPC = K::NPC, CS = K::CS, NCH = K::NCH;
+  constexpr int CPR1 = C / 8, CPR2 = HID / 8;           // 16-byte chunks per W1 / W2 row
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  char* const smem = reinterpret_cast<char*>(smem4);
+  // [W1 | W2 | taps] resident for the whole kernel, then per step parity p: [sH | sG]
+  uint4* const sW1 = smem4;
+  uint4* const sW2 = reinterpret_cast<uint4*>(smem + K::SW1);
+  float* const sB1 = reinterpret_cast<float*>(smem + K::SW1 + K::SW2);
+  float* const sEp = sB1 + HID;                          // b2 [C], gamma [C], beta [C]
+  auto sH = [&](int p) __attribute__((always_inline)) { return reinterpret_cast<uint32_t*>(smem + K::WTS + p * (K::SH + K::SG)); };
+  auto sG = [&](int p) __attribute__((always_inline)) { return smem + K::WTS + p * (K::SH + K::SG) + K::SH; };
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int G = gridDim.x, first = xcd_remap(blockIdx.x, G);   // strips first, first + G, ...
+  const int nst = first < total ? (total - first + G - 1) / G : 0;
+  const int T_ = nst * NCH;                             // pipeline items (strip, chunk) of this workgroup
+  auto strip_of = [&](int k, int& b, int& y0) __attribute__((always_inline)) {
+    const int sid = first + k * G;
+    b = sid / nstrip;
+    y0 = (sid - b * nstrip) * K::R;
   };
-  auto w2_stash = [&]() {
+  auto barrier = []() __attribute__((always_inline)) { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+
+  // prologue: the weights into LDS (XOR-swizzled rows), zero border pair columns of both sH buffers
+  for (int e = tid; e < K::SW1 / 16; e += K::NT) {
+    const int n = e / CPR1, c = e - n * CPR1;
+    sW1[swz<CPR1>(n, c)] = *reinterpret_cast<const uint4*>(W1 + (long)n * C + c * 8);
+  }
+  for (int e = tid; e < K::SW2 / 16; e += K::NT) {
+    const int n = e / CPR2, c = e - n * CPR2;
+    sW2[swz<CPR2>(n, c)] = *reinterpret_cast<const uint4*>(W2 + (long)n * HID + c * 8);
+  }
+  for (int e = tid; e < HID; e += K::NT) sB1[e] = b1[e];
+  uint4* const sTp = reinterpret_cast<uint4*>(smem + K::WTS + 2 * (K::SH + K::SG) + K::SXR);
+  for (int e = tid; e < K::STP / 16; e += K::NT) sTp[e] = tpk[e];
+  for (int e = tid; e < 3 * C; e += K::NT) sEp[e] = e < C ? b2[e] : (gamma ? (e < 2 * C ? gamma[e - C] : beta[e - 2 * C]) : 0.f);
+  for (int e = tid; e < 2 * K::HR * 2 * HC; e += K::NT) {
+    const int p = e / (K::HR * 2 * HC), r = e % (K::HR * 2 * HC);
+    const int hr = r / (2 * HC), side = (r / HC) & 1, c = r % HC;
+    sH(p)[(hr * NPC + (side ? NPC - 1 : 0)) * CS + c] = 0u;
+  }
+  barrier();
+
+  if (wave < K::NPW) {
+    // ===== producer waves: fc2 of item s - 2 (+ strip epilogue), fc1 of item s =====
+    const int pw = wave;
+    tx8 xa[K::I1][K::KS];        // XN fragments of the strip fc1 is on
+    f32x4 acc2[K::I2][K::NT2];   // fc2 accumulators of the strip fc2 is on
+    char* const sXr = smem + K::WTS + 2 * (K::SH + K::SG) + pw * (K::I2 * 16 * C * 2);   // residual rows [i][r][C]
+    auto load_xa = [&](int k, tx8 (&xa)[K::I1][K::KS]) __attribute__((always_inline)) {
+      int b, y0;
+      strip_of(k, b, y0);
+      const T* XNb = XN + (long)b * H * W * C;
 #pragma unroll
-    for (int i = 0; i < K::W2PT; ++i) {
-      const int e = tid + 256 * i;
-      if (e < K::W2CH) {
-        const int n = e / (HC / 8), k8 = (e % (HC / 8)) * 8;
-        *reinterpret_cast<uint4*>(&sW2[n][k8]) = w2r[i];
+      for (int i = 0; i < K::I1; ++i) {
+        const int t = min(16 * (pw + K::NPW * i) + fr, K::NH - 1);
+        const int hy = t / W, hx = t - hy * W;
+        const int y = min(max(y0 - 1 + hy, 0), H - 1);
+        const T* xr = XNb + ((long)y * W + hx) * C + 8 * fq;
+#pragma unroll
+        for (int ks = 0; ks < K::KS; ++ks) xa[i][ks] = *reinterpret_cast<const tx8*>(xr + 32 * ks);
       }
-    }
-    if (tid < 160) *reinterpret_cast<float4*>(&sT[tid / 16][(tid % 16) * 4]) = tpr;
-  };
-  w2_fetch(0);
-
-  f32x4 acc2[K::I2][K::NT2];
+    };
 #pragma unroll
-  for (int i = 0; i < K::I2; ++i)
+    for (int i = 0; i < K::I2; ++i)
 #pragma unroll
-    for (int j = 0; j < K::NT2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // fc1 A fragments (W1 rows of the chunk) and b1 of the chunk live in ONE register set that is
-  // refilled for chunk hc+1 as soon as chunk hc's fc1 has consumed it, so the L2/HBM latency of the
-  // refill hides under chunk hc's dwconv and fc2 phases (software pipeline, no extra registers).
-  bf16x8 wa[K::KS1][4];
-  float b1v[4][4];
-  auto w1_fetch = [&](int hc) {
+      for (int j = 0; j < K::NT2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (T_ > 0) load_xa(0, xa);
+    for (int s = 0; s < T_ + 2; ++s) {
+      const int g2 = s - 2;
+      if (g2 >= 0) {
+        // ---- fc2 partial sums of item g2 (transposed: A = W2 rows, B = G rows)
+        const int c2 = g2 % NCH;
+        const char* G2 = sG(g2 & 1);
+        if (c2 == 0) {   // residual rows of this strip -> the wave's LDS slot (read by its epilogue NCH steps later)
+          int b, y0;
+          strip_of(g2 / NCH, b, y0);
+          constexpr int CPRX = C / 8, NQX = K::I2 * 16 * CPRX / 64;
 #pragma unroll
-    for (int ks = 0; ks < K::KS1; ++ks)
+          for (int k = 0; k < NQX; ++k) {
+            const int q = k * 64 + lane, i = q / (16 * CPRX), r = (q / CPRX) % 16, c = q % CPRX;
+            const int o = min(16 * (pw + K::NPW * i) + r, K::NO - 1);
+            const T* src = X + (((long)b * H + min(y0 + o / W, H - 1)) * W + o % W) * C + c * 8;
+            dma16(src, __builtin_amdgcn_readfirstlane(lds_addr(sXr + k * 1024)));
+          }
+        }
 #pragma unroll
-      for (int jh = 0; jh < 4; ++jh)
-        wa[ks][jh] = *reinterpret_cast<const bf16x8*>(W1 + (long)(hc * HC + 16 * jh + fr) * C + 32 * ks + fk);
+        for (int ks = 0; ks < K::KS2; ++ks) {
+          tx8 wf[K::NT2];
 #pragma unroll
-    for (int jh = 0; jh < 4; ++jh)
-      *reinterpret_cast<float4*>(&b1v[jh][0]) = *reinterpret_cast<const float4*>(b1 + hc * HC + 16 * jh + (lane >> 4) * 4);
-  };
-  w1_fetch(0);
-  const int c8 = (tid & 7) * 8;      // each thread's dwconv work always covers channel group c8
-
-  for (int hc = 0; hc < K::NCH; ++hc) {
-    __syncthreads();                 // previous chunk's fc2 done with sG / sW2; sX staged (hc = 0)
-    w2_stash();
-    w2_fetch(hc + 1 < K::NCH ? hc + 1 : hc);
-
-    // ---- (1) fc1 chunk over the halo tokens, computed transposed: H^T = W1c . XN^T, so a lane's
-    // accumulator holds 4 consecutive hidden channels of one token -> one 8-byte LDS store.
-    {
-      f32x4 acc1[4][K::I1];
+          for (int j = 0; j < K::NT2; ++j) wf[j] = *reinterpret_cast<const tx8*>(&sW2[swz<CPR2>(16 * j + fr, c2 * (HC / 8) + 4 * ks + fq)]);
 #pragma unroll
-      for (int jh = 0; jh < 4; ++jh)
+          for (int i = 0; i < K::I2; ++i) {
+            const int mt = pw + K::NPW * i;
+            if (mt < K::MTO) {
+              const int o = 16 * mt + fr;
+              const tx8 g = *reinterpret_cast<const tx8*>(G2 + o * K::GROW + (((4 * ks + fq) ^ gsw(o)) << 4));
 #pragma unroll
-        for (int i = 0; i < K::I1; ++i) acc1[jh][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+              for (int j = 0; j < K::NT2; ++j) acc2[i][j] = mfma16x16x32(wf[j], g, acc2[i][j]);
+            }
+          }
+        }
+        if (c2 == NCH - 1) {
+          // ---- strip epilogue: lane holds output channels 16 j + 4 fq + r of token 16 mt + fr
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the residual DMA of this strip (issued NCH steps ago)
+          int b, y0;
+          strip_of(g2 / NCH, b, y0);
 #pragma unroll
-      for (int ks = 0; ks < K::KS1; ++ks) {
+          for (int i = 0; i < K::I2; ++i) {
+            const int mt = pw + K::NPW * i;
+            if (mt < K::MTO) {
+              const int o = min(16 * mt + fr, K::NO - 1);
+              const int row = y0 + o / W;
+              const bool ok = row < H && 16 * mt + fr < K::NO;
+              const long off = (((long)b * H + min(row, H - 1)) * W + o % W) * C + 4 * fq;
+              // the rounded block output replaces the accumulators in place (register budget)
+              float sum = 0.f;
 #pragma unroll
-        for (int i = 0; i < K::I1; ++i) {
-          const int t = wave + 4 * i;
-          if (t < K::MTH) {
-            const bf16x8 xb = *reinterpret_cast<const bf16x8*>(&sX[16 * t + fr][32 * ks + fk]);
+              for (int j = 0; j < K::NT2; ++j) {
+                const float4 bb = *reinterpret_cast<const float4*>(sEp + 16 * j + 4 * fq);
+                const uint2 xr = *reinterpret_cast<const uint2*>(sXr + ((i * 16 + fr) * C + 16 * j + 4 * fq) * 2);
+                const f32x2 x01 = unpack2<T>(xr.x), x23 = unpack2<T>(xr.y);
+                T o4[4] = {(T)(acc2[i][j][0] + bb.x + x01.x), (T)(acc2[i][j][1] + bb.y + x01.y),
+                           (T)(acc2[i][j][2] + bb.z + x23.x), (T)(acc2[i][j][3] + bb.w + x23.y)};
 #pragma unroll
-            for (int jh = 0; jh < 4; ++jh)
-              acc1[jh][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[ks][jh], xb, acc1[jh][i], 0, 0, 0);
+                for (int r = 0; r < 4; ++r) { acc2[i][j][r] = (float)o4[r]; sum += acc2[i][j][r]; }
+                if (ok && Y) *reinterpret_cast<uint2*>(Y + off + 16 * j) = *reinterpret_cast<const uint2*>(o4);
+                __builtin_amdgcn_sched_barrier(0);   // keep the per-j operand loads from being hoisted (registers)
+              }
+              if (gamma) {   // LayerNorm of the row: its C channels sit in lanes fr, fr + 16, + 32, + 48
+                sum += __shfl_xor(sum, 16, 64);
+                sum += __shfl_xor(sum, 32, 64);
+                const float mean = sum / C;
+                float sq = 0.f;
+#pragma unroll
+                for (int j = 0; j < K::NT2; ++j)
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) { const float dd = acc2[i][j][r] - mean; sq += dd * dd; }
+                sq += __shfl_xor(sq, 16, 64);
+                sq += __shfl_xor(sq, 32, 64);
+                const float rstd = 1.0f / sqrtf(sq / C + eps);
+#pragma unroll
+                for (int j = 0; j < K::NT2; ++j) {
+                  const float4 gg = *reinterpret_cast<const float4*>(sEp + C + 16 * j + 4 * fq);
+                  const float4 be = *reinterpret_cast<const float4*>(sEp + 2 * C + 16 * j + 4 * fq);
+                  T n4[4] = {(T)((acc2[i][j][0] - mean) * rstd * gg.x + be.x), (T)((acc2[i][j][1] - mean) * rstd * gg.y + be.y),
+                             (T)((acc2[i][j][2] - mean) * rstd * gg.z + be.z), (T)((acc2[i][j][3] - mean) * rstd * gg.w + be.w)};
+                  if (ok) *reinterpret_cast<uint2*>(Yn + off + 16 * j) = *reinterpret_cast<const uint2*>(n4);
+                  __builtin_amdgcn_sched_barrier(0);
+                }
+              }
+#pragma unroll
+              for (int j = 0; j < K::NT2; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
           }
         }
       }
-      // + b1, zero the tokens outside the image (dwconv zero padding) -> sH (bf16, like the unfused path)
-      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      if (s < T_) {
+        // ---- fc1 of item s -> sH(s & 1): halo tokens x HC hidden channels of chunk c1
+        const int c1 = s % NCH;
+        int b, y0;
+        strip_of(s / NCH, b, y0);
+        uint32_t* H1 = sH(s & 1);
+        float bv[K::NT1];
 #pragma unroll
-      for (int i = 0; i < K::I1; ++i) {
-        const int t = wave + 4 * i;
-        if (t >= K::MTH) continue;
-        const int row = 16 * t + fr;                 // halo token
-        const int hy = row / K::HW_, hx = row - hy * K::HW_;
-        const int iy = y0 - 1 + hy, ix = x0 - 1 + hx;
-        const bool ok = row < K::NH && iy >= 0 && iy < H && ix >= 0 && ix < W;
+        for (int j = 0; j < K::NT1; ++j) bv[j] = sB1[c1 * HC + 16 * j + fr];
+        auto store_tile = [&](int mt, const f32x4* acc) __attribute__((always_inline)) {
+          // lane holds tokens t0 .. t0 + 3 (one image row, t0 % 4 == 0) of hidden channel 16 j + fr
+          const int t0 = 16 * mt + 4 * fq;
+          if (t0 < K::NH) {
+            const int ty = t0 / W, tx = t0 - ty * W;
+            const int yy = y0 - 1 + ty;
+            const bool ok = yy >= 0 && yy < H;
+            uint32_t* dst = H1 + (ty * NPC + (tx >> 1) + 1) * CS + fr;
 #pragma unroll
-        for (int jh = 0; jh < 4; ++jh) {
-          bf16x4 hv;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) hv[r] = (bf16)(ok ? acc1[jh][i][r] + b1v[jh][r] : 0.f);
-          *reinterpret_cast<bf16x4*>(&sH[row][16 * jh + (lane >> 4) * 4]) = hv;
-        }
-      }
-    }
-    w1_fetch(hc + 1 < K::NCH ? hc + 1 : hc);   // refill: lands during dwconv + fc2
-    __syncthreads();
-
-    // ---- (2) depthwise 3x3 + bias + GELU: thread -> channel group c8, tokens o = tid/8 + 32 i
-    {
-#pragma unroll
-      for (int i = 0; i < (K::MTO * 16 + 31) / 32; ++i) {
-        const int o = (tid >> 3) + 32 * i;
-        if (o >= K::MTO * 16) break;
-        float v[8];
-        *reinterpret_cast<float4*>(&v[0]) = *reinterpret_cast<const float4*>(&sT[9][c8]);
-        *reinterpret_cast<float4*>(&v[4]) = *reinterpret_cast<const float4*>(&sT[9][c8 + 4]);
-        if (o < K::NO) {
-          const int oy = o / TW, ox = o - oy * TW;
-#pragma unroll
-          for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {
-              const bf16x8 h = *reinterpret_cast<const bf16x8*>(&sH[(oy + dy) * K::HW_ + ox + dx][c8]);
-              float w[8];
-              *reinterpret_cast<float4*>(&w[0]) = *reinterpret_cast<const float4*>(&sT[dy * 3 + dx][c8]);
-              *reinterpret_cast<float4*>(&w[4]) = *reinterpret_cast<const float4*>(&sT[dy * 3 + dx][c8 + 4]);
-#pragma unroll
-              for (int q = 0; q < 8; ++q) v[q] += (float)h[q] * w[q];
+            for (int j = 0; j < K::NT1; ++j) {
+              dst[16 * j] = ok ? pack2<T>(acc[j][0] + bv[j], acc[j][1] + bv[j]) : 0u;
+              dst[CS + 16 * j] = ok ? pack2<T>(acc[j][2] + bv[j], acc[j][3] + bv[j]) : 0u;
             }
-        }
-        bf16x8 gv;
+          }
+        };
+        // m-tile outer: the chunk's W1 fragments held, one accumulator set live at a time
+        tx8 wb[K::KS][K::NT1];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) gv[q] = (bf16)gelu_fast(v[q]);
-        *reinterpret_cast<bf16x8*>(&sG[o][c8]) = gv;
+        for (int ks = 0; ks < K::KS; ++ks)
+#pragma unroll
+          for (int j = 0; j < K::NT1; ++j) wb[ks][j] = *reinterpret_cast<const tx8*>(&sW1[swz<CPR1>(c1 * HC + 16 * j + fr, 4 * ks + fq)]);
+#pragma unroll
+        for (int i = 0; i < K::I1; ++i)
+          if (pw + K::NPW * i < K::MTH) {
+            f32x4 acc[K::NT1];
+#pragma unroll
+            for (int j = 0; j < K::NT1; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int ks = 0; ks < K::KS; ++ks)
+#pragma unroll
+              for (int j = 0; j < K::NT1; ++j) acc[j] = mfma16x16x32(xa[i][ks], wb[ks][j], acc[j]);
+            store_tile(pw + K::NPW * i, acc);
+          }
+        // the strip's last chunk consumed xa: fetch the next strip's fragments
+        // the strip's last chunk consumed xa: fetch the next strip's fragments
+        if (c1 == NCH - 1 && s / NCH + 1 < nst) load_xa(s / NCH + 1, xa);
       }
+      barrier();
     }
-    __syncthreads();
-
-    // ---- (3) fc2 partial: acc2 += G (tile x 64) . W2[:, chunk]^T
+  } else {
+    // ===== dwconv waves: item s - 1, sH(p) -> sG(p), p = (s - 1) & 1 =====
+    // wave = one channel quad (4 channels) of the chunk, so its taps are wave-uniform (scalar loads, no
+    // LDS traffic); lane = a pixel pair x RV output rows; 16-byte reads of 4 channel pairs
+    const int dq = wave - K::NPW;
+    const bool has_item = lane < K::NITEM;
+    const int dp = lane % K::NPAIR, dg = lane / K::NPAIR;
+    uint4 tv[13];                // taps of the current item, refilled for the next one before the barrier
+    auto tload = [&](int g) __attribute__((always_inline)) {
+      const uint4* tq = sTp + ((g % NCH) * K::NQ + dq) * 13;   // wave-uniform LDS address: broadcast reads
 #pragma unroll
-    for (int ks = 0; ks < HC / 32; ++ks) {
-      bf16x8 bfr[K::NT2];
+      for (int i = 0; i < 13; ++i) tv[i] = tq[i];
+    };
+    if (T_ > 0) tload(0);
+    for (int s = 0; s < T_ + 2; ++s) {
+      const int g = s - 1;
+      if (g >= 0 && g < T_) {
+        const int p = g & 1;
+        const uint32_t* H0 = sH(p);
+        char* G0 = sG(p);
+        // packed taps of channel 4 quad + c: 12 records {dy, c: (w1,w2), (w0,w1), (0,w0), (w2,0)} + bias
+        uint32_t w12[4][3], w01[4][3], wz0[4][3], w2z[4][3];
 #pragma unroll
-      for (int j = 0; j < K::NT2; ++j) bfr[j] = *reinterpret_cast<const bf16x8*>(&sW2[16 * j + fr][32 * ks + fk]);
+        for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-      for (int i = 0; i < K::I2; ++i) {
-        const int t = wave + 4 * i;
-        if (t < K::MTO) {
-          const bf16x8 a = *reinterpret_cast<const bf16x8*>(&sG[16 * t + fr][32 * ks + fk]);
+          for (int c = 0; c < 4; ++c) {
+            const uint4 t = tv[dy * 4 + c];
+            w12[c][dy] = t.x; w01[c][dy] = t.y; wz0[c][dy] = t.z; w2z[c][dy] = t.w;
+          }
+        const float bias[4] = {__uint_as_float(tv[12].x), __uint_as_float(tv[12].y), __uint_as_float(tv[12].z),
+                               __uint_as_float(tv[12].w)};
+        float acc[K::RV][4][2];
 #pragma unroll
-          for (int j = 0; j < K::NT2; ++j) acc2[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bfr[j], acc2[i][j], 0, 0, 0);
+        for (int rr = 0; rr < K::RV; ++rr)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[rr][c][0] = acc[rr][c][1] = bias[c];
+        const uint4* H4 = reinterpret_cast<const uint4*>(H0);
+#pragma unroll
+        for (int ir = 0; ir < K::RV + 2; ++ir) {            // halo row dg*RV + ir
+          const int pc = (dg * K::RV + ir) * NPC + dp;
+          const uint4 L = H4[pc * (CS / 4) + dq], M = H4[(pc + 1) * (CS / 4) + dq], Rt = H4[(pc + 2) * (CS / 4) + dq];
+          const uint32_t l4[4] = {L.x, L.y, L.z, L.w}, m4[4] = {M.x, M.y, M.z, M.w}, r4[4] = {Rt.x, Rt.y, Rt.z, Rt.w};
+#pragma unroll
+          for (int rr = 0; rr < K::RV; ++rr) {
+            const int dy = ir - rr;
+            if (dy < 0 || dy > 2) continue;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              acc[rr][c][0] = P2<T>::dot(m4[c], w12[c][dy], P2<T>::dot(l4[c], wz0[c][dy], acc[rr][c][0]));
+              acc[rr][c][1] = P2<T>::dot(m4[c], w01[c][dy], P2<T>::dot(r4[c], w2z[c][dy], acc[rr][c][1]));
+            }
+          }
+          // output row rr = ir - 2 is complete: GELU -> sG (two tokens, 4 channels = 8 bytes each)
+          const int rr = ir - 2;
+          if (rr >= 0 && has_item) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int o = (dg * K::RV + rr) * W + 2 * dp + h;
+              uint2 v;
+              v.x = pack2<T>(gelu_dw(acc[rr][0][h]), gelu_dw(acc[rr][1][h]));
+              v.y = pack2<T>(gelu_dw(acc[rr][2][h]), gelu_dw(acc[rr][3][h]));
+              *reinterpret_cast<uint2*>(G0 + o * K::GROW + (((dq >> 1) ^ gsw(o)) << 4) + (dq & 1) * 8) = v;
+            }
+          }
         }
       }
+      if (g + 1 >= 0 && g + 1 < T_ && g >= 0) tload(g + 1);   // next item's taps: covered by the barrier's wait
+      barrier();
     }
-  }
-  __syncthreads();
-
-  // ---- epilogue: + b2 -> f32 tile in LDS -> + residual -> 16-byte stores
-#pragma unroll
-  for (int i = 0; i < K::I2; ++i) {
-    const int t = wave + 4 * i;
-    if (t >= K::MTO) continue;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int o = 16 * t + (lane >> 4) * 4 + r;
-      if (o >= K::NO) continue;
-#pragma unroll
-      for (int j = 0; j < K::NT2; ++j) sO[o][16 * j + fr] = acc2[i][j][r] + b2[16 * j + fr];
-    }
-  }
-  __syncthreads();
-  constexpr int CPR = C / 8;
-  constexpr int NIT = (K::NO * CPR + 255) / 256;
-  bf16x8 xr[NIT];
-  long offs[NIT];
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {       // residual loads first, clamped in range
-    const int e = min(tid + 256 * it, K::NO * CPR - 1);
-    const int o = e / CPR, c8 = (e % CPR) * 8;
-    const int oy = o / TW, ox = o - oy * TW;
-    const int iy = min(y0 + oy, H - 1), ix = min(x0 + ox, W - 1);
-    offs[it] = (img + (long)iy * W + ix) * C + c8;
-    xr[it] = *reinterpret_cast<const bf16x8*>(X + offs[it]);
-  }
-#pragma unroll
-  for (int it = 0; it < NIT; ++it) {
-    const int e = tid + 256 * it;
-    if (e >= K::NO * CPR) continue;
-    const int o = e / CPR, c8 = (e % CPR) * 8;
-    const int oy = o / TW, ox = o - oy * TW;
-    if (y0 + oy >= H || x0 + ox >= W) continue;
-    bf16x8 out;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) out[q] = (bf16)(sO[o][c8 + q] + (float)xr[it][q]);
-    *reinterpret_cast<bf16x8*>(Y + offs[it]) = out;
   }
 }
 
-template <int C, int TH, int TW>
-static int launch(const void* XN, const void* X, const void* W1, const float* b1, const float* taps, const float* db,
-                  const void* W2, const float* b2, void* Y, int B, int H, int W, hipStream_t st) {
-  const int tx = (W + TW - 1) / TW, ty = (H + TH - 1) / TH;
-  const long nwg = (long)B * tx * ty;
-  hipLaunchKernelGGL((mixffn_bf16<C, TH, TW>), dim3((unsigned)nwg), dim3(256), 0, st, (const bf16*)XN, (const bf16*)X,
-                     (const bf16*)W1, b1, taps, db, (const bf16*)W2, b2, (bf16*)Y, H, W, tx, ty);
-  return check_launch("mixffn_bf16");
+template <typename T, class K>
+static int launch(const void* XN, const void* X, const void* W1, const float* b1, const void* tpk, const void* W2,
+                  const float* b2, void* Y, void* Yn, const float* gamma, const float* beta, float eps, int B, int H,
+                  hipStream_t st) {
+  const int nstrip = (H + K::R - 1) / K::R;
+  const long total = (long)B * nstrip;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mixffn_ws<T, K>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
+    cus = std::max(cus, 1);
+  }
+  if (total > 0x7fffffffL) { set_error("svk_mixffn_fused: too many strips"); return SVK_EINVAL; }
+  const int grid = (int)std::min<long>(total, cus);
+  hipLaunchKernelGGL((mixffn_ws<T, K>), dim3(grid), dim3(K::NT), K::LDS, st, (const T*)XN, (const T*)X, (const T*)W1,
+                     b1, (const uint4*)tpk, (const T*)W2, b2, (T*)Y, (T*)Yn, gamma, beta, eps, H, nstrip, (int)total);
+  static char name[96];
+  if (!name[0])
+    snprintf(name, sizeof(name), "mixffn_ws<%s, Cfg<%d, %d, %d, %d, %d>>", type_name<T>(), K::C, K::W, K::R, K::RV,
+             K::HC);
+  set_last_kernel(name);
+  return check_launch("mixffn_ws");
+}
+
+template <typename T>
+static int dispatch(const void* XN, const void* X, const void* W1, const float* b1, const void* tpk, const void* W2,
+                    const float* b2, void* Y, void* Yn, const float* gamma, const float* beta, float eps, int B, int H,
+                    int W, int C, hipStream_t st) {
+  // stage-1 / stage-2 shapes of the 224 x 224 MiT path (C = 32 / 64 at W = 56, 64 / 128 at W = 28)
+#define SVK_FFN(CC, WW, RR, RVV) \
+  if (W == WW && C == CC) return launch<T, Cfg<CC, WW, RR, RVV, 32>>(XN, X, W1, b1, tpk, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  SVK_FFN(64, 56, 2, 1)
+  SVK_FFN(32, 56, 2, 1)
+#undef SVK_FFN
+  set_error("svk_mixffn_fused: (W=%d, C=%d) not instantiated", W, C);
+  return SVK_EUNSUPPORTED;
 }
 
 }  // namespace ffn
@@ -306,30 +459,27 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
 
 using namespace svk;
 
+extern "C" int svk_mixffn_supported(int W, int C) {
+  return W == 56 && (C == 64 || C == 32);
+}
+
 extern "C" int svk_mixffn_fused(int dtype, const void* XN, const void* X, const void* W1, const float* b1,
-                                const float* taps, const float* dbias, const void* W2, const float* b2, void* Y,
-                                int B, int H, int W, int C, void* stream) {
-  if (dtype != SVK_BF16) { set_error("svk_mixffn_fused: bf16 only"); return SVK_EUNSUPPORTED; }
-  if (B < 0 || H <= 0 || W <= 0 || !XN || !X || !W1 || !b1 || !taps || !dbias || !W2 || !b2 || !Y) {
+                                const void* tpk, const void* W2, const float* b2, void* Y,
+                                void* Yn, const float* gamma, const float* beta, float eps, int B, int H, int W,
+                                int C, void* stream) {
+  if (B < 0 || H <= 0 || !XN || !X || !W1 || !b1 || !tpk || !W2 || !b2 || (!Y && !gamma) ||
+      (gamma && (!beta || !Yn))) {
     set_error("svk_mixffn_fused: bad args"); return SVK_EINVAL;
   }
-  if ((((uintptr_t)XN) | ((uintptr_t)X) | ((uintptr_t)W1) | ((uintptr_t)W2) | ((uintptr_t)Y)) & 15) {
+  if ((((uintptr_t)XN) | ((uintptr_t)X) | ((uintptr_t)W1) | ((uintptr_t)W2) | ((uintptr_t)Y) | ((uintptr_t)Yn) |
+       ((uintptr_t)tpk) | ((uintptr_t)b2) | ((uintptr_t)gamma) | ((uintptr_t)beta)) & 15) {
     set_error("svk_mixffn_fused: pointers must be 16-byte aligned"); return SVK_EINVAL;
+  }
+  if (!svk_mixffn_supported(W, C)) {
+    set_error("svk_mixffn_fused: (W=%d, C=%d) not instantiated", W, C); return SVK_EUNSUPPORTED;
   }
   if (B == 0) return SVK_OK;
   hipStream_t st = (hipStream_t)stream;
-  // 4 x 14 output tiles (6 x 16 halo) keep LDS and registers small enough for several workgroups
-  // per CU, so one workgroup's VALU dwconv phase overlaps another's MFMA phases; 14x14 maps use 7 x 14.
-  const bool rows7 = (H % 4 != 0) && (H % 7 == 0);
-  switch (C) {
-    case 32: return rows7 ? ffn::launch<32, 7, 14>(XN, X, W1, b1, taps, dbias, W2, b2, Y, B, H, W, st)
-                          : ffn::launch<32, 4, 14>(XN, X, W1, b1, taps, dbias, W2, b2, Y, B, H, W, st);
-    case 64: return rows7 ? ffn::launch<64, 7, 14>(XN, X, W1, b1, taps, dbias, W2, b2, Y, B, H, W, st)
-                          : ffn::launch<64, 4, 14>(XN, X, W1, b1, taps, dbias, W2, b2, Y, B, H, W, st);
-    case 128: return rows7 ? ffn::launch<128, 7, 14>(XN, X, W1, b1, taps, dbias, W2, b2, Y, B, H, W, st)
-                           : ffn::launch<128, 4, 14>(XN, X, W1, b1, taps, dbias, W2, b2, Y, B, H, W, st);
-    default:
-      set_error("svk_mixffn_fused: C=%d not instantiated (32/64/128)", C);
-      return SVK_EUNSUPPORTED;
-  }
+  SVK_DISPATCH_H16(dtype, T, return ffn::dispatch<T>(XN, X, W1, b1, tpk, W2, b2, Y, Yn, gamma, beta, eps, B, H,
+                                                     W, C, st));
 }

@@ -40,8 +40,11 @@ class DWConv(nn.Module):
 
     def _pack(self, dt):
         c = self.dwconv.weight.shape[0]
-        return dict(taps=self.dwconv.weight.detach().float().reshape(c, 9).t().contiguous(),
-                    b=self.dwconv.bias.detach().float().contiguous())
+        p = dict(taps=self.dwconv.weight.detach().float().reshape(c, 9).t().contiguous(),
+                 b=self.dwconv.bias.detach().float().contiguous())
+        if dt in ops.H16:   # records of the whole-MixFFN kernel
+            p["tpk"] = ops.mixffn_pack_taps(p["taps"], p["b"], dt)
+        return p
 
     def forward(self, x, H, W, act=None):
         """x [B, N, C] tokens (N = H*W) -> [B, N, C]; ``act`` lets Mlp fuse its GELU."""
@@ -69,28 +72,33 @@ class Mlp(nn.Module):
     def _pack(self, dt):
         return dict(w1=lin_w(self.fc1, dt), b1=lin_b(self.fc1), w2=lin_w(self.fc2, dt), b2=lin_b(self.fc2))
 
-    def forward(self, x, H, W, residual=None):
+    def forward(self, x, H, W, residual=None, ln=None):
+        """``ln = (gamma, beta, eps)``: return LayerNorm(residual + mlp(x)) (the stage norm that follows the
+        last Block, fused into the whole-MixFFN kernel's epilogue when it runs)."""
         p = get_packed(self, x.dtype, self._pack)
         B, N, C = x.shape
-        if (ops.FUSED_MIXFFN and residual is not None and x.dtype == torch.bfloat16 and C in ops.MIXFFN_CHANNELS
-                and self.fc1.out_features == 4 * C and self.fc2.out_features == C):
-            # one kernel: fc1 -> dwconv3x3 -> GELU -> fc2 -> + residual, hidden kept on chip
-            # (opt-in, SVK_FUSED_MIXFFN=1: measured slower than the three-kernel path so far)
+        hid = self.fc1.out_features
+        if (ops.FUSED_MIXFFN and residual is not None and x.dtype in ops.H16 and hid == 4 * C
+                and self.fc2.out_features == C and ops.mixffn_supported(W, C)):
+            # fc1 -> dwconv3x3 -> GELU -> fc2 -> + residual (-> LayerNorm) in one kernel, hidden on chip
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             y = ops.mixffn_fused(x.contiguous().view(B, H, W, C), residual.contiguous().view(B, H, W, C),
-                                 p["w1"], p["b1"], pd["taps"], pd["b"], p["w2"], p["b2"])
+                                 p["w1"], p["b1"], pd["tpk"], p["w2"], p["b2"], ln=ln)
             return y.view(B, N, C)
-        hid = self.fc1.out_features
         # measured: wins where the hidden map is largest (stages 1-2, C <= 128); at C = 320 / 512 the
         # recomputed halo fc1 work outweighs the saved traffic
         if ops.FC1_DWCONV and x.dtype in ops.H16 and C in (32, 64, 128) and hid % 64 == 0:
             # fc1 -> DWConv -> GELU in one kernel, the hidden map kept on chip (Mlp.forward :60-63)
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")
-            return ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
-        h = ops.gemm(x, p["w1"], p["b1"])
-        h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)
-        return ops.gemm(h, p["w2"], p["b2"], residual=residual)
+            y = ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
+        else:
+            h = ops.gemm(x, p["w1"], p["b1"])
+            h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)
+            y = ops.gemm(h, p["w2"], p["b2"], residual=residual)
+        if ln is not None:
+            ops.layernorm(y, ln[0], ln[1], ln[2], out=y)
+        return y
 
 
 class Attention(nn.Module):
@@ -158,13 +166,14 @@ class Block(nn.Module):
         g2, b2 = _ln_params(self.norm2)
         return dict(g1=g1, b1=b1, g2=g2, b2=b2)
 
-    def forward(self, x, H, W):
+    def forward(self, x, H, W, ln=None):
+        """``ln``: (gamma, beta, eps) of a LayerNorm applied to the block output (see Mlp.forward)."""
         p = get_packed(self, x.dtype, self._pack)
         x = x.contiguous()
         h = ops.layernorm(x, p["g1"], p["b1"], self.norm1.eps)
         x = self.attn(h, H, W, residual=x)
         h = ops.layernorm(x, p["g2"], p["b2"], self.norm2.eps)
-        return self.mlp(h, H, W, residual=x)
+        return self.mlp(h, H, W, residual=x, ln=ln)
 
 
 class OverlapPatchEmbed(nn.Module):
@@ -471,12 +480,15 @@ class MixVisionTransformerEVP(nn.Module):
         for s in range(4):
             t, H, W = getattr(self, f"patch_embed{s + 1}").embed_nhwc(h)
             prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1)
-            for i, blk in enumerate(getattr(self, f"block{s + 1}")):
-                t = self.prompt_generator.get_prompt(t, prompt, s + 1, i)
-                t = blk(t, H, W)
             norm = getattr(self, f"norm{s + 1}")
             pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
-            ops.layernorm(t, pn[0], pn[1], norm.eps, out=t)
+            blocks = getattr(self, f"block{s + 1}")
+            for i, blk in enumerate(blocks):
+                t = self.prompt_generator.get_prompt(t, prompt, s + 1, i)
+                # the stage norm (:370-412) rides on the last block's MixFFN epilogue
+                t = blk(t, H, W, ln=(pn[0], pn[1], norm.eps) if i == len(blocks) - 1 else None)
+            if len(blocks) == 0:
+                t = ops.layernorm(t, pn[0], pn[1], norm.eps)
             outs.append((t, H, W))
             h = t.view(t.shape[0], H, W, -1)
         return outs

@@ -54,7 +54,7 @@ SIGNATURES = {
     "svk_anticipation_gt": [P, c_long, c_int, c_int, ctypes.c_double, P, P],
     "svk_window_unfold": [c_int, P, c_long, P, P, c_int, c_int, c_int, P],
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
-    "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
     # training step
     "svk_dwconv3x3_ex": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
@@ -92,6 +92,7 @@ LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int,
               "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int],
               "svk_mstcn_bwd_workspace": [c_int, c_int]}
+INT_QUERIES = {"svk_mixffn_supported": [c_int, c_int]}
 
 _lib = None
 
@@ -125,6 +126,12 @@ def load():
             continue
         fn.argtypes = argtypes
         fn.restype = c_long
+    for name, argtypes in INT_QUERIES.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.argtypes = argtypes
+        fn.restype = c_int
     _lib = lib
     return lib
 

@@ -254,28 +254,61 @@ def attention(q, k, v, heads, scale, out=None):
     return out
 
 
-MIXFFN_CHANNELS = (32, 64, 128)
-FUSED_MIXFFN = os.environ.get("SVK_FUSED_MIXFFN", "0") == "1"
+FUSED_MIXFFN = os.environ.get("SVK_FUSED_MIXFFN", "1") == "1"
 
 
-def mixffn_fused(xn, x, w1, b1, taps, dbias, w2, b2):
-    """x + fc2(GELU(dwconv3x3(fc1(xn)))) on NHWC [B, H, W, C] bf16 maps (hidden kept on chip)."""
+def mixffn_supported(W, C):
+    """True when svk_mixffn_fused has an instantiation for map width W and channels C."""
+    return bool(_lib.load().svk_mixffn_supported(int(W), int(C)))
+
+
+def mixffn_pack_taps(taps, dbias, dtype):
+    """Depthwise taps [9, hid] f32 (row dy*3+dx) + bias [hid] f32 -> the packed form svk_mixffn_fused
+    reads (include/svk.h): per channel quad q (channels 4q..4q+3) 13 16-byte records — 12 for
+    (dy, c) = the dtype pairs (w1,w2), (w0,w1), (0,w0), (w2,0) of tap row dy of channel 4q + c — then the
+    4 biases as f32; int32 [hid / 4 * 52]."""
+    hid = taps.shape[1]
+    w = taps.t().reshape(hid, 3, 3).to(dtype)                        # [ch][dy][dx]
+    z = torch.zeros_like(w[..., 0])
+    pairs = torch.stack([torch.stack([w[..., 1], w[..., 2]], -1), torch.stack([w[..., 0], w[..., 1]], -1),
+                         torch.stack([z, w[..., 0]], -1), torch.stack([w[..., 2], z], -1)], 2)   # [ch, dy, 4, 2]
+    rec = pairs.contiguous().view(torch.int32).reshape(hid // 4, 4, 3, 4)     # [q][c][dy][word]
+    rec = rec.permute(0, 2, 1, 3).reshape(hid // 4, 48)                       # [q][dy][c][word]
+    bias = dbias.float().contiguous().view(torch.int32).reshape(hid // 4, 4)
+    return torch.cat([rec, bias], 1).contiguous().reshape(-1)
+
+
+def mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=None):
+    """x + fc2(GELU(dwconv3x3(fc1(xn)))) on NHWC [B, H, W, C] bf16 / f16 maps, the 4C hidden kept on
+    chip (svk_mixffn_fused); ``tpk`` from mixffn_pack_taps.  ``ln = (gamma, beta, eps)`` returns the
+    LayerNorm of that sum instead (the stage norm fused into the epilogue; the sum is then not written)."""
+    if xn.dtype not in H16:
+        raise _lib.SvkError("svk.mixffn_fused: bf16 / f16 only")
     for t, nm in ((xn, "xn"), (x, "x"), (w1, "w1"), (w2, "w2")):
-        _chk(t, nm, torch.bfloat16)
+        _chk(t, nm, xn.dtype)
         if not t.is_contiguous():
             raise _lib.SvkError(f"svk.mixffn_fused: {nm} must be contiguous")
-    for t, nm in ((b1, "b1"), (taps, "taps"), (dbias, "dbias"), (b2, "b2")):
+    for t, nm in ((b1, "b1"), (b2, "b2")):
         _chk(t, nm, torch.float32)
+    _chk(tpk, "tpk", torch.int32)
     B, H, W, C = xn.shape
-    if x.shape != xn.shape or w1.shape != (4 * C, C) or w2.shape != (C, 4 * C) or taps.shape != (9, 4 * C):
+    if (x.shape != xn.shape or w1.shape != (4 * C, C) or w2.shape != (C, 4 * C) or tpk.shape != (52 * C,)
+            or not tpk.is_contiguous()):
         raise _lib.SvkError("svk.mixffn_fused: shape mismatch")
     out = torch.empty_like(x)
+    g = bt = None
+    eps = 0.0
+    if ln is not None:
+        g, bt, eps = ln
+        _chk(g, "gamma", torch.float32); _chk(bt, "beta", torch.float32)
     t0 = _prof_begin()
-    _lib.call("svk_mixffn_fused", BF16, _p(xn), _p(x), _p(w1), _p(b1), _p(taps), _p(dbias), _p(w2), _p(b2),
-              _p(out), B, H, W, C, _stream())
+    _lib.call("svk_mixffn_fused", dtype_code(xn.dtype), _p(xn), _p(x), _p(w1), _p(b1), _p(tpk), _p(w2), _p(b2),
+              None if ln is not None else _p(out), _p(out) if ln is not None else None, _p(g), _p(bt), float(eps),
+              B, H, W, C, _stream())
     if t0 is not None:
         M = B * H * W
-        _prof_end(t0, f"mixffn_bf16<{C}>", 2.0 * M * C * 4 * C * 2, (3 * M * C + 8 * C * C) * 2, (M, C, "mixffn"))
+        _prof_end(t0, f"mixffn<{C}>", 2.0 * M * C * 4 * C * 2 + 2.0 * 9 * M * 4 * C,
+                  (3 * M * C + 8 * C * C) * 2, (M, C, "mixffn"))
     return out
 
 

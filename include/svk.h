@@ -91,13 +91,22 @@ int svk_attention(int dtype, const void* Q, long ldq, long sbq, const void* K, l
 int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B,
                   int H, int W, int C, int act, void* stream);
 
-/* Fused MixFFN + Block residual (mix_transformer_evp.py:32-67, 19-30, 169), bf16 only:
- * Y = X + fc2(GELU(dwconv3x3(fc1(XN)))) over NHWC [B, H, W, C] maps, hidden 4C kept on chip.
- * W1 [4C][C], W2 [C][4C] bf16; b1 [4C], taps [9][4C], dbias [4C], b2 [C] f32.  C in {32, 64, 128};
- * SVK_EUNSUPPORTED otherwise (callers then run svk_gemm + svk_dwconv3x3 + svk_gemm). */
-int svk_mixffn_fused(int dtype, const void* XN, const void* X, const void* W1, const float* b1,
-                     const float* taps, const float* dbias, const void* W2, const float* b2, void* Y,
-                     int B, int H, int W, int C, void* stream);
+/* Whole MixFFN + Block residual (mix_transformer_evp.py:32-67, DWConv :19-30, Block :169) in one kernel,
+ * optionally followed by the next LayerNorm (the stage norm :370-412):
+ *   Y = X + fc2(GELU(dwconv3x3(fc1(XN)))),  Yn = LN(Y; gamma, beta, eps) when gamma != NULL (Y may
+ *   then be NULL: only the normalised map is written)
+ * over NHWC [B, H, W, C] bf16 / f16 maps; the 4C-wide hidden map never leaves the chip.  W1 [4C][C],
+ * W2 [C][4C] in the map dtype; b1 [4C], b2 [C], gamma/beta [C] f32.  tpk = the depthwise taps and bias
+ * packed per hidden channel quad q (channels 4q .. 4q+3) as 13 16-byte records: 12 for (dy, c) holding
+ * the 32-bit pairs of the map dtype (w[dy][1], w[dy][2]), (w[dy][0], w[dy][1]), (0, w[dy][0]),
+ * (w[dy][2], 0) of channel 4q + c (element 0 in the low half), then the 4 depthwise biases as f32
+ * (svk.ops.mixffn_pack_taps).  All pointers 16-byte aligned.
+ * Instantiated for the 224x224 MiT stage-1/2 shapes (svk_mixffn_supported(W, C)); SVK_EUNSUPPORTED
+ * otherwise (callers then run svk_mixffn_fc1_dwconv + svk_gemm). */
+int svk_mixffn_supported(int W, int C);
+int svk_mixffn_fused(int dtype, const void* XN, const void* X, const void* W1, const float* b1, const void* tpk,
+                     const void* W2, const float* b2, void* Y, void* Yn, const float* gamma, const float* beta,
+                     float eps, int B, int H, int W, int C, void* stream);
 
 /* MixFFN front half, G = act(dwconv3x3(XN W1^T + b1) + dbias) over NHWC maps (Mlp.fc1 -> DWConv -> GELU,
  * mix_transformer_evp.py:60-63, 24-30): the 4C-wide hidden map stays on chip (fc1 recomputed on one

@@ -35,9 +35,19 @@ def test_library_exports_every_header_symbol():
             assert len(_lib.SIGNATURES[name]) == nargs, f"{name}: ctypes binding has wrong arity"
         elif name in _lib.LONG_FUNCS:
             assert len(_lib.LONG_FUNCS[name]) == nargs, f"{name}: ctypes binding has wrong arity"
+        elif name in _lib.INT_QUERIES:
+            assert len(_lib.INT_QUERIES[name]) == nargs, f"{name}: ctypes binding has wrong arity"
         else:
             assert name in _lib.STRING_FUNCS
-    assert set(_lib.SIGNATURES) | set(_lib.STRING_FUNCS) | set(_lib.LONG_FUNCS) == set(funcs)
+    assert set(_lib.SIGNATURES) | set(_lib.STRING_FUNCS) | set(_lib.LONG_FUNCS) | set(_lib.INT_QUERIES) == set(funcs)
+
+
+def test_mixffn_supported_query():
+    """svk_mixffn_supported needs no GPU: the whole-MixFFN kernel covers the 224x224 stage-1 shapes."""
+    from svk import _lib
+    lib = _lib.load()
+    assert lib.svk_mixffn_supported(56, 64) == 1 and lib.svk_mixffn_supported(56, 32) == 1
+    assert lib.svk_mixffn_supported(28, 128) == 0 and lib.svk_mixffn_supported(14, 320) == 0
 
 
 def test_library_version_and_error_path():

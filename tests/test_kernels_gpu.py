@@ -271,14 +271,17 @@ def test_dwconv3x3_gelu(cuda, dt, B, H, W, C):
     _close(got, F.gelu(ref).permute(0, 2, 3, 1), dt)
 
 
-@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (2, 28, 28, 128), (3, 14, 14, 128), (2, 56, 56, 32),
-                                     (1, 10, 17, 64), (2, 7, 7, 32), (1, 28, 28, 64)])
-def test_mixffn_fused(cuda, B, H, W, C):
-    """Fused fc1 -> dwconv3x3 -> GELU -> fc2 + residual (bf16) against fp64 torch on the same
-    bf16-rounded inputs; the reference path also rounds the hidden to bf16 at the same two points
-    (after fc1, after GELU) as the unfused svk path does."""
+@pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,H,W,C,ln", [(2, 56, 56, 64, False), (2, 56, 56, 32, False), (1, 10, 56, 64, True),
+                                        (3, 7, 56, 32, True), (2, 56, 56, 64, True), (5, 3, 56, 64, False)])
+def test_mixffn_fused(cuda, dt, B, H, W, C, ln):
+    """Whole MixFFN (fc1 -> dwconv3x3 -> GELU -> fc2 + residual [-> LayerNorm]) in one kernel against
+    fp64 torch on the same rounded inputs.  The reference rounds where the kernel stores in the map
+    dtype: the fc1 output (hidden, on chip), the depthwise taps (autocast casts the conv weight too) and
+    the GELU output; H = 7 / 3 leave a partial last strip, B = 5 more strips than one pass of the
+    persistent grid covers when few CUs are free (the pipeline runs across strips)."""
     from svk import ops
-    dt = torch.bfloat16
+    assert ops.mixffn_supported(W, C)
     xn = _rand(B, H, W, C, dt=dt, dev=cuda, seed=40)
     x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=41)
     w1 = _rand(4 * C, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=42)
@@ -287,13 +290,17 @@ def test_mixffn_fused(cuda, B, H, W, C):
     db = _rand(4 * C, dt=torch.float32, dev=cuda, scale=0.1, seed=45)
     w2 = _rand(C, 4 * C, dt=dt, dev=cuda, scale=(4 * C) ** -0.5, seed=46)
     b2 = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=47)
-    got = ops.mixffn_fused(xn, x, w1, b1, taps, db, w2, b2)
+    gam = (1 + _rand(C, dt=torch.float32, dev=cuda, scale=0.2, seed=48)) if ln else None
+    bet = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=49) if ln else None
+    got = ops.mixffn_fused(xn, x, w1, b1, ops.mixffn_pack_taps(taps, db, dt), w2, b2, ln=(gam, bet, 1e-6) if ln else None)
     torch.cuda.synchronize()
     h = (xn.cpu().double() @ w1.cpu().double().t() + b1.cpu().double()).to(dt).double()
     hc = h.permute(0, 3, 1, 2)
-    k = taps.cpu().double().t().reshape(4 * C, 1, 3, 3)
+    k = taps.cpu().to(dt).double().t().reshape(4 * C, 1, 3, 3)
     g = F.gelu(F.conv2d(hc, k, db.cpu().double(), padding=1, groups=4 * C)).permute(0, 2, 3, 1).to(dt).double()
     ref = x.cpu().double() + g @ w2.cpu().double().t() + b2.cpu().double()
+    if ln:
+        ref = F.layer_norm(ref.to(dt).double(), (C,), gam.cpu().double(), bet.cpu().double(), 1e-6)
     _close(got, ref, dt)
 
 

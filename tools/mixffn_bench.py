@@ -10,9 +10,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 from svk import ops  # noqa: E402
 
 
-def run(B, H, C, reps, only):
+def run(B, H, C, reps, only, dt=torch.float16):
     dev = torch.device("cuda:0")
-    dt = torch.bfloat16
     xn = torch.randn(B, H, H, C, device=dev).to(dt)
     x = torch.randn(B, H, H, C, device=dev).to(dt)
     w1 = (torch.randn(4 * C, C, device=dev) * C ** -0.5).to(dt)
@@ -21,17 +20,27 @@ def run(B, H, C, reps, only):
     db = torch.randn(4 * C, device=dev) * 0.1
     w2 = (torch.randn(C, 4 * C, device=dev) * (4 * C) ** -0.5).to(dt)
     b2 = torch.randn(C, device=dev) * 0.1
+    tpk = ops.mixffn_pack_taps(taps, db, dt)
 
     def fused():
-        return ops.mixffn_fused(xn, x, w1, b1, taps, db, w2, b2)
+        return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2)
+
+    def fused_ln():
+        return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=(b2 + 1, b2, 1e-6))
+
+    def fc1dw():
+        g = ops.mixffn_fc1_dwconv(xn, w1, b1, taps, db, act="gelu")
+        return ops.gemm(g.view(-1, 4 * C), w2, b2, residual=x.view(-1, C))
 
     def unfused():
         h = ops.gemm(xn.view(-1, C), w1, b1)
         g = ops.dwconv3x3(h.view(B, H, H, 4 * C), taps, db, act="gelu")
         return ops.gemm(g.view(-1, 4 * C), w2, b2, residual=x.view(-1, C))
 
-    for name, fn in (("fused", fused), ("unfused", unfused)):
+    for name, fn in (("fused", fused), ("fused_ln", fused_ln), ("fc1dw", fc1dw), ("unfused", unfused)):
         if only and name != only:
+            continue
+        if name.startswith("fused") and not ops.mixffn_supported(H, C):
             continue
         fn()
         torch.cuda.synchronize()

@@ -1,0 +1,63 @@
+"""Persistent-GEMM tile sweep on the MFMA-heavy MiT-b2 (B = 256) shapes, f16: every pk_cfg variant
+interleaved in one process.  Usage (GPU box): python tools/pk_cfg_sweep.py [--reps 30]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "deep-learning-for-surgical-video-analysis_amd"))
+from svk import ops, _lib  # noqa: E402
+
+SHAPES = [  # (M, N, K, residual, what)
+    (50176, 320, 1280, True, "s3 fc2"), (50176, 1280, 320, False, "s3 fc1"), (50176, 320, 320, True, "s3 q/proj"),
+    (12544, 640, 320, False, "s3 kv"), (12544, 2048, 512, False, "s4 fc1"), (12544, 512, 2048, True, "s4 fc2"),
+    (12544, 512, 512, True, "s4 q/proj"), (12544, 1024, 512, False, "s4 kv"), (12544, 2048, 1024, False, "head"),
+    (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"),
+]
+CFGS = [(-1, "auto"), (0, "128x128"), (10, "128x64"), (40, "128x160"), (50, "256x128")]
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=30)
+    args = ap.parse_args()
+    dt, dev = torch.float16, torch.device("cuda:0")
+    lib = _lib.load()
+    for M, N, K, res, what in SHAPES:
+        a = torch.randn(M, K, device=dev).to(dt)
+        w = (torch.randn(N, K, device=dev) * K ** -0.5).to(dt)
+        b = torch.randn(N, device=dev)
+        r = torch.randn(M, N, device=dev).to(dt) if res else None
+        out = torch.empty(M, N, device=dev, dtype=dt)
+        ref = None
+        row = []
+        for cfg, name in CFGS:
+            if cfg == 40 and N % 160:
+                continue
+            lib.svk_tune(b"pk_cfg", cfg)
+            y = ops.gemm(a, w, b, residual=r, out=out).clone()
+            if ref is None:
+                ref = y
+            err = float((y.float() - ref.float()).abs().max())
+            ms = timeit(lambda: ops.gemm(a, w, b, residual=r, out=out), args.reps)
+            row.append(f"{name} {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF d={err:.1e}")
+        lib.svk_tune(b"pk_cfg", -1)
+        print(f"{what:10s} ({M},{N},{K}) " + " | ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()
