@@ -398,6 +398,138 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restri
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32 MFMA attention (v_mfma_f32_16x16x4_f32: f32 operands, exact f32 products, f32 accumulation —
+// the parity path of generate_evp_LFB.py's fp32 extraction).  Same structure as the resident-K/V
+// 16-bit kernel: the whole K and V of one (batch, head) are staged in LDS (f32, row-major, rows
+// padded by 4 floats so the fragment reads of keys 4 apart fall in different banks) once per
+// workgroup of 256 queries; each wave walks 16-query tiles.
+//   S^T = K . Q^T   A = K rows (lane: key 16t + (lane & 15)), B = the wave's Q rows held in registers;
+//                   the reduction index d is assigned d = (HDP / 4) g + ks to lane group g = lane >> 4
+//                   (any bijection works when A and B agree), so a lane's 16 K values per key tile are
+//                   CONTIGUOUS: 16-byte LDS reads, and its Q fragment is HDP / 4 consecutive floats.
+//   C layout: lane column (lane & 15) = query, rows 4g + r = keys -> softmax in registers + 2 shuffles.
+//   O = P . V       k-step (t, r) covers keys {16t + 4g + r : g < 4}: lane group g supplies exactly the
+//                   P value it holds, and B = V[16t + 4g + r][16 dt + (lane & 15)].
+template <int HDP, int NKC>
+__global__ __launch_bounds__(256) void attention_mfma_f32(const float* __restrict__ Q, long ldq, long sbq,
+                                                          const float* __restrict__ K, long ldk, long sbk,
+                                                          const float* __restrict__ V, long ldv, long sbv,
+                                                          float* __restrict__ O, long ldo, long sbo, int Nq, int Nk,
+                                                          int hd, float scale_log2) {
+  constexpr int KC = 64, NKP = NKC * KC, LDR = HDP + 4, QD = HDP / 4, NDT = HDP / 16, QB = 256;
+  extern __shared__ __attribute__((aligned(16))) float smf[];
+  float* sK = smf;                  // [NKP][LDR]
+  float* sV = smf + NKP * LDR;      // [NKP][LDR]
+  const int b = blockIdx.z, h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c = lane & 15;
+  const float* Qb = Q + (long)b * sbq + (long)h * hd;
+  const float* Kb = K + (long)b * sbk + (long)h * hd;
+  const float* Vb = V + (long)b * sbv + (long)h * hd;
+  float* Ob = O + (long)b * sbo + (long)h * hd;
+
+  for (int e = tid; e < NKP * HDP; e += 256) {
+    const int key = e / HDP, d = e - key * HDP;
+    const bool ok = key < Nk && d < hd;
+    sK[key * LDR + d] = ok ? Kb[(long)key * ldk + d] : 0.f;
+    sV[key * LDR + d] = ok ? Vb[(long)key * ldv + d] : 0.f;
+  }
+  __syncthreads();
+
+  const int qbase = blockIdx.x * QB;
+  for (int qt = wave; qt < QB / 16; qt += 4) {
+    const int q0 = qbase + qt * 16;
+    if (q0 >= Nq) break;
+    float qf[QD];
+    {
+      const int qr = q0 + c;
+      const float* qp = Qb + (long)(qr < Nq ? qr : 0) * ldq;
+#pragma unroll
+      for (int ks = 0; ks < QD; ++ks) {
+        const int d = QD * g + ks;
+        qf[ks] = (qr < Nq && d < hd) ? qp[d] : 0.f;
+      }
+    }
+    f32x4 o[NDT];
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m_run = -INFINITY, l_run = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < NKC; ++ch) {
+      const int kc0 = ch * KC;
+      f32x4 s[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* kr = sK + (kc0 + 16 * t + c) * LDR + QD * g;
+#pragma unroll
+        for (int k4 = 0; k4 < QD / 4; ++k4) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(kr + 4 * k4);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], qf[4 * k4 + j], s[t], 0, 0, 0);
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = kc0 + 16 * t + 4 * g + r;
+          const float v = key < Nk ? s[t][r] * scale_log2 : -INFINITY;
+          s[t][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = exp2f(m_run - m_new);
+      float ps = 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[t][r] - m_new);
+          s[t][r] = p;
+          ps += p;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l_run = l_run * alpha + ps;
+      m_run = m_new;
+      if (ch > 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ar = __shfl(alpha, 4 * g + r, 64);
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) o[dt][r] *= ar;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float* vr = sV + (kc0 + 16 * t + 4 * g + r) * LDR + c;
+#pragma unroll
+          for (int dt = 0; dt < NDT; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(s[t][r], vr[16 * dt], o[dt], 0, 0, 0);
+        }
+    }
+    // lane holds O[query q0 + 4g + r][16 dt + c]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = q0 + 4 * g + r;
+      const float inv = 1.0f / __shfl(l_run, 4 * g + r, 64);
+      if (q < Nq) {
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const int d = 16 * dt + c;
+          if (d < hd) Ob[(long)q * ldo + d] = o[dt][r] * inv;
+        }
+      }
+    }
+  }
+}
+
 }  // namespace svk
 
 using namespace svk;
@@ -446,6 +578,35 @@ extern "C" int svk_attention(int dtype, const void* Q, long ldq, long sbq, const
                            sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
       return check_launch("attention_mfma_bf16");
     });
+  }
+  static const bool f32_scalar = getenv("SVK_ATTN_F32_SCALAR") != nullptr;   // the exact scalar kernel (A/B checks)
+  if (dtype == SVK_F32 && !f32_scalar) {
+    const int nkc = (Nk + 63) / 64;
+    dim3 rgrid((Nq + 255) / 256, heads, B);
+    auto go = [&](auto hdp_c, auto nkc_c) {
+      constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
+      constexpr int sm = 2 * NKC * 64 * (HDP + 4) * (int)sizeof(float);
+      static bool attr = false;
+      if (!attr && sm > 65536) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attention_mfma_f32<HDP, NKC>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, sm);
+        attr = true;
+      }
+      hipLaunchKernelGGL((attention_mfma_f32<HDP, NKC>), rgrid, block, sm, st, (const float*)Q, ldq, sbq,
+                         (const float*)K, ldk, sbk, (const float*)V, ldv, sbv, (float*)O, ldo, sbo, Nq, Nk, hd,
+                         scale * 1.4426950408889634f);
+    };
+    auto by_nkc = [&](auto hdp) {
+      switch (nkc) {
+        case 1: go(hdp, std::integral_constant<int, 1>{}); break;
+        case 2: go(hdp, std::integral_constant<int, 2>{}); break;
+        case 3: go(hdp, std::integral_constant<int, 3>{}); break;
+        default: go(hdp, std::integral_constant<int, 4>{}); break;
+      }
+    };
+    if (hd <= 32) by_nkc(std::integral_constant<int, 32>{});
+    else by_nkc(std::integral_constant<int, 64>{});
+    return check_launch("attention_mfma_f32");
   }
   SVK_DISPATCH_DTYPE(dtype, T, {
     const size_t sm = (size_t)2 * Nk * hd * sizeof(float);

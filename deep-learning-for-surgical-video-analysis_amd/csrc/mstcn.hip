@@ -37,16 +37,29 @@ struct Map {
   static constexpr int RP = NTH / FMAX, RT = TT / RP;
 };
 
+// Ragged multi-video batches (trans_SV_output.py:251-291 / tecno.py:80-91 walk the test videos one by
+// one): the videos' maps are concatenated time-major and one launch covers every video's tiles.  Tile
+// record {first row of the tile's video, that video's length, tile start inside the video, 0}; taps
+// never cross a video boundary (out-of-video rows read zero, exactly the per-video zero padding).
+// tiles == nullptr: one video of length T, tile = blockIdx.x.
 template <int FMAX, bool TRAIN>
 __global__ __launch_bounds__(NTH) void mstcn_layer_kernel(const float* __restrict__ X, const float* __restrict__ WdT,
                                                           const float* __restrict__ bd, const float* __restrict__ W1T,
                                                           const float* __restrict__ b1, float* __restrict__ Y, int T,
                                                           int F, int dil, int causal, const float* __restrict__ mask,
-                                                          float* __restrict__ Hout) {
-  constexpr int LD = FMAX + 1, RP = Map<FMAX>::RP, RT = Map<FMAX>::RT;
-  __shared__ float xs[3][TT][LD];
-  __shared__ float hs[TT][LD];
-  const int t0 = blockIdx.x * TT;
+                                                          float* __restrict__ Hout, const int4* __restrict__ tiles) {
+  // rows padded to a multiple of 4 floats + 4: 16-byte broadcast reads of 4 input channels
+  constexpr int LD = FMAX + 4, RP = Map<FMAX>::RP, RT = Map<FMAX>::RT;
+  __shared__ __attribute__((aligned(16))) float xs[3][TT][LD];
+  __shared__ __attribute__((aligned(16))) float hs[TT][LD];
+  int t0 = blockIdx.x * TT;
+  if (tiles) {
+    const int4 tl = tiles[blockIdx.x];
+    X += (long)tl.x * F;
+    Y += (long)tl.x * F;
+    T = tl.y;
+    t0 = tl.z;
+  }
   int off[3];
   tap_offsets(causal, dil, off);
   for (int e = threadIdx.x; e < 3 * TT * F; e += NTH) {
@@ -59,6 +72,7 @@ __global__ __launch_bounds__(NTH) void mstcn_layer_kernel(const float* __restric
   __syncthreads();
   const int fo = threadIdx.x % FMAX, rg = threadIdx.x / FMAX;
   const bool act = fo < F;
+  const int F4 = F & ~3;
   float acc[RT];
 #pragma unroll
   for (int k = 0; k < RT; ++k) acc[k] = act ? bd[fo] : 0.f;
@@ -66,7 +80,19 @@ __global__ __launch_bounds__(NTH) void mstcn_layer_kernel(const float* __restric
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const float* w = WdT + (long)j * F * F + fo;
-      for (int ci = 0; ci < F; ++ci) {
+      int ci = 0;
+      for (; ci < F4; ci += 4) {
+        const float w0 = w[(long)ci * F], w1 = w[(long)(ci + 1) * F], w2 = w[(long)(ci + 2) * F], w3 = w[(long)(ci + 3) * F];
+#pragma unroll
+        for (int k = 0; k < RT; ++k) {
+          const float4 xv = *reinterpret_cast<const float4*>(&xs[j][rg + k * RP][ci]);
+          acc[k] += w0 * xv.x;
+          acc[k] += w1 * xv.y;
+          acc[k] += w2 * xv.z;
+          acc[k] += w3 * xv.w;
+        }
+      }
+      for (; ci < F; ++ci) {
         const float wv = w[(long)ci * F];
 #pragma unroll
         for (int k = 0; k < RT; ++k) acc[k] += wv * xs[j][rg + k * RP][ci];
@@ -86,10 +112,25 @@ __global__ __launch_bounds__(NTH) void mstcn_layer_kernel(const float* __restric
   if (!act) return;
 #pragma unroll
   for (int k = 0; k < RT; ++k) acc[k] = b1[fo];
-  for (int ci = 0; ci < F; ++ci) {
-    const float wv = W1T[(long)ci * F + fo];
+  {
+    int ci = 0;
+    for (; ci < F4; ci += 4) {
+      const float w0 = W1T[(long)ci * F + fo], w1 = W1T[(long)(ci + 1) * F + fo], w2 = W1T[(long)(ci + 2) * F + fo],
+                  w3 = W1T[(long)(ci + 3) * F + fo];
 #pragma unroll
-    for (int k = 0; k < RT; ++k) acc[k] += wv * hs[rg + k * RP][ci];
+      for (int k = 0; k < RT; ++k) {
+        const float4 hv = *reinterpret_cast<const float4*>(&hs[rg + k * RP][ci]);
+        acc[k] += w0 * hv.x;
+        acc[k] += w1 * hv.y;
+        acc[k] += w2 * hv.z;
+        acc[k] += w3 * hv.w;
+      }
+    }
+    for (; ci < F; ++ci) {
+      const float wv = W1T[(long)ci * F + fo];
+#pragma unroll
+      for (int k = 0; k < RT; ++k) acc[k] += wv * hs[rg + k * RP][ci];
+    }
   }
 #pragma unroll
   for (int k = 0; k < RT; ++k) {
@@ -269,14 +310,15 @@ __global__ void softmax_rows_bwd_kernel(const float* __restrict__ P, long ldp, c
 
 template <bool TRAIN>
 static int launch_layer(const float* X, const float* WdT, const float* bd, const float* W1T, const float* b1,
-                        const float* mask, float* Y, float* H, int T, int F, int dil, int causal, hipStream_t st) {
-  dim3 grid((T + TT - 1) / TT);
+                        const float* mask, float* Y, float* H, int T, int F, int dil, int causal, hipStream_t st,
+                        const int4* tiles = nullptr, int ntiles = 0) {
+  dim3 grid(tiles ? ntiles : (T + TT - 1) / TT);
   if (F <= 32)
     hipLaunchKernelGGL((mstcn_layer_kernel<32, TRAIN>), grid, dim3(NTH), 0, st, X, WdT, bd, W1T, b1, Y, T, F, dil, causal,
-                       mask, H);
+                       mask, H, tiles);
   else
     hipLaunchKernelGGL((mstcn_layer_kernel<64, TRAIN>), grid, dim3(NTH), 0, st, X, WdT, bd, W1T, b1, Y, T, F, dil, causal,
-                       mask, H);
+                       mask, H, tiles);
   return check_launch(TRAIN ? "mstcn_layer_train" : "mstcn_layer");
 }
 
@@ -291,6 +333,21 @@ extern "C" int svk_mstcn_layer(const float* X, const float* WdT, const float* bd
   }
   if (T == 0) return SVK_OK;
   return launch_layer<false>(X, WdT, bd, W1T, b1, nullptr, Y, nullptr, T, F, dilation, causal, (hipStream_t)stream);
+}
+
+extern "C" int svk_mstcn_tile_size() { return TT; }
+
+extern "C" int svk_mstcn_layer_ragged(const float* X, const float* WdT, const float* bd, const float* W1T, const float* b1,
+                                      float* Y, const int* tiles, int ntiles, int F, int dilation, int causal,
+                                      void* stream) {
+  if (ntiles < 0 || F <= 0 || F > 64 || dilation <= 0 || !X || !WdT || !bd || !W1T || !b1 || !Y || X == Y ||
+      (ntiles > 0 && (!tiles || ((uintptr_t)tiles & 15)))) {
+    set_error("svk_mstcn_layer_ragged: bad args (F=%d must be <= 64, X != Y, 16-byte aligned tile table)", F);
+    return SVK_EINVAL;
+  }
+  if (ntiles == 0) return SVK_OK;
+  return launch_layer<false>(X, WdT, bd, W1T, b1, nullptr, Y, nullptr, 0, F, dilation, causal, (hipStream_t)stream,
+                             reinterpret_cast<const int4*>(tiles), ntiles);
 }
 
 extern "C" int svk_mstcn_layer_train(const float* X, const float* WdT, const float* bd, const float* W1T, const float* b1,

@@ -46,10 +46,10 @@ class DilatedResidualLayer(nn.Module):
         w1, b1 = _w1x1(self.conv_1x1)
         return dict(wdT=wdT, bd=self.conv_dilated.bias.detach().float().contiguous(), w1T=w1.t().contiguous(), b1=b1)
 
-    def forward_tm(self, x):
-        """x [T, F] time-major f32 -> [T, F]."""
+    def forward_tm(self, x, tiles=None):
+        """x [T, F] time-major f32 -> [T, F] (``tiles``: x is a ragged batch of videos, ops.mstcn_tiles)."""
         p = get_packed(self, torch.float32, self._pack)
-        return ops.mstcn_layer(x, p["wdT"], p["bd"], p["w1T"], p["b1"], self.dilation, self.causal_conv)
+        return ops.mstcn_layer(x, p["wdT"], p["bd"], p["w1T"], p["b1"], self.dilation, self.causal_conv, tiles=tiles)
 
     def forward(self, x):
         """Reference signature: x [B, F, T] -> [B, F, T]."""
@@ -75,12 +75,12 @@ class SingleStageModel(nn.Module):
         wo, bo = _w1x1(self.conv_out_classes)
         return dict(wi=wi, bi=bi, wo=wo, bo=bo)
 
-    def forward_tm(self, x, out=None):
+    def forward_tm(self, x, out=None, tiles=None):
         """x [T, dim] time-major f32 -> class logits [T, classes] (written into ``out`` if given)."""
         p = get_packed(self, torch.float32, self._pack)
         h = ops.gemm(x, p["wi"], p["bi"])
         for layer in self.layers:
-            h = layer.forward_tm(h)
+            h = layer.forward_tm(h, tiles)
         return ops.gemm(h, p["wo"], p["bo"], out=out)
 
     def forward(self, x):
@@ -109,15 +109,38 @@ class MultiStageModel_S(nn.Module):
                                      for s in range(self.num_stages - 1)])
         self.smoothing = False
 
-    def forward_tm(self, x):
+    def forward_tm(self, x, tiles=None):
         """x [T, f_dim] (f32, time-major) -> [stages, T, classes] time-major logits."""
         T = x.shape[0]
         out = torch.empty(self.num_stages, T, self.num_classes, device=x.device, dtype=torch.float32)
-        self.stage1_phase.forward_tm(x, out=out[0])
+        self.stage1_phase.forward_tm(x, out=out[0], tiles=tiles)
         for s, stage in enumerate(self.stages):
             prob = ops.softmax_rows(out[s])                       # softmax over classes (mstcn.py:126)
-            stage.forward_tm(prob, out=out[s + 1])
+            stage.forward_tm(prob, out=out[s + 1], tiles=tiles)
         return out
+
+    def forward_videos(self, feats, lengths):
+        """Eval forward of a ragged batch of videos in one pass (one launch per layer for all of them).
+
+        ``feats`` [sum(lengths), f_dim]: the videos' feature rows concatenated time-major in order —
+        the layout of the long-range feature bank the callers slice per video (trans_SV_output.py:251-291,
+        tecno.py:80-91).  Returns [stages, sum(lengths), classes] time-major logits; video v's rows
+        ``out[:, o_v:o_v + T_v]`` equal ``self(feats[o_v:o_v + T_v].t()[None])`` (as [S, 1, C, T_v]
+        after ``.permute(0, 2, 1)[:, None]``).  See ``split_videos``."""
+        check_inference(self, feats)
+        if feats.dim() != 2 or feats.shape[0] != sum(int(t) for t in lengths):
+            raise ValueError("forward_videos: feats must be [sum(lengths), f_dim]")
+        x = feats if (feats.dtype == torch.float32 and feats.is_contiguous()) else feats.float().contiguous()
+        return self.forward_tm(x, tiles=ops.mstcn_tiles(lengths, x.device))
+
+    @staticmethod
+    def split_videos(out_tm, lengths):
+        """forward_videos output -> per-video [stages, 1, classes, T_v] views (the reference's layout)."""
+        res, o = [], 0
+        for T in lengths:
+            res.append(out_tm[:, o:o + int(T)].permute(0, 2, 1).unsqueeze(1))
+            o += int(T)
+        return res
 
     def forward(self, x):
         """x [B, f_dim, T] -> [stages, B, classes, T] (mstcn.py:122-130).  Train mode (tecno.py:195):

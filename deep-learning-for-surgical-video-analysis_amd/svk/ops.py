@@ -410,16 +410,45 @@ def softmax_rows(x, out=None):
     return out
 
 
-def mstcn_layer(x, wdT, bd, w1T, b1, dilation, causal, out=None):
-    """x [T, F] f32 time-major; wdT [3, F_in, F_out]; w1T [F_in, F_out] (transposed packs)."""
+_TILE_CACHE = {}
+
+
+def mstcn_tiles(lengths, device):
+    """Device tile table of svk_mstcn_layer_ragged for videos of the given lengths, concatenated
+    time-major in that order: int32 [ntiles, 4] = {first row of the video, T_v, tile start, 0}."""
+    key = (tuple(int(t) for t in lengths), str(device))
+    tab = _TILE_CACHE.get(key)
+    if tab is None:
+        tt = _lib.load().svk_mstcn_tile_size()
+        rows, start = [], 0
+        for T in key[0]:
+            if T < 0:
+                raise _lib.SvkError("svk.mstcn_tiles: negative video length")
+            rows += [(start, T, t0, 0) for t0 in range(0, T, tt)]
+            start += T
+        tab = torch.tensor(rows, dtype=torch.int32).reshape(-1, 4).to(device)
+        _TILE_CACHE[key] = tab
+    return tab
+
+
+def mstcn_layer(x, wdT, bd, w1T, b1, dilation, causal, out=None, tiles=None):
+    """x [T, F] f32 time-major; wdT [3, F_in, F_out]; w1T [F_in, F_out] (transposed packs).
+    ``tiles`` (mstcn_tiles): x is a ragged batch of videos concatenated time-major, one launch for all."""
     for t, nm in ((x, "x"), (wdT, "wdT"), (bd, "bd"), (w1T, "w1T"), (b1, "b1")):
         _chk(t, nm, torch.float32)
     T, F = x.shape
     if out is None:
         out = torch.empty_like(x)
     t0 = _prof_begin()
-    _lib.call("svk_mstcn_layer", _p(x), _p(wdT), _p(bd), _p(w1T), _p(b1), _p(out), T, F, dilation,
-              1 if causal else 0, _stream())
+    if tiles is not None:
+        _chk(tiles, "tiles", torch.int32)
+        if tiles.dim() != 2 or tiles.shape[1] != 4 or not tiles.is_contiguous():
+            raise _lib.SvkError("svk.mstcn_layer: tiles must be a contiguous [ntiles, 4] int32 table")
+        _lib.call("svk_mstcn_layer_ragged", _p(x), _p(wdT), _p(bd), _p(w1T), _p(b1), _p(out), _p(tiles),
+                  tiles.shape[0], F, dilation, 1 if causal else 0, _stream())
+    else:
+        _lib.call("svk_mstcn_layer", _p(x), _p(wdT), _p(bd), _p(w1T), _p(b1), _p(out), T, F, dilation,
+                  1 if causal else 0, _stream())
     _prof_end(t0, "mstcn_layer_kernel", 8.0 * T * F * F, 8 * T * F, (T, F, "mstcn"))
     return out
 

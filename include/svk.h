@@ -146,6 +146,15 @@ int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C,
 int svk_mstcn_layer(const float* X, const float* WdT, const float* bd, const float* W1T,
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
+/* Ragged batch of videos in one launch (trans_SV_output.py:251-291 and tecno.py's test loop run the
+ * model video by video): X / Y hold the videos' [T_v, F] maps concatenated time-major; tiles is a
+ * device table of ntiles int4 records {first row of the video, T_v, tile start t0 inside the video, 0},
+ * one per svk_mstcn_tile_size() time steps of every video (16-byte aligned).  Per video the result
+ * equals svk_mstcn_layer on that video alone (taps never cross a video boundary). */
+int svk_mstcn_tile_size(void);
+int svk_mstcn_layer_ragged(const float* X, const float* WdT, const float* bd, const float* W1T, const float* b1,
+                           float* Y, const int* tiles, int ntiles, int F, int dilation, int causal, void* stream);
+
 /* Training (tecno.py:195-259 trains MultiStageModel_S with nn.Dropout(p = 0.5) active in every
  * DilatedResidualLayer): Y = X + mask * (W1 relu(dilated conv) + b1) with mask values 0 or 1/keep;
  * H [T, F] receives relu(pre) for the backward. */

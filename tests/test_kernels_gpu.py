@@ -376,6 +376,27 @@ def test_mstcn_layer(cuda, F_, T, d, causal):
     torch.testing.assert_close(got.cpu().double(), ref[0].t(), rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("F_,d,causal", [(64, 8, True), (64, 512, True), (32, 4, False), (20, 2, True)])
+def test_mstcn_layer_ragged_equals_per_video(cuda, F_, d, causal):
+    """One launch over a ragged batch (incl. empty and 1-frame videos, lengths not multiples of the tile)
+    == the single-video kernel on each video, bit for bit (taps never cross a video boundary)."""
+    from svk import ops
+    lens = [1, 0, 17, 300, 16, 2457, 33]
+    x = _rand(sum(lens), F_, dt=torch.float32, dev=cuda, seed=27)
+    wd = _rand(F_, F_, 3, dt=torch.float32, dev="cpu", scale=F_ ** -0.5, seed=23).permute(2, 1, 0).contiguous().to(cuda)
+    bd = _rand(F_, dt=torch.float32, dev=cuda, seed=24)
+    w1 = _rand(F_, F_, dt=torch.float32, dev=cuda, scale=F_ ** -0.5, seed=25).t().contiguous()
+    b1 = _rand(F_, dt=torch.float32, dev=cuda, seed=26)
+    got = ops.mstcn_layer(x, wd, bd, w1, b1, d, causal, tiles=ops.mstcn_tiles(lens, cuda))
+    o = 0
+    for T in lens:
+        if T:
+            one = ops.mstcn_layer(x[o:o + T].contiguous(), wd, bd, w1, b1, d, causal)
+            assert torch.equal(got[o:o + T], one), f"video of length {T} differs"
+        o += T
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("F_,T,d,causal", [(64, 1000, 8, True), (32, 77, 128, False), (20, 50, 2, True),
                                            (64, 6001, 512, True)])
 def test_mstcn_layer_train_bwd(cuda, F_, T, d, causal):

@@ -125,6 +125,30 @@ def test_mstcn_full_length_video_vs_oracle(cuda):
     np.testing.assert_allclose(out.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=2e-4)
 
 
+@pytest.mark.parametrize("causal", [True, False])
+def test_mstcn_ragged_videos_vs_per_video_and_oracle(cuda, causal):
+    """forward_videos (one launch per layer for a ragged batch of videos) == the caller's per-video
+    forward bit for bit, and == the oracle per video."""
+    from models import mstcn
+    m = mstcn.MultiStageModel_S(4, 10, 64, 256, 14, causal)
+    sd = P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 5)
+    m.load_state_dict(sd)
+    m = m.to(cuda).eval()
+    lens = [1000, 1, 37, 2048, 613]
+    feats = torch.cat([I.lfb(T, 256, 20 + i)[0] for i, T in enumerate(lens)], 0)
+    with torch.no_grad():
+        out = m.forward_videos(feats.to(cuda), lens)
+        per = [m(f[None].to(cuda).transpose(2, 1)) for f in torch.split(feats, lens)]
+    torch.cuda.synchronize()
+    assert out.shape == (4, sum(lens), 14)
+    for T, got, one, f in zip(lens, m.split_videos(out, lens), per, torch.split(feats, lens)):
+        assert got.shape == (4, 1, 14, T)
+        torch.testing.assert_close(got, one, rtol=1e-6, atol=1e-6)
+        if T <= 1000:
+            ref = MS.multi_stage_s(f[None].transpose(2, 1), sd, 4, 10, causal)
+            np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=1e-5, atol=2e-4)
+
+
 @pytest.mark.parametrize("T", [1, 29, 30, 75, 1000])
 def test_transformer_original_forward_vs_oracle(cuda, golden, T):
     from models import adapter_transformer

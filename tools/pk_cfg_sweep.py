@@ -56,6 +56,8 @@ def main():
             ms = timeit(lambda: ops.gemm(a, w, b, residual=r, out=out), args.reps)
             row.append(f"{name} {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF d={err:.1e}")
         lib.svk_tune(b"pk_cfg", -1)
+        ms = timeit(lambda: torch.matmul(a, w.t(), out=out), args.reps)   # hipBLASLt, no epilogue (yardstick)
+        row.append(f"torch {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF")
         print(f"{what:10s} ({M},{N},{K}) " + " | ".join(row), flush=True)
 
 
