@@ -241,19 +241,33 @@ def workload_mamba(args, dev, rank, dtype):
     torch.manual_seed(0)
     model = mstcn.CausalMambaModel(4, 10, 64, 256, 14, True).to(dev).eval()     # tecno.py:153
     lens = video_lengths(40, seed=rank)
-    feats = [torch.randn(1, T, 256, device=dev) for T in lens]
+    bank = torch.randn(sum(lens), 256, device=dev)      # the videos' LFB rows, concatenated time-major
+    feats = [f[None] for f in torch.split(bank, lens)]
 
-    def step():
+    def step():           # all 40 videos in one ragged pass (CausalMambaModel.forward_videos)
+        return model.forward_videos(bank, lens)
+
+    def per_video():      # the callers' loop: one forward per video
         out = None
         for f in feats:
             out = model(f.transpose(2, 1))
         return out
 
     def check(out):
-        assert out.shape == (1, 1, 14, lens[-1]) and torch.isfinite(out).all()
+        assert out.shape == (sum(lens), 14) and torch.isfinite(out).all()
+        last = per_video()
+        torch.testing.assert_close(model.split_videos(out, lens)[-1], last, rtol=1e-4, atol=1e-4)
+        with torch.no_grad():
+            per_video()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            per_video()
+            torch.cuda.synchronize()
+        config["per_video_loop_frames_s"] = round(sum(lens) / (time.perf_counter() - t0), 1)
 
     config = {"workload": "tecno.py CausalMambaModel(f_maps 64, f_dim 256, 10 Mamba blocks: d_state 64, d_conv 4, "
-                          "expand 2) over 40 full-length videos (T ~ U[1000, 6000]) per step",
+                          "expand 2) over 40 full-length videos (T ~ U[1000, 6000]) per step, one ragged pass "
+                          "(forward_videos: one launch per kernel for all videos)",
               "model": "CausalMambaModel(4,10,64,256,14,True)", "videos_per_step": 40}
     return step, sum(lens), config, check, (lambda: cpu_baseline_mamba(args.cpu_baseline_seconds))
 

@@ -33,7 +33,7 @@
 
 namespace svk {
 
-__device__ __attribute__((aligned(16))) uint4 g_pk_zero[4];   // 64 zero bytes: the K-tail source
+static __device__ __attribute__((aligned(16))) uint4 g_pk_zero[4];   // 64 zero bytes: the K-tail source
 
 typedef __attribute__((address_space(1))) void* gas_ptr;
 typedef __attribute__((address_space(3))) void* las_ptr;
@@ -517,9 +517,9 @@ int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st) {
   return launch_pk<T, PkCfg<128, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
 }
 
-template int gemm_pk_try<bf16>(const GemmArgs&, hipStream_t, int);
-template int gemm_pk_try<f16>(const GemmArgs&, hipStream_t, int);
-template int gemm_pk_conv_splitk<bf16>(const GemmArgs&, hipStream_t);
-template int gemm_pk_conv_splitk<f16>(const GemmArgs&, hipStream_t);
+// one element type per translation unit (gemm_pk_bf16.hip / gemm_pk_f16.hip define SVK_PK_T): the two
+// halves of the instantiation set compile in parallel
+template int gemm_pk_try<SVK_PK_T>(const GemmArgs&, hipStream_t, int);
+template int gemm_pk_conv_splitk<SVK_PK_T>(const GemmArgs&, hipStream_t);
 
 }  // namespace svk

@@ -1,0 +1,3 @@
+// bf16 instantiations of the persistent GEMM (gemm_pk.hip)
+#define SVK_PK_T bf16
+#include "gemm_pk.hip"

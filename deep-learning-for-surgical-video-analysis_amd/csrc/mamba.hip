@@ -31,12 +31,12 @@ __global__ __launch_bounds__(256) void mamba_conv_silu_kernel(const float* __res
                                                               const float* __restrict__ W,
                                                               const float* __restrict__ bias,
                                                               float* __restrict__ Y, int T, long total, int Di,
-                                                              int K) {
+                                                              int K, const int* __restrict__ tpos) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
   const int d = (int)(i % Di);
   const long r = i / Di;                 // global row b*T + t
-  const int t = (int)(r % T);
+  const int t = tpos ? tpos[r] : (int)(r % T);   // ragged batch: the row's time index inside its video
   float acc = bias ? bias[d] : 0.f;
   for (int k = 0; k < K; ++k) {
     const int dt = K - 1 - k;            // tap k reads x[t - (K-1) + k] (pad K-1, keep first T)
@@ -52,6 +52,9 @@ __device__ __forceinline__ float softplus20(float s) { return s <= 20.f ? log1pf
 // delta sum DS[b, z, d] (its decay is exp(A * sum delta)).  OUT = true (pass 2): fold the earlier
 // segments' (decay, end state) pairs into the initial state, rerun the segment and write y.  With one
 // segment pass 2 alone is the plain sequential scan.
+// Ragged batches (segs != nullptr, gridDim.z == 1): blockIdx.y indexes a table of (video, segment)
+// records {first row of the video, its length T_v, segment index z, index of the video's first record};
+// a video's records are consecutive, so its segment states HS / DS sit at records sbase .. sbase + S_v - 1.
 template <int NS, bool OUT>
 __global__ __launch_bounds__(256) void mamba_scan_kernel(const float* __restrict__ U, const float* __restrict__ XD,
                                                          long ldxd, const float* __restrict__ Z, long ldz,
@@ -59,7 +62,7 @@ __global__ __launch_bounds__(256) void mamba_scan_kernel(const float* __restrict
                                                          const float* __restrict__ A, const float* __restrict__ Dp,
                                                          float* __restrict__ Y, float* __restrict__ HS,
                                                          float* __restrict__ DS, int T, int Di, int R, int seg,
-                                                         float* __restrict__ Yss) {
+                                                         float* __restrict__ Yss, const int4* __restrict__ segs) {
   constexpr int CPW = 64 / NS;           // channels per wave
   constexpr int CPB = 4 * CPW;           // channels per workgroup
   constexpr int XW = MB_RMAX + 2 * NS + 1;
@@ -73,15 +76,26 @@ __global__ __launch_bounds__(256) void mamba_scan_kernel(const float* __restrict
   const int cw = wave * CPW + cl;        // channel slot within the workgroup
   const int c0 = blockIdx.x * CPB;
   const int d = c0 + cw;
-  const int b = blockIdx.y, z = blockIdx.z, S = gridDim.z;
-  const long row0 = (long)b * T;
+  long row0;
+  int z, sbase;
+  if (segs) {
+    const int4 e = segs[blockIdx.y];
+    row0 = e.x;
+    T = e.y;
+    z = e.z;
+    sbase = e.w;
+  } else {
+    z = blockIdx.z;
+    row0 = (long)blockIdx.y * T;
+    sbase = blockIdx.y * gridDim.z;
+  }
   const float a = d < Di ? A[(long)d * NS + n] : 0.f;
   const int W = R + 2 * NS;
   const int tbeg = z * seg, tend = min(T, tbeg + seg);
   float h = 0.f, dsum = 0.f;
   if (OUT && d < Di) {
     for (int zz = 0; zz < z; ++zz) {
-      const long sidx = ((long)b * S + zz) * Di + d;
+      const long sidx = ((long)sbase + zz) * Di + d;
       h = __expf(a * DS[sidx]) * h + HS[sidx * NS + n];
     }
   }
@@ -172,7 +186,7 @@ __global__ __launch_bounds__(256) void mamba_scan_kernel(const float* __restrict
     }
   }
   if (!OUT && d < Di) {
-    const long sidx = ((long)b * S + z) * Di + d;
+    const long sidx = ((long)sbase + z) * Di + d;
     HS[sidx * NS + n] = h;
     if (n == 0) DS[sidx] = dsum;
   }
@@ -191,8 +205,21 @@ extern "C" int svk_mamba_conv_silu(const float* X, long ldx, const float* W, con
   const long total = (long)B * T * Di;
   if (total == 0) return SVK_OK;
   hipLaunchKernelGGL(mamba_conv_silu_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                     (hipStream_t)stream, X, ldx, W, bias, Y, T, total, Di, K);
+                     (hipStream_t)stream, X, ldx, W, bias, Y, T, total, Di, K, nullptr);
   return check_launch("mamba_conv_silu");
+}
+
+extern "C" int svk_mamba_conv_silu_ragged(const float* X, long ldx, const float* W, const float* bias, float* Y,
+                                          const int* tpos, long rows, int Di, int K, void* stream) {
+  if (rows < 0 || Di <= 0 || K <= 0 || K > 8 || ldx < Di || !X || !W || !Y || (rows > 0 && !tpos)) {
+    set_error("svk_mamba_conv_silu_ragged: bad args (rows=%ld Di=%d K=%d ldx=%ld)", rows, Di, K, ldx);
+    return SVK_EINVAL;
+  }
+  const long total = rows * Di;
+  if (total == 0) return SVK_OK;
+  hipLaunchKernelGGL(mamba_conv_silu_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, X, ldx, W, bias, Y, 1, total, Di, K, tpos);
+  return check_launch("mamba_conv_silu_ragged");
 }
 
 static int mamba_scan_launch(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
@@ -217,9 +244,9 @@ static int mamba_scan_launch(const float* U, const float* XD, long ldxd, const f
   do {                                                                                                          \
     if (S > 1)                                                                                                  \
       hipLaunchKernelGGL((mamba_scan_kernel<NS, false>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt,  \
-                         A, Dp, Y, HS, DS, T, Di, R, seg, nullptr);                                             \
+                         A, Dp, Y, HS, DS, T, Di, R, seg, nullptr, nullptr);                                    \
     hipLaunchKernelGGL((mamba_scan_kernel<NS, true>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A, \
-                       Dp, Y, HS, DS, T, Di, R, seg, Yss);                                                      \
+                       Dp, Y, HS, DS, T, Di, R, seg, Yss, nullptr);                                             \
   } while (0)
   if (N == 64) SVK_MAMBA_LAUNCH(64);
   else if (N == 32) SVK_MAMBA_LAUNCH(32);
@@ -240,6 +267,43 @@ extern "C" int svk_mamba_scan_train(const float* U, const float* XD, long ldxd, 
                                     void* stream) {
   if (!Yss) { set_error("svk_mamba_scan_train: Yss is required"); return SVK_EINVAL; }
   return mamba_scan_launch(U, XD, ldxd, Z, ldz, Wdt, bdt, A, Dp, Y, B, T, Di, N, R, seg_len, ws, Yss, stream);
+}
+
+extern "C" int svk_mamba_scan_ragged(const float* U, const float* XD, long ldxd, const float* Z, long ldz,
+                                     const float* Wdt, const float* bdt, const float* A, const float* Dp, float* Y,
+                                     const int* segs, int nseg, int Di, int N, int R, int seg_len, float* ws,
+                                     void* stream) {
+  if (nseg < 0 || Di <= 0 || R <= 0 || R > MB_RMAX || (N != 16 && N != 32 && N != 64) || ldxd < R + 2 * N ||
+      ldz < Di || !U || !XD || !Z || !Wdt || !bdt || !A || !Dp || !Y || seg_len <= 0 || seg_len % MB_TC != 0 ||
+      (nseg > 0 && (!segs || !ws || ((uintptr_t)segs & 15)))) {
+    set_error("svk_mamba_scan_ragged: bad args (Di=%d N=%d R=%d ldxd=%ld seg_len=%d must be a multiple of %d; "
+              "segs 16-byte aligned, workspace required)", Di, N, R, ldxd, seg_len, MB_TC);
+    return SVK_EINVAL;
+  }
+  if (nseg == 0) return SVK_OK;
+  const int cpb = 4 * (64 / N);
+  dim3 grid((Di + cpb - 1) / cpb, nseg, 1);
+  hipStream_t s = (hipStream_t)stream;
+  float* HS = ws;
+  float* DS = ws + (long)nseg * Di * N;
+  const int4* sg = reinterpret_cast<const int4*>(segs);
+#define SVK_MAMBA_RLAUNCH(NS)                                                                                  \
+  do {                                                                                                          \
+    hipLaunchKernelGGL((mamba_scan_kernel<NS, false>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A, \
+                       Dp, Y, HS, DS, 0, Di, R, seg_len, nullptr, sg);                                          \
+    hipLaunchKernelGGL((mamba_scan_kernel<NS, true>), grid, dim3(256), 0, s, U, XD, ldxd, Z, ldz, Wdt, bdt, A,  \
+                       Dp, Y, HS, DS, 0, Di, R, seg_len, nullptr, sg);                                          \
+  } while (0)
+  if (N == 64) SVK_MAMBA_RLAUNCH(64);
+  else if (N == 32) SVK_MAMBA_RLAUNCH(32);
+  else SVK_MAMBA_RLAUNCH(16);
+#undef SVK_MAMBA_RLAUNCH
+  return check_launch("mamba_scan_ragged");
+}
+
+extern "C" long svk_mamba_scan_ragged_workspace(int nseg, int Di, int N) {
+  if (nseg <= 0 || Di <= 0 || N <= 0) return 0;
+  return (long)nseg * Di * (N + 1) * (long)sizeof(float);
 }
 
 extern "C" long svk_mamba_scan_workspace(int B, int T, int Di, int N, int seg_len) {

@@ -216,14 +216,15 @@ class Mamba(nn.Module):
                     w_out=f(self.out_proj.weight),
                     b_out=None if self.out_proj.bias is None else f(self.out_proj.bias))
 
-    def forward_tm(self, x, B, T, residual=None):
-        """x [B*T, d_model] f32 time-major -> out_proj(y) (+ residual) [B*T, d_model]."""
+    def forward_tm(self, x, B, T, residual=None, ragged=None):
+        """x [B*T, d_model] f32 time-major -> out_proj(y) (+ residual) [B*T, d_model].  ``ragged``
+        (ops.mamba_ragged): x is a ragged batch of videos concatenated time-major (B, T unused)."""
         p = get_packed(self, torch.float32, self._pack)
         di = self.d_inner
         xz = ops.gemm(x, p["w_in"], p["b_in"])                           # [BT, 2 Di]
-        xc = ops.mamba_conv_silu(xz[:, :di], p["conv_w"], p["conv_b"], B, T)
+        xc = ops.mamba_conv_silu(xz[:, :di], p["conv_w"], p["conv_b"], B, T, ragged=ragged)
         xdbl = ops.gemm(xc, p["w_x"])                                     # [BT, R + 2N]
-        y = ops.mamba_scan(xc, xdbl, xz[:, di:], p["w_dt"], p["b_dt"], p["a_neg"], p["d_skip"], B, T)
+        y = ops.mamba_scan(xc, xdbl, xz[:, di:], p["w_dt"], p["b_dt"], p["a_neg"], p["d_skip"], B, T, ragged=ragged)
         return ops.gemm(y, p["w_out"], p["b_out"], residual=residual)
 
     def forward(self, hidden_states):
@@ -287,3 +288,31 @@ class CausalMambaModel(nn.Module):
         h = ops.layernorm(h, p["g"], p["b"], self.norm.eps)
         logits = ops.gemm(h, p["w_h"], p["b_h"])                          # [B*T, classes]
         return logits.view(B, T, self.num_classes).permute(0, 2, 1).unsqueeze(0)
+
+    def forward_videos(self, feats, lengths):
+        """Eval forward of a ragged batch of videos in one pass (one launch per kernel for all of them).
+
+        ``feats`` [sum(lengths), f_dim]: the videos' feature rows concatenated time-major (the feature
+        bank layout the callers slice per video, tecno.py:80-91).  Returns [sum(lengths), classes]
+        time-major logits; video v's rows equal ``self(feats[o_v:o_v + T_v].t()[None])`` (see
+        ``split_videos``): the causal conv and the scan restart at every video's first frame."""
+        check_inference(self, feats)
+        if feats.dim() != 2 or feats.shape[0] != sum(int(t) for t in lengths):
+            raise ValueError("forward_videos: feats must be [sum(lengths), f_dim]")
+        x = feats if (feats.dtype == torch.float32 and feats.is_contiguous()) else feats.float().contiguous()
+        p = get_packed(self, torch.float32, self._pack)
+        rg = ops.mamba_ragged(lengths, x.device)
+        h = ops.gemm(x, p["w_in"], p["b_in"])
+        for blk in self.blocks:
+            h = blk.forward_tm(h, 1, x.shape[0], residual=h, ragged=rg)
+        h = ops.layernorm(h, p["g"], p["b"], self.norm.eps)
+        return ops.gemm(h, p["w_h"], p["b_h"])
+
+    @staticmethod
+    def split_videos(out_tm, lengths):
+        """forward_videos output -> per-video [1, 1, classes, T_v] views (the reference's layout)."""
+        res, o = [], 0
+        for T in lengths:
+            res.append(out_tm[o:o + int(T)].t().unsqueeze(0).unsqueeze(0))
+            o += int(T)
+        return res

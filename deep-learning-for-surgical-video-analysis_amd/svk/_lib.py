@@ -34,6 +34,8 @@ SIGNATURES = {
     "svk_mstcn_layer": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_mstcn_layer_ragged": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],
     "svk_mamba_conv_silu": [P, c_long, P, P, P, c_int, c_int, c_int, c_int, P],
+    "svk_mamba_conv_silu_ragged": [P, c_long, P, P, P, P, c_long, c_int, c_int, P],
+    "svk_mamba_scan_ragged": [P, P, c_long, P, c_long, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P, P],
     "svk_mamba_scan": [P, P, c_long, P, c_long, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P],
     "svk_mamba_scan_train": [P, P, c_long, P, c_long, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P,
                              P],
@@ -92,6 +94,7 @@ LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int,
               "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int],
+              "svk_mamba_scan_ragged_workspace": [c_int, c_int, c_int],
               "svk_mstcn_bwd_workspace": [c_int, c_int]}
 INT_QUERIES = {"svk_mixffn_supported": [c_int, c_int], "svk_mstcn_tile_size": []}
 

@@ -453,11 +453,45 @@ def mstcn_layer(x, wdT, bd, w1T, b1, dilation, causal, out=None, tiles=None):
     return out
 
 
-def mamba_conv_silu(x, w, bias, B, T):
+_MAMBA_RAGGED = {}
+MAMBA_RAGGED_SEG = int(os.environ.get("SVK_MAMBA_RAGGED_SEG", "256"))
+
+
+def mamba_ragged(lengths, device, seg_len=None):
+    """Tables of the ragged Mamba kernels for videos of the given lengths, concatenated time-major:
+    (tpos int32 [sum T] = time index inside the video, segs int32 [nseg, 4] = {first row, T_v, segment z,
+    the video's first record}, seg_len)."""
+    seg = MAMBA_RAGGED_SEG if seg_len is None else int(seg_len)
+    key = (tuple(int(t) for t in lengths), str(device), seg)
+    hit = _MAMBA_RAGGED.get(key)
+    if hit is None:
+        tpos, segs, start = [], [], 0
+        for T in key[0]:
+            if T < 0:
+                raise _lib.SvkError("svk.mamba_ragged: negative video length")
+            base = len(segs)
+            segs += [(start, T, z, base) for z in range(-(-T // seg))]
+            tpos.append(torch.arange(T, dtype=torch.int32))
+            start += T
+        tp = (torch.cat(tpos) if tpos else torch.zeros(0, dtype=torch.int32)).to(device)
+        hit = (tp, torch.tensor(segs, dtype=torch.int32).reshape(-1, 4).to(device), seg)
+        _MAMBA_RAGGED[key] = hit
+    return hit
+
+
+def mamba_conv_silu(x, w, bias, B, T, ragged=None):
     """x [B*T, Di] f32 (row stride may exceed Di: the x-half of in_proj's xz) -> silu(causal depthwise
     conv) [B*T, Di]; w [Di, K]."""
     _chk(x, "x", torch.float32); _chk(w, "w", torch.float32); _chk(bias, "bias", torch.float32)
     M, Di, ldx = _rows(x, "x")
+    if ragged is not None:      # (tpos, segs, seg_len) of mamba_ragged: B, T unused
+        tpos = ragged[0]
+        if tpos.numel() != M or w.shape[0] != Di or not w.is_contiguous():
+            raise _lib.SvkError("svk.mamba_conv_silu: ragged table does not match x")
+        out = torch.empty(M, Di, device=x.device, dtype=torch.float32)
+        _lib.call("svk_mamba_conv_silu_ragged", _p(x), ldx, _p(w), _p(bias), _p(out), _p(tpos), M, Di, w.shape[1],
+                  _stream())
+        return out
     if M != B * T or w.shape[0] != Di or not w.is_contiguous():
         raise _lib.SvkError(f"svk.mamba_conv_silu: x {tuple(x.shape)} / w {tuple(w.shape)} vs B={B} T={T}")
     out = torch.empty(M, Di, device=x.device, dtype=torch.float32)
@@ -479,7 +513,7 @@ def mamba_seg_len(B, T, Di, N, target_groups=None):
     return -(-(-(-T // S)) // 32) * 32
 
 
-def mamba_scan(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
+def mamba_scan(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None, ragged=None):
     """Selective scan with the dt projection, softplus, D skip and silu(z) gate fused:
     u [B*T, Di], xdbl [B*T, R+2N] (dt_low | B | C), z [B*T, Di] (may be strided), w_dt [Di, R],
     a_neg = -exp(A_log) [Di, N] -> y [B*T, Di] (f32)."""
@@ -491,10 +525,22 @@ def mamba_scan(u, xdbl, z, w_dt, b_dt, a_neg, d_skip, B, T, seg_len=None):
     Mz, Dz, ldz = _rows(z, "z")
     Dn, N = a_neg.shape
     R = w_dt.shape[1]
+    if ragged is not None:
+        B, T = 1, M               # the tables carry the video boundaries
     if (M != B * T or Mx != M or Mz != M or Dz != Di or ldu != Di or Dn != Di or W != R + 2 * N
             or not (w_dt.is_contiguous() and a_neg.is_contiguous())):
         raise _lib.SvkError("svk.mamba_scan: shape mismatch")
     out = torch.empty(M, Di, device=u.device, dtype=torch.float32)
+    if ragged is not None:
+        tpos, segs, seg = ragged
+        nseg = segs.shape[0]
+        ws = torch.empty(max(1, _lib.load().svk_mamba_scan_ragged_workspace(nseg, Di, N) // 4), device=u.device,
+                         dtype=torch.float32)
+        t0 = _prof_begin()
+        _lib.call("svk_mamba_scan_ragged", _p(u), _p(xdbl), ldxd, _p(z), ldz, _p(w_dt), _p(b_dt), _p(a_neg),
+                  _p(d_skip), _p(out), _p(segs), nseg, Di, N, R, seg, _p(ws), _stream())
+        _prof_end(t0, f"mamba_scan_kernel<{N}>", M * Di * (2 * R + 6 + 6 * N), 4 * M * (3 * Di + W), (M, Di, N))
+        return out
     seg = mamba_seg_len(B, T, Di, N) if seg_len is None else int(seg_len)
     nws = _lib.load().svk_mamba_scan_workspace(B, T, Di, N, seg)
     ws = torch.empty(nws // 4, device=u.device, dtype=torch.float32) if nws > 0 else None

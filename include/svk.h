@@ -193,6 +193,19 @@ int svk_mamba_scan(const float* U, const float* XD, long ldxd, const float* Z, l
  * segments (seg_len a multiple of 32) scanned concurrently in two passes; ws (caller-owned) holds
  * svk_mamba_scan_workspace(B, T, Di, N, seg_len) bytes of per-segment end states and delta sums. */
 long svk_mamba_scan_workspace(int B, int T, int Di, int N, int seg_len);
+
+/* Ragged batches of videos (tecno.py / trans_SV_output.py walk the test videos one by one): the videos'
+ * rows are concatenated time-major.  conv: tpos[r] = time index of row r inside its video (the causal
+ * taps stop at the video's first row).  scan: segs = nseg int4 records {first row of the video, T_v,
+ * segment index z, index of the video's first record} (a video's records consecutive, 16-byte aligned),
+ * segments of seg_len steps (a multiple of 32) scanned in two passes; ws = svk_mamba_scan_ragged_workspace
+ * bytes.  Per video the result equals svk_mamba_conv_silu / svk_mamba_scan on that video alone. */
+int svk_mamba_conv_silu_ragged(const float* X, long ldx, const float* W, const float* bias, float* Y,
+                               const int* tpos, long rows, int Di, int K, void* stream);
+int svk_mamba_scan_ragged(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
+                          const float* bdt, const float* A, const float* Dp, float* Y, const int* segs, int nseg,
+                          int Di, int N, int R, int seg_len, float* ws, void* stream);
+long svk_mamba_scan_ragged_workspace(int nseg, int Di, int N);
 /* svk_mamba_scan that also stores the pre-gate output Yss = sum_n C h + D u [B*T, Di] (training). */
 int svk_mamba_scan_train(const float* U, const float* XD, long ldxd, const float* Z, long ldz, const float* Wdt,
                          const float* bdt, const float* A, const float* Dp, float* Y, float* Yss, int B, int T,

@@ -104,3 +104,58 @@ def test_causal_mamba_prefix_property_full_length(cuda):
     torch.cuda.synchronize()
     assert torch.isfinite(full).all()
     np.testing.assert_allclose(full[..., :2500].cpu().numpy(), pre.cpu().numpy(), rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("seg", [32, 96, 256])
+@pytest.mark.parametrize("N", [16, 64])
+def test_ragged_scan_and_conv_vs_oracle(cuda, N, seg):
+    """Ragged batch (incl. a 1-frame and an empty video, lengths not multiples of the segment): one launch
+    per kernel, each video equal to the oracle on that video alone (state and conv taps restart)."""
+    from svk import ops
+    g = torch.Generator().manual_seed(N + seg)
+    lens = [1, 0, 95, 300, 33]
+    M, Di, R, K = sum(lens), 48, 4, 4
+    xz = _rand(g, M, 2 * Di)
+    w = _rand(g, Di, K, scale=0.5)
+    b = _rand(g, Di, scale=0.1)
+    xdbl = _rand(g, M, R + 2 * N, scale=0.5)
+    z = _rand(g, M, Di)
+    w_dt = _rand(g, Di, R, scale=0.5)
+    b_dt = _rand(g, Di, scale=0.5) - 2.0
+    a_neg = -torch.exp(_rand(g, Di, N, scale=0.5))
+    d_skip = _rand(g, Di)
+    c = lambda t: t.float().contiguous().to(cuda)
+    rg = ops.mamba_ragged(lens, cuda, seg_len=seg)
+    xzd = xz.float().to(cuda)
+    u = ops.mamba_conv_silu(xzd[:, :Di], c(w), c(b), 1, M, ragged=rg)
+    y = ops.mamba_scan(u, c(xdbl), c(z), c(w_dt), c(b_dt), c(a_neg), c(d_skip), 1, M, ragged=rg)
+    torch.cuda.synchronize()
+    o = 0
+    for T in lens:
+        if T:
+            xi = xz[o:o + T, :Di].t()[None]
+            uref = F.silu(F.conv1d(xi, w[:, None, :], b, padding=K - 1, groups=Di)[..., :T]).transpose(1, 2)
+            np.testing.assert_allclose(u[o:o + T].cpu().double().numpy(), uref[0].numpy(), rtol=1e-5, atol=1e-5)
+            uu = u[o:o + T].cpu().double()[None]
+            xd = xdbl[o:o + T][None]
+            delta = F.softplus(xd[..., :R] @ w_dt.t() + b_dt)
+            ref = OM.selective_scan(uu, delta, a_neg, xd[..., R:R + N], xd[..., R + N:], d_skip, z[o:o + T][None])
+            np.testing.assert_allclose(y[o:o + T].cpu().double().numpy(), ref[0].numpy(), rtol=1e-4, atol=1e-4)
+        o += T
+
+
+def test_causal_mamba_ragged_videos(cuda):
+    """forward_videos over a ragged batch == the caller's per-video forward, and == the oracle."""
+    m, sd = _model(cuda, 4, 10, 64, 256, 64, 7)
+    lens = [700, 1, 65, 1500]
+    feats = torch.cat([I.lfb(T, 256, 30 + i)[0] for i, T in enumerate(lens)], 0)
+    with torch.no_grad():
+        out = m.forward_videos(feats.to(cuda), lens)
+        per = [m(f[None].to(cuda).transpose(2, 1)) for f in torch.split(feats, lens)]
+    torch.cuda.synchronize()
+    assert out.shape == (sum(lens), 14)
+    for T, got, one, f in zip(lens, m.split_videos(out, lens), per, torch.split(feats, lens)):
+        assert got.shape == (1, 1, 14, T)
+        np.testing.assert_allclose(got.cpu().numpy(), one.cpu().numpy(), rtol=0, atol=2e-5)
+        if T <= 700:
+            _check_logits(got, OM.causal_mamba(f[None].transpose(2, 1), sd, 10))

@@ -14,7 +14,8 @@ SHAPES = [  # (M, N, K, residual, what)
     (50176, 320, 1280, True, "s3 fc2"), (50176, 1280, 320, False, "s3 fc1"), (50176, 320, 320, True, "s3 q/proj"),
     (12544, 640, 320, False, "s3 kv"), (12544, 2048, 512, False, "s4 fc1"), (12544, 512, 2048, True, "s4 fc2"),
     (12544, 512, 512, True, "s4 q/proj"), (12544, 1024, 512, False, "s4 kv"), (12544, 2048, 1024, False, "head"),
-    (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"),
+    (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"), (200704, 128, 128, True, "s2 q/proj"),
+    (802816, 64, 64, True, "s1 q/proj"),
 ]
 CFGS = [(-1, "auto"), (0, "128x128"), (10, "128x64"), (40, "128x160"), (50, "256x128")]
 
