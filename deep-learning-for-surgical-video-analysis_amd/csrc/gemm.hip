@@ -811,6 +811,11 @@ int svk::wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i
   a.dY = dY; a.ldy = ldy; a.X = X; a.ldx = ldx; a.dW = dW; a.lddw = lddw; a.M = M; a.N = N; a.K = K;
   a.nzi = nzi; a.sa_o = sa_o; a.sa_i = sa_i; a.sx_o = sx_o; a.sx_i = sx_i; a.sw_o = sw_o; a.sw_i = sw_i;
   SVK_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) {
+      if (wgrad_pk_try<T>(dY, ldy, sa_o, sa_i, X, ldx, sx_o, sx_i, dW, lddw, sw_o, sw_i, nullptr, Z, nzi, M, N, K,
+                          st) == 0)
+        return SVK_OK;
+    }
     const long vw = 16 / (long)sizeof(T);
     const bool va = aligned16(dY) && ldy % vw == 0 && sa_o % vw == 0 && sa_i % vw == 0 && ldy >= (N + 7) / 8 * 8;
     const bool vb = aligned16(X) && ldx % vw == 0 && sx_o % vw == 0 && sx_i % vw == 0 && K % 8 == 0;
@@ -828,6 +833,9 @@ extern "C" int svk_gemm_wgrad(int dtype, const void* dY, long ldy, const void* X
   a.dY = dY; a.ldy = ldy; a.X = X; a.ldx = ldx; a.dW = dW; a.lddw = lddw; a.M = M; a.N = N; a.K = K; a.db = db;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) {
+      if (wgrad_pk_try<T>(dY, ldy, 0, 0, X, ldx, 0, 0, dW, lddw, 0, 0, db, 1, 1, M, N, K, st) == 0) return SVK_OK;
+    }
     const long vw = 16 / (long)sizeof(T);
     const bool va = aligned16(dY) && ldy % vw == 0 && N % 8 == 0;
     const bool vb = aligned16(X) && ldx % vw == 0 && K % 8 == 0;

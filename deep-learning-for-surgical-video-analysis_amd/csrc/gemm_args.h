@@ -33,4 +33,11 @@ struct GemmArgs {
 template <typename T> int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
 template <typename T> int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
 
+// wgrad_pk.hip: dW (+ db) += dY^T X (16-bit operands, LDS-DMA slabs + ds_read_b64_tr_b16 fragments),
+// batched over Z = (Z / nzi, Z % nzi) element offsets; returns 1 when not eligible (caller: wgrad_kernel).
+template <typename T>
+int wgrad_pk_try(const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o, long sx_i,
+                 float* dW, long lddw, long sw_o, long sw_i, float* db, int Z, int nzi, int M, int N, int K,
+                 hipStream_t st);
+
 }  // namespace svk

@@ -739,7 +739,7 @@ def gemm_wgrad(dy, x, dw, db=None):
     else:
         _lib.call("svk_gemm_wgrad", dtype_code(dy.dtype), _p(dy), ldy, _p(x), ldx, _p(dw), lddw, _p(db), M, N, K,
                   _stream())
-        name = "wgrad_kernel"
+        name = "wgrad_pk" if dy.dtype in H16 else "wgrad_kernel"
     _prof_end(t0, name, 2.0 * M * N * K, (M * (N + K)) * dy.element_size() + N * K * 4, (M, N, K, "wgrad"))
     return dw
 
