@@ -481,6 +481,8 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
       cfg = (t128 < 512 && a.N <= 128) ? 30 : (a.N % 128 == 0 ? 20 : 10);
     } else {
       cfg = (big || (a.N % 128 == 0 && a.M < 32768)) ? 0 : 10;
+      // (round-2 sweep: 128 x 128 for the stage-3 fc1 and 128 x 160 for its fc2 win 5-7 us each in
+      // isolation but lost 2 % of the whole graph-replayed step: kept 128 x 64)
     }
   }
   const bool reg_epi = cfg == 0 && (big || a.M < 32768);

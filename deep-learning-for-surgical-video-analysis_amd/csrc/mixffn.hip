@@ -132,7 +132,7 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
                                                      const float* __restrict__ b2, T* __restrict__ Y,
                                                      T* __restrict__ Yn, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps, int H,
-                                                     int nstrip, int total) {
+                                                     int nstrip, int total, int diag) {
   typedef v8_t<T> tx8;
   constexpr int W = K::W, C = K::C, HC = K::HC, HID = K::HID, NPC = K::NPC, CS = K::CS, NCH = K::NCH;
   constexpr int CPR1 = C / 8, CPR2 = HID / 8;           // 16-byte chunks per W1 / W2 row
@@ -400,8 +400,13 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
             for (int h = 0; h < 2; ++h) {
               const int o = (dg * K::RV + rr) * W + 2 * dp + h;
               uint2 v;
-              v.x = pack2<T>(gelu_dw(acc[rr][0][h]), gelu_dw(acc[rr][1][h]));
-              v.y = pack2<T>(gelu_dw(acc[rr][2][h]), gelu_dw(acc[rr][3][h]));
+              if (diag == 1) {   // timing diagnostic only (svk_tune("ffn_diag", 1)): GELU replaced by ReLU
+                v.x = pack2<T>(fmaxf(acc[rr][0][h], 0.f), fmaxf(acc[rr][1][h], 0.f));
+                v.y = pack2<T>(fmaxf(acc[rr][2][h], 0.f), fmaxf(acc[rr][3][h], 0.f));
+              } else {
+                v.x = pack2<T>(gelu_dw(acc[rr][0][h]), gelu_dw(acc[rr][1][h]));
+                v.y = pack2<T>(gelu_dw(acc[rr][2][h]), gelu_dw(acc[rr][3][h]));
+              }
               *reinterpret_cast<uint2*>(G0 + o * K::GROW + (((dq >> 1) ^ gsw(o)) << 4) + (dq & 1) * 8) = v;
             }
           }
@@ -431,7 +436,8 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
   if (total > 0x7fffffffL) { set_error("svk_mixffn_fused: too many strips"); return SVK_EINVAL; }
   const int grid = (int)std::min<long>(total, cus);
   hipLaunchKernelGGL((mixffn_ws<T, K>), dim3(grid), dim3(K::NT), K::LDS, st, (const T*)XN, (const T*)X, (const T*)W1,
-                     b1, (const uint4*)tpk, (const T*)W2, b2, (T*)Y, (T*)Yn, gamma, beta, eps, H, nstrip, (int)total);
+                     b1, (const uint4*)tpk, (const T*)W2, b2, (T*)Y, (T*)Yn, gamma, beta, eps, H, nstrip, (int)total,
+                     g_tune[TUNE_FFN_DIAG] > 0 ? g_tune[TUNE_FFN_DIAG] : 0);
   static char name[96];
   if (!name[0])
     snprintf(name, sizeof(name), "mixffn_ws<%s, Cfg<%d, %d, %d, %d, %d>>", type_name<T>(), K::C, K::W, K::R, K::RV,

@@ -1,5 +1,3 @@
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_train_gpu.py tests/test_kernels_gpu.py -k "wgrad or attention" -x -q --timeout 240 --timeout-method thread > gpurun_out/t_t.log 2>&1; rc=$?; tail -2 gpurun_out/t_t.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python bench.py --workload train --steps 10 --warmup 3 --cpu-baseline-seconds 10 --dump-gemm gpurun_out/train_shapes.txt > gpurun_out/b_t.log 2>&1; rc=$?; grep -o '"value": [0-9.]*' gpurun_out/b_t.log | head -2; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_t -o run -- python bench.py --no-cpu-baseline --workload train --no-graph --steps 5 --warmup 2 > gpurun_out/prof_t.log 2>&1 || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_sw -o run -- python tools/pk_cfg_sweep.py --reps 5 > gpurun_out/prof_sw.log 2>&1; rc=$?; grep -o 'Cijk[A-Za-z0-9_]*' gpurun_out/prof_sw/run_kernel_stats.csv | sort | uniq | cut -c1-160 | head -20; exit $rc
+timeout -k 10 400 python -u -m pytest tests/test_train_gpu.py -k b88 -x -q -s --timeout 380 --timeout-method thread -p no:cacheprovider > gpurun_out/t_b88.log 2>&1; rc=$?; tail -2 gpurun_out/t_b88.log; grep "B=88" gpurun_out/t_b88.log | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+R=r02 bash tools/gpu_prof.sh
