@@ -147,6 +147,24 @@ class Attention(nn.Module):
         o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], self.num_heads, self.scale)
         return ops.gemm(o, p["wp"], p["bp"], residual=residual)
 
+    def block_fusable(self, x, H, W):
+        """True when svk_attn_block_s1 covers this layer: 16-bit, one 64-channel head, <= 64 reduced keys."""
+        r = self.sr_ratio
+        return (ops.FUSED_ATTN_BLOCK and x.dtype in ops.H16 and self.num_heads == 1 and self.dim == 64 and r > 1
+                and (H // r) * (W // r) <= 64)
+
+    def forward_block(self, hn, H, W, x, ln2):
+        """(x + attn(hn), norm2(x + attn(hn))) for the stage-1 shape in one kernel after the sequence
+        reduction (q, attention, proj + residual and the next LayerNorm never leave the chip)."""
+        B, N, C = hn.shape
+        p = get_packed(self, hn.dtype, self._pack)
+        hn = hn.contiguous()
+        r = self.sr_ratio
+        xs = ops.conv2d_ln_nhwc(hn.view(B, H, W, C), p["wsr"], r, r, 0, p["bsr"], p["gn"], p["bn"], self.norm.eps)
+        kv = ops.gemm(xs.view(B, -1, C), p["wkv"], p["bkv"])
+        return ops.attn_block_s1(hn, x.contiguous(), kv, p["wq"], p["bq"], p["wp"], p["bp"], ln2[0], ln2[1], ln2[2],
+                                 self.scale)
+
 
 class Block(nn.Module):
     """x + attn(LN(x)); x + mlp(LN(x)) (mix_transformer_evp.py:134-171), residual adds fused in the GEMMs."""
@@ -171,6 +189,9 @@ class Block(nn.Module):
         p = get_packed(self, x.dtype, self._pack)
         x = x.contiguous()
         h = ops.layernorm(x, p["g1"], p["b1"], self.norm1.eps)
+        if self.attn.block_fusable(x, H, W):
+            x, h = self.attn.forward_block(h, H, W, x, (p["g2"], p["b2"], self.norm2.eps))
+            return self.mlp(h, H, W, residual=x, ln=ln)
         x = self.attn(h, H, W, residual=x)
         h = ops.layernorm(x, p["g2"], p["b2"], self.norm2.eps)
         return self.mlp(h, H, W, residual=x, ln=ln)

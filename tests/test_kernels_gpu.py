@@ -502,3 +502,38 @@ def test_mixffn_fc1_dwconv(cuda, B, H, W, C, dt):
     k = taps.cpu().double().t().reshape(hid, 1, 3, 3)
     ref = F.gelu(F.conv2d(hr.permute(0, 3, 1, 2), k, db.cpu().double(), padding=1, groups=hid)).permute(0, 2, 3, 1)
     _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("B,N,Nk", [(2, 3136, 49), (3, 300, 64), (1, 17, 5)])
+def test_attn_block_s1_vs_unfused(cuda, dt, B, N, Nk):
+    """The fused stage-1 attention half of a Block (q GEMM -> attention -> proj + residual -> LayerNorm)
+    == the unfused kernel chain with the same roundings (within one storage ulp), and == fp64 torch."""
+    from svk import ops
+    C = 64
+    hn = _rand(B, N, C, dt=dt, dev=cuda, seed=40)
+    x = _rand(B, N, C, dt=dt, dev=cuda, seed=41)
+    kv = _rand(B, Nk, 2 * C, dt=dt, dev=cuda, seed=42)
+    wq = _rand(C, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=43)
+    wp = _rand(C, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=44)
+    bq = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=45)
+    bp = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=46)
+    g2 = _rand(C, dt=torch.float32, dev=cuda, seed=47)
+    b2 = _rand(C, dt=torch.float32, dev=cuda, seed=48)
+    scale = C ** -0.5
+    y, h2 = ops.attn_block_s1(hn, x, kv, wq, bq, wp, bp, g2, b2, 1e-6, scale)
+    q = ops.gemm(hn, wq, bq)
+    o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], 1, scale)
+    yu = ops.gemm(o, wp, bp, residual=x)
+    h2u = ops.layernorm(yu, g2, b2, 1e-6)
+    torch.cuda.synchronize()
+    ulp = 2.0 ** -10 if dt == torch.float16 else 2.0 ** -7
+    for got, ref in ((y, yu), (h2, h2u)):
+        d = (got.float() - ref.float()).abs() / ref.float().abs().clamp_min(1.0)
+        assert float(d.max()) <= 2 * ulp, float(d.max())
+    # fp64 reference of the same math on the same (rounded) inputs
+    f = lambda t: t.cpu().double()
+    qd = f(hn) @ f(wq).t() + f(bq)
+    att = ((qd @ f(kv[:, :, :C]).transpose(1, 2)) * scale).softmax(-1) @ f(kv[:, :, C:])
+    yd = f(x) + att @ f(wp).t() + f(bp)
+    _close(y, yd, dt)
