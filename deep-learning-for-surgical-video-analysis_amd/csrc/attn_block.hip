@@ -22,6 +22,7 @@
 //   leave as 16-byte row pieces through the patch.
 #include "svk_common.h"
 #include <stdio.h>
+#include <type_traits>
 
 namespace svk {
 namespace ab {
@@ -29,9 +30,9 @@ namespace ab {
 constexpr int D = 64;          // channels = head dim (one head)
 constexpr int KLD = D + 8;     // LDS row stride (elements) of Wq / Wp / K / the patches
 constexpr int VLD = 64 + 8;    // V^T row stride (keys padded to 64)
-constexpr int QB = 256;
+constexpr int QB = 256;   // default queries per workgroup (svk_tune("ffn_diag") 2 / 3: 512 / 1024, sweep)
 
-template <typename T>
+template <typename T, int QB>
 __global__ __launch_bounds__(256) void attn_block_s1(const T* __restrict__ Hn, const T* __restrict__ X,
                                                      const T* __restrict__ KV, long ldkv, const T* __restrict__ Wq,
                                                      const float* __restrict__ bq, const T* __restrict__ Wp,
@@ -90,16 +91,29 @@ __global__ __launch_bounds__(256) void attn_block_s1(const T* __restrict__ Hn, c
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   const int qbase = blockIdx.x * QB;
+  // software pipeline over the wave's tiles: the next tile's h rows and this tile's x rows are in flight
+  // while the current tile computes
+  auto load_h = [&](int q0, tx8 (&hb)[2]) {
+    const int qr = min(q0 + c, N - 1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) hb[ks] = *reinterpret_cast<const tx8*>(Hb + (long)qr * D + 32 * ks + 8 * g);
+  };
+  tx8 hb_next[2];
+  if (qbase + wave * 16 < N) load_h(qbase + wave * 16, hb_next);
   for (int qt = wave; qt < QB / 16; qt += 4) {
     const int q0 = qbase + qt * 16;
     if (q0 >= N) break;
+    tx8 xr[2];                                     // this tile's x rows (row e >> 3, chunk e & 7 of e = lane + 64 k)
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      xr[k] = *reinterpret_cast<const tx8*>(Xb + (long)min(q0 + (e >> 3), N - 1) * D + (e & 7) * 8);
+    }
     // ---- Q^T = Wq . H^T: lane (c, g) gets q[query q0 + c][16 dt + 4 g + r]
     f32x4 qa[4];
     {
-      const int qr = min(q0 + c, N - 1);
-      tx8 hb[2];
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) hb[ks] = *reinterpret_cast<const tx8*>(Hb + (long)qr * D + 32 * ks + 8 * g);
+      tx8 hb[2] = {hb_next[0], hb_next[1]};
+      if (q0 + 64 < min(N, qbase + QB)) load_h(q0 + 64, hb_next);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         qa[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -206,13 +220,10 @@ __global__ __launch_bounds__(256) void attn_block_s1(const T* __restrict__ Hn, c
     // ya[nt][r] = Y[query c][n = 16 nt + 4 g + r] (W fragment x O fragment): the lane owns 16 channels
     // {16 nt + 4 g + r} of query c.  Stage the x tile through the patch (row layout) for the residual.
     wave_sync();                                   // the o reads of the patch are done
-    {
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int e = lane + 64 * k, row = e >> 3, c8 = (e & 7) * 8;
-        const int q = min(q0 + row, N - 1);
-        *reinterpret_cast<tx8*>(&patch[row][c8]) = *reinterpret_cast<const tx8*>(Xb + (long)q * D + c8);
-      }
+    for (int k = 0; k < 2; ++k) {
+      const int e = lane + 64 * k;
+      *reinterpret_cast<tx8*>(&patch[e >> 3][(e & 7) * 8]) = xr[k];
     }
     wave_sync();
     float yv[4][4], sum = 0.f;
@@ -293,12 +304,19 @@ extern "C" int svk_attn_block_s1(int dtype, const void* Hn, const void* X, const
   }
   if (B == 0 || N == 0) return SVK_OK;
   if (B > 65535) { set_error("svk_attn_block_s1: grid too large"); return SVK_EUNSUPPORTED; }
-  dim3 grid((N + ab::QB - 1) / ab::QB, B);
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t st = (hipStream_t)stream;
+  const int qsel = g_tune[TUNE_FFN_DIAG];
   SVK_DISPATCH_H16(dtype, T, {
-    hipLaunchKernelGGL((ab::attn_block_s1<T>), grid, dim3(256), 0, st, (const T*)Hn, (const T*)X, (const T*)KV, ldkv,
-                       (const T*)Wq, bq, (const T*)Wp, bp, gamma2, beta2, eps, (T*)Y, (T*)H2, N, Nk, sl2);
+    auto go = [&](auto qb_c) {
+      constexpr int QBv = decltype(qb_c)::value;
+      dim3 grid((N + QBv - 1) / QBv, B);
+      hipLaunchKernelGGL((ab::attn_block_s1<T, QBv>), grid, dim3(256), 0, st, (const T*)Hn, (const T*)X, (const T*)KV,
+                         ldkv, (const T*)Wq, bq, (const T*)Wp, bp, gamma2, beta2, eps, (T*)Y, (T*)H2, N, Nk, sl2);
+    };
+    if (qsel == 2) go(std::integral_constant<int, 512>{});
+    else if (qsel == 3) go(std::integral_constant<int, 1024>{});
+    else go(std::integral_constant<int, ab::QB>{});
     set_last_kernel(dtype == SVK_F16 ? "attn_block_s1<_Float16>" : "attn_block_s1<__bf16>");
     return check_launch("attn_block_s1");
   });

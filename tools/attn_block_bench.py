@@ -36,6 +36,11 @@ def main():
              "attn": lambda: ops.attention(q, kv[:, :, :C], kv[:, :, C:], 1, 0.125),
              "proj": lambda: ops.gemm(o, wp, bp, residual=x),
              "ln2": lambda: ops.layernorm(y, g2, b2, 1e-6)}
+    from svk import _lib
+    for sel, qb in ((0, 256), (2, 512), (3, 1024)):
+        _lib.load().svk_tune(b"ffn_diag", sel)
+        print(f"QB={qb}: fused {timeit(fused):7.1f} us")
+    _lib.load().svk_tune(b"ffn_diag", 0)
     tf = timeit(fused)
     tp = {k: timeit(f) for k, f in parts.items()}
     print(f"fused {tf:7.1f} us | unfused {sum(tp.values()):7.1f} us = " + " + ".join(f"{k} {v:.1f}" for k, v in tp.items()))
