@@ -148,13 +148,14 @@ class Attention(nn.Module):
         return ops.gemm(o, p["wp"], p["bp"], residual=residual)
 
     def block_fusable(self, x, H, W):
-        """True when svk_attn_block_s1 covers this layer: 16-bit, one 64-channel head, <= 64 reduced keys."""
+        """True when svk_attn_block covers this layer: 16-bit, 64-channel heads with C in {64, 128} (MiT
+        stages 1-2), <= 64 reduced keys."""
         r = self.sr_ratio
-        return (ops.FUSED_ATTN_BLOCK and x.dtype in ops.H16 and self.num_heads == 1 and self.dim == 64 and r > 1
-                and (H // r) * (W // r) <= 64)
+        return (ops.FUSED_ATTN_BLOCK and x.dtype in ops.H16 and self.dim in (64, 128) and self.dim == 64 * self.num_heads
+                and r > 1 and (H // r) * (W // r) <= 64)
 
     def forward_block(self, hn, H, W, x, ln2):
-        """(x + attn(hn), norm2(x + attn(hn))) for the stage-1 shape in one kernel after the sequence
+        """(x + attn(hn), norm2(x + attn(hn))) for the stage-1/2 shapes in one kernel after the sequence
         reduction (q, attention, proj + residual and the next LayerNorm never leave the chip)."""
         B, N, C = hn.shape
         p = get_packed(self, hn.dtype, self._pack)
@@ -162,7 +163,7 @@ class Attention(nn.Module):
         r = self.sr_ratio
         xs = ops.conv2d_ln_nhwc(hn.view(B, H, W, C), p["wsr"], r, r, 0, p["bsr"], p["gn"], p["bn"], self.norm.eps)
         kv = ops.gemm(xs.view(B, -1, C), p["wkv"], p["bkv"])
-        return ops.attn_block_s1(hn, x.contiguous(), kv, p["wq"], p["bq"], p["wp"], p["bp"], ln2[0], ln2[1], ln2[2],
+        return ops.attn_block(hn, x.contiguous(), kv, p["wq"], p["bq"], p["wp"], p["bp"], ln2[0], ln2[1], ln2[2],
                                  self.scale)
 
 

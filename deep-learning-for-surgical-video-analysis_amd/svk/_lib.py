@@ -57,7 +57,7 @@ SIGNATURES = {
     "svk_anticipation_gt": [P, c_long, c_int, c_int, ctypes.c_double, P, P],
     "svk_window_unfold": [c_int, P, c_long, P, P, c_int, c_int, c_int, P],
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
-    "svk_attn_block_s1": [c_int, P, P, P, c_long, P, P, P, P, P, P, c_float, P, P, c_int, c_int, c_int, c_int,
+    "svk_attn_block": [c_int, P, P, P, c_long, P, P, P, P, P, P, c_float, P, P, c_int, c_int, c_int, c_int,
                           c_float, P],
     "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],

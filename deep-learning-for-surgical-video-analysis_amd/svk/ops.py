@@ -265,12 +265,12 @@ def mixffn_supported(W, C):
 FUSED_ATTN_BLOCK = os.environ.get("SVK_FUSED_ATTN_BLOCK", "1") == "1"
 
 
-def attn_block_s1(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
-    """Stage-1 attention half of a MiT Block (one 64-channel head, <= 64 reduced keys) in one kernel:
-    returns (y, h2) with y = x + proj(attn(q(hn), k, v)) and h2 = LayerNorm(y) (svk_attn_block_s1).
-    hn, x [B, N, 64] contiguous; kv [B, Nk, 128] (k | v)."""
+def attn_block(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
+    """Attention half of a MiT Block with 64-channel heads (C = 64 / 1 head, C = 128 / 2 heads; <= 64
+    reduced keys) in one kernel: returns (y, h2) with y = x + proj(attn(q(hn), k, v)) and h2 = LayerNorm(y)
+    (svk_attn_block).  hn, x [B, N, C] contiguous; kv [B, Nk, 2C] (k | v)."""
     if hn.dtype not in H16:
-        raise _lib.SvkError("svk.attn_block_s1: bf16 / f16 only")
+        raise _lib.SvkError("svk.attn_block: bf16 / f16 only")
     for t, nm in ((hn, "hn"), (x, "x"), (kv, "kv"), (wq, "wq"), (wp, "wp")):
         _chk(t, nm, hn.dtype)
     for t, nm in ((bq, "bq"), (bp, "bp"), (gamma2, "gamma2"), (beta2, "beta2")):
@@ -279,15 +279,15 @@ def attn_block_s1(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
     Bk, Nk, C2 = kv.shape
     if (x.shape != hn.shape or Bk != B or C2 != 2 * C or not (hn.is_contiguous() and x.is_contiguous()
                                                                and kv.is_contiguous())):
-        raise _lib.SvkError("svk.attn_block_s1: shape / layout mismatch")
+        raise _lib.SvkError("svk.attn_block: shape / layout mismatch")
     y = torch.empty_like(x)
     h2 = torch.empty_like(x)
     t0 = _prof_begin()
-    _lib.call("svk_attn_block_s1", dtype_code(hn.dtype), _p(hn), _p(x), _p(kv), 2 * C, _p(wq), _p(bq), _p(wp), _p(bp),
+    _lib.call("svk_attn_block", dtype_code(hn.dtype), _p(hn), _p(x), _p(kv), 2 * C, _p(wq), _p(bq), _p(wp), _p(bp),
               _p(gamma2), _p(beta2), float(eps), _p(y), _p(h2), B, N, Nk, C, float(scale), _stream())
     if t0 is not None:
         M = B * N
-        _prof_end(t0, "attn_block_s1", 2.0 * M * C * C * 2 + 4.0 * M * 64 * C, 4 * M * C * 2, (M, C, "attn_block"))
+        _prof_end(t0, f"attn_block<{C}>", 2.0 * M * C * C * 2 + 4.0 * M * 64 * C, 4 * M * C * 2, (M, C, "attn_block"))
     return y, h2
 
 

@@ -146,11 +146,12 @@ int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C,
 int svk_mstcn_layer(const float* X, const float* WdT, const float* bd, const float* W1T,
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
-/* Stage-1 attention half of a MiT Block in one kernel (mix_transformer_evp.py:71-131, 134-171; one head of
- * C = 64 channels, sequence-reduced keys Nk <= 64), bf16 / f16: q = Hn Wq^T + bq, o = softmax(scale q k^T) v,
- * Y = X + o Wp^T + bp, H2 = LayerNorm(Y; gamma2, beta2, eps).  Hn = norm1(X), X, Y, H2 contiguous [B, N, 64];
- * KV [B, Nk, ldkv] holds k | v (the kv Linear's output); Wq, Wp nn.Linear [64, 64]; bq may be NULL. */
-int svk_attn_block_s1(int dtype, const void* Hn, const void* X, const void* KV, long ldkv, const void* Wq,
+/* Attention half of a MiT Block in one kernel for the 64-channel-head stages (mix_transformer_evp.py:71-131,
+ * 134-171; C = 64 with one head (stage 1) or C = 128 with two heads (stage 2), sequence-reduced keys
+ * Nk <= 64), bf16 / f16: q = Hn Wq^T + bq, o_h = softmax(scale q_h k_h^T) v_h, Y = X + o Wp^T + bp,
+ * H2 = LayerNorm(Y; gamma2, beta2, eps).  Hn = norm1(X), X, Y, H2 contiguous [B, N, C]; KV [B, Nk, ldkv]
+ * holds k | v (the kv Linear's output); Wq, Wp nn.Linear [C, C]; bq may be NULL. */
+int svk_attn_block(int dtype, const void* Hn, const void* X, const void* KV, long ldkv, const void* Wq,
                       const float* bq, const void* Wp, const float* bp, const float* gamma2, const float* beta2,
                       float eps, void* Y, void* H2, int B, int N, int Nk, int C, float scale, void* stream);
 

@@ -505,12 +505,14 @@ def test_mixffn_fc1_dwconv(cuda, B, H, W, C, dt):
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("B,N,Nk", [(2, 3136, 49), (3, 300, 64), (1, 17, 5)])
-def test_attn_block_s1_vs_unfused(cuda, dt, B, N, Nk):
-    """The fused stage-1 attention half of a Block (q GEMM -> attention -> proj + residual -> LayerNorm)
-    == the unfused kernel chain with the same roundings (within one storage ulp), and == fp64 torch."""
+@pytest.mark.parametrize("B,N,Nk,C", [(2, 3136, 49, 64), (3, 300, 64, 64), (1, 17, 5, 64), (2, 784, 49, 128),
+                                      (3, 1000, 64, 128), (1, 9, 3, 128)])
+def test_attn_block_vs_unfused(cuda, dt, B, N, Nk, C):
+    """The fused attention half of a Block (q GEMM -> attention -> proj + residual -> LayerNorm; stage 1 C = 64
+    one head, stage 2 C = 128 two heads) == the unfused kernel chain with the same roundings (within two
+    storage ulps), and == fp64 torch."""
     from svk import ops
-    C = 64
+    heads = C // 64
     hn = _rand(B, N, C, dt=dt, dev=cuda, seed=40)
     x = _rand(B, N, C, dt=dt, dev=cuda, seed=41)
     kv = _rand(B, Nk, 2 * C, dt=dt, dev=cuda, seed=42)
@@ -520,10 +522,10 @@ def test_attn_block_s1_vs_unfused(cuda, dt, B, N, Nk):
     bp = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=46)
     g2 = _rand(C, dt=torch.float32, dev=cuda, seed=47)
     b2 = _rand(C, dt=torch.float32, dev=cuda, seed=48)
-    scale = C ** -0.5
-    y, h2 = ops.attn_block_s1(hn, x, kv, wq, bq, wp, bp, g2, b2, 1e-6, scale)
+    scale = 64 ** -0.5
+    y, h2 = ops.attn_block(hn, x, kv, wq, bq, wp, bp, g2, b2, 1e-6, scale)
     q = ops.gemm(hn, wq, bq)
-    o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], 1, scale)
+    o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], heads, scale)
     yu = ops.gemm(o, wp, bp, residual=x)
     h2u = ops.layernorm(yu, g2, b2, 1e-6)
     torch.cuda.synchronize()
@@ -533,7 +535,8 @@ def test_attn_block_s1_vs_unfused(cuda, dt, B, N, Nk):
         assert float(d.max()) <= 2 * ulp, float(d.max())
     # fp64 reference of the same math on the same (rounded) inputs
     f = lambda t: t.cpu().double()
+    sh = lambda t: t.reshape(B, t.shape[1], heads, 64).transpose(1, 2)
     qd = f(hn) @ f(wq).t() + f(bq)
-    att = ((qd @ f(kv[:, :, :C]).transpose(1, 2)) * scale).softmax(-1) @ f(kv[:, :, C:])
-    yd = f(x) + att @ f(wp).t() + f(bp)
+    att = ((sh(qd) @ sh(f(kv[:, :, :C])).transpose(-1, -2)) * scale).softmax(-1) @ sh(f(kv[:, :, C:]))
+    yd = f(x) + att.transpose(1, 2).reshape(B, N, C) @ f(wp).t() + f(bp)
     _close(y, yd, dt)

@@ -1,5 +1,5 @@
-"""Fused stage-1 attention half of a Block (svk_attn_block_s1) vs the unfused chain (q GEMM, sequence-
-reduced attention, proj GEMM + residual, LayerNorm) at B = 256.  Usage (GPU box): python tools/attn_block_bench.py"""
+"""Fused stage-1 attention half of a Block (svk_attn_block) vs the unfused chain (q GEMM, sequence-
+reduced attention, proj GEMM + residual, LayerNorm) at B = 256 (stage 1 and stage 2 shapes).  Usage (GPU box): python tools/attn_block_bench.py"""
 import os
 import sys
 
@@ -23,27 +23,27 @@ def timeit(fn, reps=20):
 
 
 def main():
-    dev, dt, B, N, Nk, C = torch.device("cuda:0"), torch.float16, 256, 3136, 49, 64
+    for N, C in ((3136, 64), (784, 128)):
+        run(N, C)
+
+
+def run(N, C):
+    dev, dt, B, Nk, heads = torch.device("cuda:0"), torch.float16, 256, 49, C // 64
     r = lambda *s: torch.randn(*s, device=dev).to(dt)
     hn, x, kv = r(B, N, C), r(B, N, C), r(B, Nk, 2 * C)
     wq, wp = r(C, C) * 0.125, r(C, C) * 0.125
     bq, bp, g2, b2 = (torch.randn(C, device=dev) for _ in range(4))
-    fused = lambda: ops.attn_block_s1(hn, x, kv, wq, bq, wp, bp, g2, b2, 1e-6, 0.125)
+    fused = lambda: ops.attn_block(hn, x, kv, wq, bq, wp, bp, g2, b2, 1e-6, 0.125)
     q = ops.gemm(hn, wq, bq)
-    o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], 1, 0.125)
+    o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], heads, 0.125)
     y = ops.gemm(o, wp, bp, residual=x)
     parts = {"q": lambda: ops.gemm(hn, wq, bq),
-             "attn": lambda: ops.attention(q, kv[:, :, :C], kv[:, :, C:], 1, 0.125),
+             "attn": lambda: ops.attention(q, kv[:, :, :C], kv[:, :, C:], heads, 0.125),
              "proj": lambda: ops.gemm(o, wp, bp, residual=x),
              "ln2": lambda: ops.layernorm(y, g2, b2, 1e-6)}
-    from svk import _lib
-    for sel, qb in ((0, 256), (2, 512), (3, 1024)):
-        _lib.load().svk_tune(b"ffn_diag", sel)
-        print(f"QB={qb}: fused {timeit(fused):7.1f} us")
-    _lib.load().svk_tune(b"ffn_diag", 0)
     tf = timeit(fused)
     tp = {k: timeit(f) for k, f in parts.items()}
-    print(f"fused {tf:7.1f} us | unfused {sum(tp.values()):7.1f} us = " + " + ".join(f"{k} {v:.1f}" for k, v in tp.items()))
+    print(f"C={C}: fused {tf:7.1f} us | unfused {sum(tp.values()):7.1f} us = " + " + ".join(f"{k} {v:.1f}" for k, v in tp.items()))
     print(f"fused: {4 * B * N * C * 2 / (tf * 1e-6) / 1e12:.2f} TB/s over h, x in and y, h2 out")
 
 
