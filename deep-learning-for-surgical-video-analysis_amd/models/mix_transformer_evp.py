@@ -185,11 +185,13 @@ class Block(nn.Module):
         g2, b2 = _ln_params(self.norm2)
         return dict(g1=g1, b1=b1, g2=g2, b2=b2)
 
-    def forward(self, x, H, W, ln=None):
-        """``ln``: (gamma, beta, eps) of a LayerNorm applied to the block output (see Mlp.forward)."""
+    def forward(self, x, H, W, ln=None, h=None):
+        """``ln``: (gamma, beta, eps) of a LayerNorm applied to the block output (see Mlp.forward);
+        ``h``: norm1(x) when the caller already has it (the fused prompt + norm1 kernel)."""
         p = get_packed(self, x.dtype, self._pack)
         x = x.contiguous()
-        h = ops.layernorm(x, p["g1"], p["b1"], self.norm1.eps)
+        if h is None:
+            h = ops.layernorm(x, p["g1"], p["b1"], self.norm1.eps)
         if self.attn.block_fusable(x, H, W):
             x, h = self.attn.forward_block(h, H, W, x, (p["g2"], p["b2"], self.norm2.eps))
             return self.mlp(h, H, W, residual=x, ln=ln)
@@ -336,6 +338,23 @@ class PromptGenerator(nn.Module):
         ps = get_packed(sh, dt, lambda d: dict(w=lin_w(sh, d), b=lin_b(sh)))
         feat = ops.gemm(summed, pl["w"], pl["b"], act="gelu")
         return ops.gemm(feat, ps["w"], ps["b"], residual=x)
+
+    def get_prompt_ln(self, x, prompt, block_num, depth_num, norm):
+        """(get_prompt(...), norm(get_prompt(...))) in one kernel for C in {64, 128} at 16 bits
+        (svk_prompt_ln); None when not covered."""
+        summed = getattr(prompt, "summed", None)
+        C = x.shape[-1]
+        if (not ops.FUSED_PROMPT_LN or summed is None or x.dtype not in ops.H16 or C not in (64, 128)
+                or summed.shape[-1] != C // 4):
+            return None
+        lw = getattr(self, f"lightweight_mlp{block_num}_{depth_num}")[0]
+        sh = getattr(self, f"shared_mlp{block_num}")
+        dt = x.dtype
+        pl = get_packed(lw, dt, lambda d: dict(w=lin_w(lw, d), b=lin_b(lw)))
+        ps = get_packed(sh, dt, lambda d: dict(w=lin_w(sh, d), b=lin_b(sh)))
+        pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
+        return ops.prompt_ln(x.contiguous(), summed.contiguous(), pl["w"], pl["b"], ps["w"], ps["b"], pn[0], pn[1],
+                             norm.eps)
 
 
 class _Prompt(tuple):
@@ -506,9 +525,14 @@ class MixVisionTransformerEVP(nn.Module):
             pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
             blocks = getattr(self, f"block{s + 1}")
             for i, blk in enumerate(blocks):
-                t = self.prompt_generator.get_prompt(t, prompt, s + 1, i)
                 # the stage norm (:370-412) rides on the last block's MixFFN epilogue
-                t = blk(t, H, W, ln=(pn[0], pn[1], norm.eps) if i == len(blocks) - 1 else None)
+                ln = (pn[0], pn[1], norm.eps) if i == len(blocks) - 1 else None
+                fused = self.prompt_generator.get_prompt_ln(t, prompt, s + 1, i, blk.norm1)
+                if fused is not None:          # prompt add + norm1 in one kernel (stages 1-2)
+                    t = blk(fused[0], H, W, ln=ln, h=fused[1])
+                else:
+                    t = self.prompt_generator.get_prompt(t, prompt, s + 1, i)
+                    t = blk(t, H, W, ln=ln)
             if len(blocks) == 0:
                 t = ops.layernorm(t, pn[0], pn[1], norm.eps)
             outs.append((t, H, W))

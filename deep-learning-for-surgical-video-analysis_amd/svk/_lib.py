@@ -59,6 +59,7 @@ SIGNATURES = {
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],
     "svk_attn_block": [c_int, P, P, P, c_long, P, P, P, P, P, P, c_float, P, P, c_int, c_int, c_int, c_int,
                           c_float, P],
+    "svk_prompt_ln": [c_int, P, P, P, P, P, P, P, P, c_float, P, P, c_int, c_int, P],
     "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
     # training step

@@ -263,6 +263,7 @@ def mixffn_supported(W, C):
 
 
 FUSED_ATTN_BLOCK = os.environ.get("SVK_FUSED_ATTN_BLOCK", "1") == "1"
+FUSED_PROMPT_LN = os.environ.get("SVK_FUSED_PROMPT_LN", "1") == "1"
 
 
 def attn_block(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
@@ -289,6 +290,31 @@ def attn_block(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
         M = B * N
         _prof_end(t0, f"attn_block<{C}>", 2.0 * M * C * C * 2 + 4.0 * M * 64 * C, 4 * M * C * 2, (M, C, "attn_block"))
     return y, h2
+
+
+def prompt_ln(x, summed, wl, bl, ws, bs, gamma1, beta1, eps):
+    """(x + shared(GELU(light(summed))), norm1 of that) in one kernel (svk_prompt_ln; C in {64, 128}):
+    x [B, N, C], summed [B, N, C // 4] contiguous bf16 / f16 -> (x', h)."""
+    if x.dtype not in H16:
+        raise _lib.SvkError("svk.prompt_ln: bf16 / f16 only")
+    for t, nm in ((x, "x"), (summed, "summed"), (wl, "wl"), (ws, "ws")):
+        _chk(t, nm, x.dtype)
+    for t, nm in ((bl, "bl"), (bs, "bs"), (gamma1, "gamma1"), (beta1, "beta1")):
+        _chk(t, nm, torch.float32)
+    C = x.shape[-1]
+    M = x.numel() // C
+    if (summed.numel() != M * (C // 4) or wl.shape != (C // 4, C // 4) or ws.shape != (C, C // 4)
+            or not (x.is_contiguous() and summed.is_contiguous() and wl.is_contiguous() and ws.is_contiguous())):
+        raise _lib.SvkError("svk.prompt_ln: shape / layout mismatch")
+    xo = torch.empty_like(x)
+    h = torch.empty_like(x)
+    t0 = _prof_begin()
+    _lib.call("svk_prompt_ln", dtype_code(x.dtype), _p(summed), _p(x), _p(wl), _p(bl), _p(ws), _p(bs), _p(gamma1),
+              _p(beta1), float(eps), _p(xo), _p(h), M, C, _stream())
+    if t0 is not None:
+        _prof_end(t0, f"prompt_ln<{C}>", 2.0 * M * (C // 4) * (C // 4 + C), (3 * M * C + M * C // 4) * 2,
+                  (M, C, "prompt_ln"))
+    return xo, h
 
 
 def mixffn_pack_taps(taps, dbias, dtype):

@@ -146,6 +146,14 @@ int svk_softmax_rows(const float* X, long ldx, float* Y, long ldy, int M, int C,
 int svk_mstcn_layer(const float* X, const float* WdT, const float* bd, const float* W1T,
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
+/* Prompt adapter + norm1 of a MiT Block in one kernel (mix_transformer_evp.py:776-815 get_prompt, then
+ * Block.norm1), C in {64, 128} (stages 1-2), prompt width C4 = C / 4, bf16 / f16:
+ * Xo = X + GELU(S Wl^T + bl) Ws^T + bs, Ho = LayerNorm(Xo; gamma1, beta1, eps).  S [M, C4], X / Xo / Ho [M, C]
+ * contiguous; Wl [C4, C4], Ws [C, C4] (nn.Linear); bl / bs may be NULL. */
+int svk_prompt_ln(int dtype, const void* S, const void* X, const void* Wl, const float* bl, const void* Ws,
+                  const float* bs, const float* gamma1, const float* beta1, float eps, void* Xo, void* Ho, int M,
+                  int C, void* stream);
+
 /* Attention half of a MiT Block in one kernel for the 64-channel-head stages (mix_transformer_evp.py:71-131,
  * 134-171; C = 64 with one head (stage 1) or C = 128 with two heads (stage 2), sequence-reduced keys
  * Nk <= 64), bf16 / f16: q = Hn Wq^T + bq, o_h = softmax(scale q_h k_h^T) v_h, Y = X + o Wp^T + bp,

@@ -540,3 +540,29 @@ def test_attn_block_vs_unfused(cuda, dt, B, N, Nk, C):
     att = ((sh(qd) @ sh(f(kv[:, :, :C])).transpose(-1, -2)) * scale).softmax(-1) @ sh(f(kv[:, :, C:]))
     yd = f(x) + att.transpose(1, 2).reshape(B, N, C) @ f(wp).t() + f(bp)
     _close(y, yd, dt)
+
+
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("M,C", [(2 * 3136, 64), (1000, 64), (17, 64), (2 * 784, 128), (33, 128)])
+def test_prompt_ln_vs_unfused(cuda, dt, M, C):
+    """Prompt adapter + norm1 in one kernel == the unfused chain (lightweight GEMM + GELU, shared GEMM +
+    residual, LayerNorm) within two storage ulps."""
+    from svk import ops
+    C4 = C // 4
+    x = _rand(M, C, dt=dt, dev=cuda, seed=50)
+    sm = _rand(M, C4, dt=dt, dev=cuda, seed=51)
+    wl = _rand(C4, C4, dt=dt, dev=cuda, scale=C4 ** -0.5, seed=52)
+    ws = _rand(C, C4, dt=dt, dev=cuda, scale=C4 ** -0.5, seed=53)
+    bl = _rand(C4, dt=torch.float32, dev=cuda, scale=0.1, seed=54)
+    bs = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=55)
+    g1 = _rand(C, dt=torch.float32, dev=cuda, seed=56)
+    b1 = _rand(C, dt=torch.float32, dev=cuda, seed=57)
+    xo, h = ops.prompt_ln(x, sm, wl, bl, ws, bs, g1, b1, 1e-6)
+    f = ops.gemm(sm, wl, bl, act="gelu")
+    xu = ops.gemm(f, ws, bs, residual=x)
+    hu = ops.layernorm(xu, g1, b1, 1e-6)
+    torch.cuda.synchronize()
+    ulp = 2.0 ** -10 if dt == torch.float16 else 2.0 ** -7
+    for got, ref in ((xo, xu), (h, hu)):
+        d = (got.float() - ref.float()).abs() / ref.float().abs().clamp_min(1.0)
+        assert float(d.max()) <= 2 * ulp, float(d.max())
