@@ -555,6 +555,77 @@ __global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, 
   }
 }
 
+// 4-column variant (W % 4 == 0, C <= 3, Cpad == 8, the prompt generator's frame / segmap filter): a thread
+// owns 4 consecutive columns x GR rows; each input row piece is three aligned float4 loads (columns x0 - 4 ..
+// x0 + 7, reflected at the image edges from the middle block) instead of 5 scalar loads per column, and
+// each output pixel leaves as one 16-byte store.  Same arithmetic order as gauss5x5_kernel (bitwise equal).
+template <typename T>
+__global__ __launch_bounds__(256) void gauss5x5_x4_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W,
+                                   int nstrip) {
+  const int W4 = W >> 2;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)B * nstrip * W4) return;
+  const int x0 = (int)(idx % W4) * 4;
+  const long t = idx / W4;
+  const int s = (int)(t % nstrip);
+  const int b = (int)(t / nstrip);
+  const int y0 = s * GR;
+  const float k1[5] = {1.f / 16.f, 4.f / 16.f, 6.f / 16.f, 4.f / 16.f, 1.f / 16.f};
+  const bool left = x0 == 0, right = x0 + 4 == W;
+  float out[GR][4][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (c >= C) {
+#pragma unroll
+      for (int r = 0; r < GR; ++r)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[r][k][c] = 0.f;
+      continue;
+    }
+    const float* src = X + ((long)b * C + c) * H * W;
+    float h[GR + 4][4];
+#pragma unroll
+    for (int r = 0; r < GR + 4; ++r) {
+      const int yy = reflect(min(y0 + r - 2, H + 1), H);
+      const float* row = src + (long)yy * W + x0;
+      const float4 m = *reinterpret_cast<const float4*>(row);
+      const float4 l = left ? m : *reinterpret_cast<const float4*>(row - 4);
+      const float4 rr = right ? m : *reinterpret_cast<const float4*>(row + 4);
+      // window w[j] = column x0 - 2 + j (reflect: -2 -> 2, -1 -> 1, W -> W - 2, W + 1 -> W - 3)
+      const float w[8] = {left ? m.z : l.z, left ? m.y : l.w, m.x, m.y, m.z, m.w, right ? m.z : rr.x, right ? m.y : rr.y};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) a += w[k + j] * k1[j];
+        h[r][k] = a;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < GR; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) a += h[r + i][k] * k1[i];
+        out[r][k][c] = a;
+      }
+  }
+#pragma unroll
+  for (int r = 0; r < GR; ++r) {
+    const int y = y0 + r;
+    if (y >= H) break;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      T o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] = from_f<T>(c < 3 ? out[r][k][c < 3 ? c : 0] : 0.f);
+      store_vec8(Y + (((long)b * H + y) * W + x0 + k) * 8, o);
+    }
+  }
+}
+
+
 // ---- bilinear resize, align_corners=False, no antialias (F.interpolate semantics) ----------
 __device__ __forceinline__ void src_index(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
   const float scale = (float)in / (float)out;
@@ -737,6 +808,13 @@ extern "C" int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int 
   if (B == 0) return SVK_OK;
   const int nstrip = (H + GR - 1) / GR;
   const long n = (long)B * nstrip * W;   // one thread per (column, strip of GR rows)
+  if (W % 4 == 0 && W >= 8 && C <= 3 && Cpad == 8 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0) {
+    SVK_DISPATCH_DTYPE(dtype_out, T, {
+      hipLaunchKernelGGL((gauss5x5_x4_kernel<T>), grid1d(n / 4), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H,
+                         W, nstrip);
+      return check_launch("gauss5x5_reflect");
+    });
+  }
   SVK_DISPATCH_DTYPE(dtype_out, T, {
     if (C <= 3)
       hipLaunchKernelGGL((gauss5x5_kernel<T, 3>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W,
