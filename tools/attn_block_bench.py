@@ -41,6 +41,13 @@ def run(N, C):
              "attn": lambda: ops.attention(q, kv[:, :, :C], kv[:, :, C:], heads, 0.125),
              "proj": lambda: ops.gemm(o, wp, bp, residual=x),
              "ln2": lambda: ops.layernorm(y, g2, b2, 1e-6)}
+    if C == 64:
+        from svk import _lib
+        for rep in range(3):
+            for sel, what in ((0, "4 waves x 256 queries"), (4, "8 waves x 512 queries"), (5, "8 waves x 256 queries")):
+                _lib.load().svk_tune(b"ffn_diag", sel)
+                print(f"C=64 {what}: fused {timeit(fused):7.1f} us")
+        _lib.load().svk_tune(b"ffn_diag", 0)
     tf = timeit(fused)
     tp = {k: timeit(f) for k, f in parts.items()}
     print(f"C={C}: fused {tf:7.1f} us | unfused {sum(tp.values()):7.1f} us = " + " + ".join(f"{k} {v:.1f}" for k, v in tp.items()))
