@@ -44,7 +44,7 @@ def run(N, C):
     if C == 64:
         from svk import _lib
         for rep in range(3):
-            for sel, what in ((0, "4 waves x 256 queries"), (4, "8 waves x 512 queries"), (5, "8 waves x 256 queries")):
+            for sel, what in ((6, "4 waves x 256 queries"), (4, "8 waves x 512 queries"), (0, "8 waves x 256 queries")):
                 _lib.load().svk_tune(b"ffn_diag", sel)
                 print(f"C=64 {what}: fused {timeit(fused):7.1f} us")
         _lib.load().svk_tune(b"ffn_diag", 0)
