@@ -22,10 +22,16 @@ namespace pl {
 
 template <int C_>
 struct Cfg {
-  static constexpr int C = C_, C4 = C / 4, LD = C + 8, LD4 = 32 + 8, NW = 4;
+  static constexpr int C = C_, C4 = C / 4, LD = C + 8, NW = 4;
   static constexpr int JT = C4 / 16;             // f tiles (16 prompt channels each)
+  static constexpr int KSL = (C4 + 31) / 32;     // lightweight-GEMM k-steps (inputs zero-padded)
   static constexpr int KS2 = (JT + 1) / 2;       // shared-GEMM k-steps (two f tiles each, the last may be half)
+  static constexpr int LDW = 32 * (KSL > KS2 ? KSL : KS2) + 8;   // weight row stride (elements)
   static constexpr int CT = C / 16, RC = C / 32;
+  static constexpr bool PREF = C <= 128;         // prefetch the x tile into registers (register budget)
+  // dynamic LDS carve (bytes)
+  static constexpr int OWL = 0, OWS = OWL + C4 * LDW * 2, OP = OWS + C * LDW * 2, OE = OP + NW * 16 * LD * 2;
+  static constexpr int BYTES = OE + 4 * C * 4;
 };
 
 template <typename T, int C_>
@@ -37,20 +43,20 @@ __global__ __launch_bounds__(256) void prompt_ln(const T* __restrict__ S, const 
   typedef Cfg<C_> K;
   typedef v8_t<T> tx8;
   typedef v4_t<T> tx4;
-  constexpr int C = K::C, C4 = K::C4, LD = K::LD, LD4 = K::LD4, CT = K::CT, RC = K::RC, JT = K::JT;
-  __shared__ __attribute__((aligned(16))) T sWl[C4][LD4];      // [out j][in k], k zero-padded to 32
-  __shared__ __attribute__((aligned(16))) T sWs[C][LD4];       // [out n][in j], j zero-padded to 32
-  __shared__ __attribute__((aligned(16))) T sP[K::NW][16][LD];
-  __shared__ float sEp[4][C];                                  // bs, g1, b1 | bl (first C4)
+  constexpr int C = K::C, C4 = K::C4, LD = K::LD, LDW = K::LDW, CT = K::CT, RC = K::RC, JT = K::JT;
+  extern __shared__ __attribute__((aligned(16))) char smem_pl[];
+  T (*sWl)[LDW] = reinterpret_cast<T (*)[LDW]>(smem_pl + K::OWL);   // [out j][in k], k zero-padded
+  T (*sWs)[LDW] = reinterpret_cast<T (*)[LDW]>(smem_pl + K::OWS);   // [out n][in j], j zero-padded
+  float (*sEp)[C] = reinterpret_cast<float (*)[C]>(smem_pl + K::OE);  // bs, g1, b1 | bl (first C4)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c = lane & 15;
   const T zero = (T)0.f;
-  for (int e = tid; e < C4 * 32; e += 256) {
-    const int j = e / 32, k = e % 32;
+  for (int e = tid; e < C4 * (LDW - 8); e += 256) {
+    const int j = e / (LDW - 8), k = e % (LDW - 8);
     sWl[j][k] = k < C4 ? Wl[j * C4 + k] : zero;
   }
-  for (int e = tid; e < C * 32; e += 256) {
-    const int n = e / 32, j = e % 32;
+  for (int e = tid; e < C * (LDW - 8); e += 256) {
+    const int n = e / (LDW - 8), j = e % (LDW - 8);
     sWs[n][j] = j < C4 ? Ws[n * C4 + j] : zero;
   }
   for (int e = tid; e < 4 * C; e += 256) {
@@ -58,7 +64,7 @@ __global__ __launch_bounds__(256) void prompt_ln(const T* __restrict__ S, const 
     sEp[w][d] = w == 0 ? (bs ? bs[d] : 0.f) : (w == 1 ? g1[d] : (w == 2 ? b1[d] : (d < C4 && bl ? bl[d] : 0.f)));
   }
   __syncthreads();
-  T (*patch)[LD] = sP[wave];
+  T (*patch)[LD] = reinterpret_cast<T (*)[LD]>(smem_pl + K::OP + wave * 16 * LD * 2);
   auto wave_sync = []() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -67,27 +73,34 @@ __global__ __launch_bounds__(256) void prompt_ln(const T* __restrict__ S, const 
   const int ntile = (M + 15) / 16;
   for (int tile = blockIdx.x * K::NW + wave; tile < ntile; tile += gridDim.x * K::NW) {
     const int t0 = tile * 16;
-    tx8 xr[RC];
+    tx8 xr[K::PREF ? RC : 1];
+    if constexpr (K::PREF) {
 #pragma unroll
-    for (int k = 0; k < RC; ++k) {
-      const int e = lane + 64 * k, row = e / (C / 8);
-      xr[k] = *reinterpret_cast<const tx8*>(X + (long)min(t0 + row, M - 1) * C + (e % (C / 8)) * 8);
+      for (int k = 0; k < RC; ++k) {
+        const int e = lane + 64 * k, row = e / (C / 8);
+        xr[k] = *reinterpret_cast<const tx8*>(X + (long)min(t0 + row, M - 1) * C + (e % (C / 8)) * 8);
+      }
     }
-    // ---- f^T = Wl . S^T (k = the C4 prompt inputs, padded to 32): lane gets f[token c][16 jt + 4 g + r]
-    tx8 sb;
+    // ---- f^T = Wl . S^T (k = the C4 prompt inputs, zero-padded): lane gets f[token c][16 jt + 4 g + r]
+    tx8 sb[K::KSL];
     {
       const int tr = min(t0 + c, M - 1);
-      if (8 * g < C4) sb = *reinterpret_cast<const tx8*>(S + (long)tr * C4 + 8 * g);
-      else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) sb[j] = zero;
+      for (int ks = 0; ks < K::KSL; ++ks) {
+        if (32 * ks + 8 * g < C4) sb[ks] = *reinterpret_cast<const tx8*>(S + (long)tr * C4 + 32 * ks + 8 * g);
+        else {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) sb[ks][j] = zero;
+        }
       }
     }
     float fv[JT][4];
 #pragma unroll
     for (int jt = 0; jt < JT; ++jt) {
-      const tx8 a = *reinterpret_cast<const tx8*>(&sWl[16 * jt + c][8 * g]);
-      const f32x4 acc = mfma16x16x32(a, sb, f32x4{0.f, 0.f, 0.f, 0.f});
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < K::KSL; ++ks)
+        acc = mfma16x16x32(*reinterpret_cast<const tx8*>(&sWl[16 * jt + c][32 * ks + 8 * g]), sb[ks], acc);
 #pragma unroll
       for (int r = 0; r < 4; ++r) fv[jt][r] = to_f(from_f<T>(gelu_fast(acc[r] + sEp[3][16 * jt + 4 * g + r])));   // as the 16-bit GEMM epilogue
     }
@@ -122,7 +135,10 @@ __global__ __launch_bounds__(256) void prompt_ln(const T* __restrict__ S, const 
 #pragma unroll
     for (int k = 0; k < RC; ++k) {
       const int e = lane + 64 * k;
-      *reinterpret_cast<tx8*>(&patch[e / (C / 8)][(e % (C / 8)) * 8]) = xr[k];
+      if constexpr (K::PREF) *reinterpret_cast<tx8*>(&patch[e / (C / 8)][(e % (C / 8)) * 8]) = xr[k];
+      else
+        *reinterpret_cast<tx8*>(&patch[e / (C / 8)][(e % (C / 8)) * 8]) =
+            *reinterpret_cast<const tx8*>(X + (long)min(t0 + e / (C / 8), M - 1) * C + (e % (C / 8)) * 8);
     }
     wave_sync();
     float yv[CT][4], sum = 0.f;
@@ -188,8 +204,8 @@ using namespace svk;
 extern "C" int svk_prompt_ln(int dtype, const void* S, const void* X, const void* Wl, const float* bl, const void* Ws,
                              const float* bs, const float* gamma1, const float* beta1, float eps, void* Xo, void* Ho,
                              int M, int C, void* stream) {
-  if (M < 0 || (C != 64 && C != 128) || !S || !X || !Wl || !Ws || !gamma1 || !beta1 || !Xo || !Ho) {
-    set_error("svk_prompt_ln: bad args (C=%d must be 64 or 128)", C); return SVK_EINVAL;
+  if (M < 0 || (C != 64 && C != 128 && C != 320) || !S || !X || !Wl || !Ws || !gamma1 || !beta1 || !Xo || !Ho) {
+    set_error("svk_prompt_ln: bad args (C=%d must be 64, 128 or 320)", C); return SVK_EINVAL;
   }
   if ((((uintptr_t)S) | ((uintptr_t)X) | ((uintptr_t)Xo) | ((uintptr_t)Ho)) & 15) {
     set_error("svk_prompt_ln: S / X / outputs must be 16-byte aligned"); return SVK_EINVAL;
@@ -206,13 +222,22 @@ extern "C" int svk_prompt_ln(int dtype, const void* S, const void* X, const void
   const int grid = (int)std::min<long>((ntile + 3) / 4, (long)cus * 8);
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
-    if (C == 64)
-      hipLaunchKernelGGL((pl::prompt_ln<T, 64>), dim3(grid), dim3(256), 0, st, (const T*)S, (const T*)X, (const T*)Wl, bl,
-                         (const T*)Ws, bs, gamma1, beta1, eps, (T*)Xo, (T*)Ho, M);
-    else
-      hipLaunchKernelGGL((pl::prompt_ln<T, 128>), dim3(grid), dim3(256), 0, st, (const T*)S, (const T*)X, (const T*)Wl, bl,
-                         (const T*)Ws, bs, gamma1, beta1, eps, (T*)Xo, (T*)Ho, M);
-    set_last_kernel(C == 64 ? "prompt_ln<64>" : "prompt_ln<128>");
+    auto go = [&](auto c_c) {
+      constexpr int CC = decltype(c_c)::value;
+      constexpr int LDS = pl::Cfg<CC>::BYTES;
+      static bool attr = false;
+      if (!attr && LDS > 65536) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&pl::prompt_ln<T, CC>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+        attr = true;
+      }
+      hipLaunchKernelGGL((pl::prompt_ln<T, CC>), dim3(grid), dim3(256), LDS, st, (const T*)S, (const T*)X,
+                         (const T*)Wl, bl, (const T*)Ws, bs, gamma1, beta1, eps, (T*)Xo, (T*)Ho, M);
+    };
+    if (C == 64) go(std::integral_constant<int, 64>{});
+    else if (C == 128) go(std::integral_constant<int, 128>{});
+    else go(std::integral_constant<int, 320>{});
+    set_last_kernel(C == 64 ? "prompt_ln<64>" : (C == 128 ? "prompt_ln<128>" : "prompt_ln<320>"));
     return check_launch("prompt_ln");
   });
 }

@@ -340,11 +340,11 @@ class PromptGenerator(nn.Module):
         return ops.gemm(feat, ps["w"], ps["b"], residual=x)
 
     def get_prompt_ln(self, x, prompt, block_num, depth_num, norm):
-        """(get_prompt(...), norm(get_prompt(...))) in one kernel for C in {64, 128} at 16 bits
+        """(get_prompt(...), norm(get_prompt(...))) in one kernel for the stages 1-3 widths at 16 bits
         (svk_prompt_ln); None when not covered."""
         summed = getattr(prompt, "summed", None)
         C = x.shape[-1]
-        if (not ops.FUSED_PROMPT_LN or summed is None or x.dtype not in ops.H16 or C not in (64, 128)
+        if (not ops.FUSED_PROMPT_LN or summed is None or x.dtype not in ops.H16 or C not in ops.PROMPT_LN_C
                 or summed.shape[-1] != C // 4):
             return None
         lw = getattr(self, f"lightweight_mlp{block_num}_{depth_num}")[0]

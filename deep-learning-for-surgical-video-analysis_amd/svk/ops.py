@@ -264,6 +264,9 @@ def mixffn_supported(W, C):
 
 FUSED_ATTN_BLOCK = os.environ.get("SVK_FUSED_ATTN_BLOCK", "1") == "1"
 FUSED_PROMPT_LN = os.environ.get("SVK_FUSED_PROMPT_LN", "1") == "1"
+# C = 320 (stage 3) is available but off: at 256 VGPRs and 130 KB of LDS it runs one wave per SIMD and
+# cost 11 % of the whole step in a same-box A/B
+PROMPT_LN_C = tuple(int(c) for c in os.environ.get("SVK_PROMPT_LN_C", "64,128").split(",") if c)
 
 
 def attn_block(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
@@ -293,7 +296,7 @@ def attn_block(hn, x, kv, wq, bq, wp, bp, gamma2, beta2, eps, scale):
 
 
 def prompt_ln(x, summed, wl, bl, ws, bs, gamma1, beta1, eps):
-    """(x + shared(GELU(light(summed))), norm1 of that) in one kernel (svk_prompt_ln; C in {64, 128}):
+    """(x + shared(GELU(light(summed))), norm1 of that) in one kernel (svk_prompt_ln; C in {64, 128, 320}):
     x [B, N, C], summed [B, N, C // 4] contiguous bf16 / f16 -> (x', h)."""
     if x.dtype not in H16:
         raise _lib.SvkError("svk.prompt_ln: bf16 / f16 only")

@@ -147,7 +147,7 @@ int svk_mstcn_layer(const float* X, const float* WdT, const float* bd, const flo
                     const float* b1, float* Y, int T, int F, int dilation, int causal, void* stream);
 
 /* Prompt adapter + norm1 of a MiT Block in one kernel (mix_transformer_evp.py:776-815 get_prompt, then
- * Block.norm1), C in {64, 128} (stages 1-2), prompt width C4 = C / 4, bf16 / f16:
+ * Block.norm1), C in {64, 128, 320} (stages 1-3), prompt width C4 = C / 4, bf16 / f16:
  * Xo = X + GELU(S Wl^T + bl) Ws^T + bs, Ho = LayerNorm(Xo; gamma1, beta1, eps).  S [M, C4], X / Xo / Ho [M, C]
  * contiguous; Wl [C4, C4], Ws [C, C4] (nn.Linear); bl / bs may be NULL. */
 int svk_prompt_ln(int dtype, const void* S, const void* X, const void* Wl, const float* bl, const void* Ws,

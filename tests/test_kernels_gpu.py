@@ -546,7 +546,8 @@ def test_attn_block_vs_unfused(cuda, dt, B, N, Nk, C):
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])
-@pytest.mark.parametrize("M,C", [(2 * 3136, 64), (1000, 64), (17, 64), (2 * 784, 128), (33, 128)])
+@pytest.mark.parametrize("M,C", [(2 * 3136, 64), (1000, 64), (17, 64), (2 * 784, 128), (33, 128), (3 * 196, 320),
+                                 (21, 320)])
 def test_prompt_ln_vs_unfused(cuda, dt, M, C):
     """Prompt adapter + norm1 in one kernel == the unfused chain (lightweight GEMM + GELU, shared GEMM +
     residual, LayerNorm) within two storage ulps."""
