@@ -24,7 +24,7 @@
 
 namespace svk {
 
-constexpr int MB_TC = 32;      // time steps per chunk (LDS ~57 KB at d_state 64: 2 workgroups per CU)
+constexpr int MB_TC = 16;      // time steps per chunk (LDS ~29 KB at d_state 64: 5 workgroups per CU; sweep: 32 steps (57 KB, 2 per CU) 5.69 M, 16: 6.41 M, 8: 5.66 M frames/s ragged)
 constexpr int MB_RMAX = 16;    // dt_rank <= 16 (d_model <= 256)
 
 __global__ __launch_bounds__(256) void mamba_conv_silu_kernel(const float* __restrict__ X, long ldx,
