@@ -44,24 +44,20 @@ __device__ __forceinline__ f32x2 pair(const Vec8<T>& v, int j) {
   }
 }
 
-// Packed-f32 GELU (erf form, erf_fast: |err| <= 1.5e-7): the FMAs/MULs issue as v_pk_*_f32 (two
-// elements per instruction), only rcp/exp are per element.
-__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) {
-  const f32x2 z = x * 0.70710678118654752f;
-  const f32x2 az = f32x2{fabsf(z.x), fabsf(z.y)};
-  const f32x2 d = az * 0.3275911f + 1.0f;
-  const f32x2 t = f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
-  f32x2 p = t * 1.061405429f - 1.453152027f;
-  p = p * t + 1.421413741f;
-  p = p * t - 0.284496736f;
-  p = p * t + 0.254829592f;
-  const f32x2 q = az * (az * -1.4426950408889634f);        // -z^2 * log2(e)
-  const f32x2 e = f32x2{__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-  const f32x2 y = 1.0f - (p * t) * e;
-  const f32x2 erf = f32x2{copysignf(y.x, z.x), copysignf(y.y, z.y)};
-  const f32x2 h = x * 0.5f;
-  return h * erf + h;
+// GELU (erf form, the A&S 7.1.26 erfc of erf_fast: |err| <= 1.5e-7), rearranged branch- and select-free as
+// relu(x) - 0.5 |x| t p(t) exp(-x^2 / 2): 11 VALU + 2 transcendental per element (the packed-f32 form
+// compiles to scalar ops in this build; same-box A/B +0.35 % on the extraction step)
+__device__ __forceinline__ float gelu_rl(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
+  float q = fmaf(-0.5f * 1.061405429f, t, -0.5f * -1.453152027f);
+  q = fmaf(q, t, -0.5f * 1.421413741f);
+  q = fmaf(q, t, -0.5f * -0.284496736f);
+  q = fmaf(q, t, -0.5f * 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);   // exp(-x^2 / 2)
+  return fmaf(ax * t * q, e, fmaxf(x, 0.f));
 }
+__device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) { return f32x2{gelu_rl(x.x), gelu_rl(x.y)}; }
 
 template <typename T, int R>
 __global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, const float* __restrict__ w,
