@@ -111,8 +111,54 @@ def video_lengths(n=40, seed=0):
 
 
 # ---------------------------------------------------------------------------------------------
+def host_cpus():
+    """The host cores the CPU baseline may use, stated the way SURVEY.md §8(d) asks: the CPUs in this
+    process's affinity mask (os.sched_getaffinity), the distinct physical cores behind them
+    (/proc/cpuinfo physical id + core id), and the cgroup CPU quota (/sys/fs/cgroup/cpu.max) and the job's CPU share (OMP_NUM_THREADS: the GPU box gives a one-GPU job
+    16 of its host CPUs).  The baseline runs one thread per usable physical core."""
+    aff = sorted(os.sched_getaffinity(0))
+    phys, cur = {}, {}
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if ":" not in line:
+                    if "processor" in cur:
+                        phys[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                    cur = {}
+                    continue
+                k, v = (t.strip() for t in line.split(":", 1))
+                cur[k] = v
+        if "processor" in cur:
+            phys[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+    except OSError:
+        pass
+    cores = len({phys[c] for c in aff if c in phys}) or len(aff)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, period = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    usable = min(cores, quota) if quota else cores
+    # the GPU box states the job's CPU share in OMP_NUM_THREADS (16 per GPU): never oversubscribe it
+    share = int(os.environ["OMP_NUM_THREADS"]) if os.environ.get("OMP_NUM_THREADS", "").isdigit() else None
+    if share:
+        usable = min(usable, share)
+    return {"affinity_cpus": len(aff), "physical_cores": cores, "cgroup_cpu_quota": quota, "job_cpu_share": share,
+            "threads": usable}
+
+
+def _cpu_threads():
+    info = host_cpus()
+    torch.set_num_threads(info["threads"])
+    return info
+
+
 def cpu_baseline_extract(variant, budget_s, batch=4):
     """Oracle (torch CPU, fp32, the reference's op order) on a bounded sample of the same workload."""
+    host = _cpu_threads()
     from oracle import inputs as I, params as P, mit_evp as M, shapes as SH
     sd = P.make_state_dict(SH.mit_evp_shapes(variant), 0)
     x, y, fl = I.frames(batch, 1), I.segmaps(batch, 1), I.flow(batch, 1)
@@ -123,11 +169,12 @@ def cpu_baseline_extract(variant, budget_s, batch=4):
             M.forward(x, y, sd, variant, fl, return_features=True)
             n += 1
         dt = time.perf_counter() - t0
-    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": torch.get_num_threads(), "host_cpus": host, "kind": "port",
             "sample": f"{n} batches x {batch} frames ({variant} + flow, fp32, return_features) in {dt:.1f} s"}
 
 
 def cpu_baseline_mstcn(budget_s, T=2456):
+    host = _cpu_threads()
     from oracle import params as P, mstcn as MS, shapes as SH, inputs as I
     sd = P.make_state_dict(SH.mstcn_shapes(4, 10, 64, 256, 14), 1)
     x = I.lfb(T, 256, 7).transpose(2, 1)
@@ -138,11 +185,12 @@ def cpu_baseline_mstcn(budget_s, T=2456):
             MS.multi_stage_s(x, sd, 4, 10, True)
             n += 1
         dt = time.perf_counter() - t0
-    return {"value": round(n * T / dt, 1), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+    return {"value": round(n * T / dt, 1), "unit": "frames/s", "cores": torch.get_num_threads(), "host_cpus": host, "kind": "port",
             "sample": f"{n} videos x {T} frames (MultiStageModel_S(4,10,64,256,14,causal), fp32) in {dt:.1f} s"}
 
 
 def cpu_baseline_mamba(budget_s, T=2456):
+    host = _cpu_threads()
     from oracle import mamba as OM, inputs as I
     sd = OM.init_state_dict(OM.mamba_shapes(256, 64, 10, 14), 1)
     x = I.lfb(T, 256, 7).transpose(2, 1)
@@ -152,7 +200,7 @@ def cpu_baseline_mamba(budget_s, T=2456):
             OM.causal_mamba(x, sd, 10, dtype=torch.float32)
             n += 1
         dt = time.perf_counter() - t0
-    return {"value": round(n * T / dt, 1), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+    return {"value": round(n * T / dt, 1), "unit": "frames/s", "cores": torch.get_num_threads(), "host_cpus": host, "kind": "port",
             "sample": f"{n} videos x {T} frames (CausalMambaModel(4,10,64,256,14), 10 Mamba blocks d_state 64, "
                       f"fp32 restatement of mamba_ssm's reference scan) in {dt:.1f} s"}
 
@@ -331,6 +379,7 @@ def workload_e2e(args, dev, rank, dtype):
 
 def cpu_baseline_train(variant, budget_s, batch=8):
     """Oracle train step (torch CPU autograd, fp32, train mode, SGD) on a bounded sample."""
+    host = _cpu_threads()
     from oracle import inputs as I, params as P, shapes as SH, train_evp as TR
     sd = P.make_state_dict(SH.mit_evp_shapes(variant), 0)
     x, y, fl = I.frames(batch, 1), I.segmaps(batch, 1), I.flow(batch, 1)
@@ -343,7 +392,7 @@ def cpu_baseline_train(variant, budget_s, batch=8):
         TR.sgd_step({k: sd[k] for k in grads}, grads)
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+    return {"value": round(n * batch / dt, 3), "unit": "frames/s", "cores": torch.get_num_threads(), "host_cpus": host, "kind": "port",
             "sample": f"{n} train steps x {batch} frames ({variant} + flow, fp32 autograd + SGD) in {dt:.1f} s"}
 
 
@@ -387,6 +436,7 @@ def workload_train(args, dev, rank, dtype):
 def cpu_baseline_tecno_train(kind, budget_s, T=1500):
     """Oracle train step (fp32 CPU autograd through the restatement, dropout draws, the tecno loss,
     clip_grad_norm_ + AdamW) on one video of T frames, repeated within the budget."""
+    host = _cpu_threads()
     from oracle import params as P, mstcn as MS, mamba as OM, inputs as I, shapes as SH
     if kind == "mstcn":
         sd = P.make_state_dict(SH.mstcn_shapes(4, 10, 64, 256, 14), 1)
@@ -414,7 +464,7 @@ def cpu_baseline_tecno_train(kind, budget_s, T=1500):
         opt.step()
         n += 1
     dt = time.perf_counter() - t0
-    return {"value": round(n * T / dt, 2), "unit": "frames/s", "cores": torch.get_num_threads(), "kind": "port",
+    return {"value": round(n * T / dt, 2), "unit": "frames/s", "cores": torch.get_num_threads(), "host_cpus": host, "kind": "port",
             "sample": f"{n} optimizer steps on one {T}-frame video ({kind}, fp32 autograd through the oracle "
                       f"restatement + AdamW) in {dt:.1f} s"}
 
@@ -475,14 +525,45 @@ WORKLOADS = {"extract": workload_extract, "mstcn": workload_mstcn, "mamba": work
              "tecno_train": workload_tecno_train}
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def count_visible_gpus(topology=None, env=None):
+    """GPUs this process may use, counted WITHOUT any HIP call (so the launcher parent never
+    initialises the runtime before it spawns the ranks): the KFD topology's GPU nodes (a node with
+    SIMDs), narrowed by ROCR_VISIBLE_DEVICES and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES the
+    way the ROCm runtime applies them (the HIP list indexes into what ROCR left visible)."""
+    env = os.environ if env is None else env
+    topology = KFD_TOPOLOGY if topology is None else topology
+    n = 0
+    try:
+        for node in os.listdir(topology):
+            try:
+                with open(os.path.join(topology, node, "properties")) as f:
+                    props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        val = env.get(var)
+        if val is None:
+            continue
+        ids = [t for t in val.split(",") if t.strip() != ""]
+        n = min(n, len(ids)) if not any(t.strip().startswith("-") for t in ids) else 0
+    return n
+
+
 def launch_ranks(args):
     """``--gpus N`` without a torchrun environment: start N ranks under torch.distributed.run (one
-    process per GPU, rendezvous on 127.0.0.1) as a CHILD process and return its exit code.  Nothing here
-    touches the GPU (device_count only counts devices).  Mismatches fail loudly instead of silently
-    measuring one rank."""
+    process per GPU, rendezvous on 127.0.0.1) as a CHILD process and return its exit code.  The GPU
+    count comes from the KFD topology (count_visible_gpus), so the parent makes no HIP call before the
+    spawn.  Mismatches fail loudly instead of silently measuring one rank."""
     world_env = os.environ.get("WORLD_SIZE")
     # the "plumbing" workload (launcher test, gloo on CPU) runs without GPUs
-    visible = args.gpus if args.workload == "plumbing" else torch.cuda.device_count()
+    visible = args.gpus if args.workload == "plumbing" else count_visible_gpus()
     if world_env is not None:
         if int(world_env) != args.gpus:
             sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}")

@@ -25,7 +25,7 @@
 // Synchronisation per K-step: issue DMA(next) -> s_waitcnt vmcnt(#DMA of next) (own DMA of the
 // current step landed) -> s_barrier (everyone's landed) -> fragment reads + MFMAs -> s_barrier
 // (nobody still reads the buffer the following step's DMA overwrites).  Raw s_barrier, never
-// __syncthreads (its fence would drain the in-flight DMA).
+// __syncthreads (its fence would drain the in-flight DMA).  Two stages: the DMA runs one step ahead.
 #include "svk_common.h"
 #include "gemm_args.h"
 #include <stdio.h>
@@ -56,7 +56,7 @@ struct PkCfg {
   // bf16 one and drop a workgroup per CU
   static constexpr int OCC = BM * BN <= 64 * 64 ? 5 : (BM * BN <= 128 * 64 ? 3 : 2);
   static_assert(A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "tile must split into whole DMA rounds");
-  static_assert(LD * (NSTAGE - 1) <= 63, "vmcnt range");
+  static_assert(LD <= 63, "vmcnt range");
 };
 
 // n / d for 0 <= n < 2^31 by multiply-high (d >= 1); host computes (mul, shr).
@@ -89,6 +89,11 @@ __device__ __forceinline__ void barrier_mem() { asm volatile("s_barrier" ::: "me
 // Epilogue operand loads hidden from hipcc's waitcnt pass (see epi_load): completion is covered by the
 // counted wait of the tile's last step.
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#ifdef SVK_PK_VISIBLE_EPI   // diagnostic build: compiler-visible epilogue loads
+__device__ __forceinline__ void gload16(f32x4& v, const char* src) { v = *reinterpret_cast<const f32x4*>(src); }
+__device__ __forceinline__ void gload8(u32x2& v, const char* src) { v = *reinterpret_cast<const u32x2*>(src); }
+__device__ __forceinline__ void gload4(float& v, const char* src) { v = *reinterpret_cast<const float*>(src); }
+#else
 __device__ __forceinline__ void gload16(f32x4& v, const char* src) {
   asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(src) : "memory");
 }
@@ -98,16 +103,7 @@ __device__ __forceinline__ void gload8(u32x2& v, const char* src) {
 __device__ __forceinline__ void gload4(float& v, const char* src) {
   asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(src) : "memory");
 }
-
-template <int LD>
-__device__ __forceinline__ void wait_dma(int pend) {   // own DMA of the current stage landed
-  switch (pend) {
-    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LD) : "memory"); break;
-    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LD) : "memory"); break;
-    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * LD) : "memory"); break;
-  }
-}
+#endif
 
 // SPLIT: split-K — unit u = (tile u / ks, K part u % ks) covers nk K-steps of the tile's ks * nk; the
 // epilogue stores raw f32 partial sums to slab part (p.slab + (part * M + m) * N + n) and a separate
@@ -355,32 +351,42 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
-  // DMA issue cursor: the (tile, K-step) stream of this workgroup, up to NSTAGE steps in flight
-  // (the current one included); `inflight` counts issued steps not yet computed.
-  int itile = first, ikt = 0, ibuf = 0, inflight = 0, buf = 0;
+  // DMA issue cursor: the (tile, K-step) stream of this workgroup.  Every step issues exactly LD
+  // LDS-DMA instructions — the next (tile, K-step)'s, or, past the last one, LD copies of the zero block
+  // into the stage buffer nobody reads any more — so the wait for the stage a step computes is ONE
+  // unconditional counted `s_waitcnt vmcnt(LD)` (only the step just issued may stay in flight): no
+  // data-dependent branch around the wait, and every operation older than that step (the epilogue
+  // loads included) has provably landed once it returns (csrc/isa_check.py audits this on the built
+  // code object).
+  static_assert(NS == 2, "the counted waits assume a two-stage ring: one step in flight beyond the current");
+  int itile = first, ikt = 0, ibuf = 0, buf = 0;
   auto issue_next = [&]() {
-    if (itile >= ntiles) return;
-    issue(itile, ikt, ibuf);
-    ++inflight;
-    ibuf = ibuf + 1 == NS ? 0 : ibuf + 1;
-    if (++ikt == nk) { ikt = 0; itile += G; }
+    if (itile < ntiles) {
+      issue(itile, ikt, ibuf);
+      if (++ikt == nk) { ikt = 0; itile += G; }
+    } else {
+      const uint32_t sa = lds0 + ibuf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
+#pragma unroll
+      for (int i = 0; i < Cfg::A_LD; ++i) dma16(zero, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
+#pragma unroll
+      for (int i = 0; i < Cfg::B_LD; ++i) dma16(zero, __builtin_amdgcn_readfirstlane(sb + (wave * Cfg::B_LD + i) * 1024));
+    }
+    ibuf ^= 1;
   };
   // One pipeline step: top up the DMA ring (into the stage computed one step ago), wait for the
   // oldest stage `buf`, compute from it.
   auto step = [&](bool last) {
     issue_next();
-    wait_dma<Cfg::LD>(inflight - 1);   // steps in flight beyond the current one may stay outstanding
-    if (last) tie_epi();               // the epilogue loads (older than the prefetch) have landed too
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::LD) : "memory");   // all but the step just issued
+    if (last) tie_epi();               // the epilogue loads (older than that step) have landed too
     barrier_mem();
     compute(buf);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_mem();                     // nobody still reads `buf` when a later DMA overwrites it
-    --inflight;
     stile = smem + buf * Cfg::STAGE;
-    buf = buf + 1 == NS ? 0 : buf + 1;
+    buf ^= 1;
   };
-#pragma unroll
-  for (int s = 0; s < NS - 1; ++s) issue_next();
+  issue_next();
   for (int tile = first; tile < ntiles; tile += G) {
     for (int kt = 0; kt < nk - 1; ++kt) step(false);
     epi_load(tile);                   // epilogue operands fly during the last step's wait and MFMAs
@@ -392,6 +398,9 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       default: epilogue(tile, std::integral_constant<int, 0>{}); break;
     }
   }
+  // the last step's zero-block DMA is still in flight: retire it before the wave (and the workgroup's
+  // LDS allocation) ends
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // ---- host side -------------------------------------------------------------------------------

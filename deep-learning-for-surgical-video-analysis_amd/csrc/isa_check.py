@@ -1,0 +1,142 @@
+"""Build-time audit of the gfx950 code objects in the svk objects (run by the Makefile after linking).
+
+1. Packed-FP32 VALU ops.  On gfx950 a VALU write of a VGPR followed by a v_pk_*_f32 that reads it as the
+   LOW lane's source through op_sel (e.g. ``v_pk_add_f32 v[0:1], v[42:43], v[44:45] op_sel:[0,1]``) reads
+   stale data in lanes 48-63 while another wave of the same SIMD issues MFMAs; s_nop 1 does not cover it
+   and hipcc 7.2 inserts no wait (reproduced by tools/hazard/pk_hazard.hip: 1.5 % of lanes 48-63 wrong
+   under MFMA load, none without op_sel or without the load; it was the round-2 gemm_pk "stale epilogue
+   element").  The library is built without packed-FP32 ops; this check proves no such instruction
+   (v_pk_add/mul/fma_f32, or v_pk_mov_b32 with op_sel) reached the code objects.
+2. Epilogue operand loads of gemm_pk.  They are issued from inline asm so hipcc's waitcnt pass does not
+   drain the cross-tile LDS-DMA prefetch; their completion is covered by the counted vmcnt of the tile's
+   last K-step.  hipcc treats the destination VGPRs as written when the asm statement ends, so any
+   compiler instruction touching them before that wait would read or clobber in-flight data.  Every
+   VGPR-destination global_load in a gemm_pk kernel is followed, on EVERY control-flow path, by an
+   s_waitcnt with a vmcnt field before any instruction reads or writes its destination registers.
+Exit status 1 with a report on any violation."""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+TARGET = "hipv4-amdgcn-amd-amdhsa--gfx950"
+INS_RE = re.compile(r"^\s+([a-z_0-9]+)\s*(.*?)\s*//\s*([0-9A-F]+):")
+TGT_RE = re.compile(r"<([A-Za-z0-9_.$]+)\+0x([0-9a-f]+)>")
+SYM_RE = re.compile(r"^([0-9a-f]+) <([^>]+)>:")
+
+
+def regs(tok):
+    tok = tok.strip()
+    m = re.match(r"v\[(\d+):(\d+)\]", tok)
+    if m:
+        return set(range(int(m.group(1)), int(m.group(2)) + 1))
+    m = re.match(r"v(\d+)$", tok)
+    return {int(m.group(1))} if m else set()
+
+
+def disasm(obj):
+    with tempfile.TemporaryDirectory() as d:
+        fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "g.co")
+        r = subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", obj,
+                            os.path.join(d, "o")], capture_output=True)
+        if r.returncode != 0 or not os.path.exists(fat):
+            return ""                                          # host-only object: no device code
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--targets={TARGET}",
+                        f"--input={fat}", f"--output={co}"], check=True, capture_output=True)
+        return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
+                              capture_output=True, text=True).stdout
+
+
+def functions(text):
+    """{symbol: [(addr, op, operands, branch_target_addr_or_None)]}"""
+    funcs, cur, base = {}, None, 0
+    for line in text.split("\n"):
+        m = SYM_RE.match(line)
+        if m:
+            cur, base = m.group(2), int(m.group(1), 16)
+            funcs[cur] = []
+            continue
+        m = INS_RE.match(line)
+        if m and cur is not None:
+            t = TGT_RE.search(line)
+            tgt = base + int(t.group(2), 16) if (t and t.group(1) == cur) else None
+            funcs[cur].append((int(m.group(3), 16), m.group(1), m.group(2), tgt))
+    return funcs
+
+
+def operands(s):
+    parts = [p.strip() for p in s.split(",")]
+    return [p.split()[0] for p in parts if p]
+
+
+def check_packed(funcs):
+    bad = []
+    for f, ins in funcs.items():
+        for addr, op, ops, _ in ins:
+            if re.match(r"v_pk_(add|mul|fma)_f32", op) or (op == "v_pk_mov_b32" and "op_sel" in ops):
+                bad.append(f"{f}+0x{addr:x}: {op} {ops}")
+    return bad
+
+
+def check_epilogue_loads(funcs):
+    bad = []
+    for f, ins in funcs.items():
+        if "gemm_pk" not in f:
+            continue
+        at = {a: k for k, (a, *_rest) in enumerate(ins)}
+        for k, (addr, op, ops, _) in enumerate(ins):
+            if not re.match(r"global_load_dword(x2|x4)?$", op):
+                continue
+            dst = regs(operands(ops)[0])
+            seen, stack = {}, [(k + 1, None)]
+            while stack:
+                j, prev = stack.pop()
+                if j in seen or j >= len(ins):
+                    continue
+                seen[j] = prev
+                a2, op2, ops2, tgt = ins[j]
+                if op2 == "s_waitcnt" and "vmcnt" in ops2:
+                    continue                                  # covered on this path
+                touched = set()
+                for o in operands(ops2):
+                    touched |= regs(o)
+                if op2.startswith(("v_", "global_", "ds_", "buffer_", "flat_")) and touched & dst:
+                    path, q = [], prev
+                    while q is not None and len(path) < 400:
+                        path.append(q)
+                        q = seen.get(q)
+                    jumps = [f"0x{ins[q][0]:x}" for q in reversed(path) if ins[q][1].startswith(("s_branch", "s_cbranch"))]
+                    bad.append(f"{f}+0x{addr:x}: {op} {ops} -> touched at +0x{a2:x}: {op2} {ops2} (via {jumps[:12]})")
+                    continue
+                if op2 == "s_endpgm":
+                    continue
+                if op2 == "s_branch":
+                    stack.append((at.get(tgt, len(ins)), j))
+                    continue
+                if op2.startswith("s_cbranch") and tgt is not None:
+                    stack.append((at.get(tgt, len(ins)), j))
+                stack.append((j + 1, j))
+    return bad
+
+
+def main(objs):
+    fails = 0
+    nload = 0
+    for obj in objs:
+        funcs = functions(disasm(obj))
+        for msg in check_packed(funcs):
+            print(f"isa_check: {os.path.basename(obj)}: packed-FP32 op_sel hazard class: {msg}")
+            fails += 1
+        for msg in check_epilogue_loads(funcs):
+            print(f"isa_check: {os.path.basename(obj)}: epilogue load register touched before its wait: {msg}")
+            fails += 1
+        nload += sum(1 for f, ins in funcs.items() if "gemm_pk" in f for _, op, _, _ in ins
+                     if re.match(r"global_load_dword(x2|x4)?$", op))
+    print(f"isa_check: {len(objs)} objects, {nload} gemm_pk epilogue loads audited, {fails} violation(s)")
+    return 1 if fails else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1:]))

@@ -40,9 +40,7 @@ def generate_anticipation_gt_onephase(phase_code, horizon):
 def plot_phase_anticipation(save_path, phase_gt, phase_pred=None):
     """One subplot per phase: ground truth (red) and optional prediction (blue) over frames, y ticks
     0 / 0.5 / >1, saved at 120 dpi (generate_phase_anticipation.py:37-52).  Host-side plotting."""
-    import matplotlib
-    matplotlib.use("Agg")
-    import matplotlib.pyplot as plt
+    import matplotlib.pyplot as plt        # the caller's backend, as the reference (no backend switch)
 
     def host(a):
         return a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else a

@@ -23,6 +23,7 @@ import torch.nn as nn
 from svk import ops
 from svk.pack import get_packed, lin_w, lin_b, conv_w, fold_bn, pad_channels
 from visualizer import get_local
+import svk
 from ._common import pair, compute_dtype, check_inference, to_nhwc, DropPath
 from .segformer_head import SegFormerHead
 
@@ -545,7 +546,15 @@ class MixVisionTransformerEVP(nn.Module):
         return [t.view(t.shape[0], H, W, -1).permute(0, 3, 1, 2) for t, H, W in self._stages(x, y)]
 
     def forward(self, x, y, flow=None, return_features=False):
-        """(mix_transformer_evp.py:418-449): features [B, 2048] if return_features else (y [B, 7], y_ant [B, 7])."""
+        """(mix_transformer_evp.py:418-449): features [B, 2048] if return_features else (y [B, 7], y_ant [B, 7]).
+        Train mode (train_evp.py:473-515): one autograd node over the svk training kernels
+        (svk.train.EVPAutograd) returning (y, y_ant) f32; the backbone frozen as train_evp.py:379-382 does."""
+        if self.training:
+            if return_features:
+                raise svk.SvkError("MixVisionTransformerEVP: return_features in train mode is not part of the "
+                                   "reference's training loop (train_evp.py:495); call .eval() for extraction")
+            from svk.train import autograd_forward
+            return autograd_forward(self, x, y, flow, compute_dtype(self))
         check_inference(self, x, y, flow)
         outs = self._stages(x, y)
         if flow is not None:

@@ -5,6 +5,7 @@ output through the PyTorch caching allocator (the library never allocates) and
 launches on the current stream.  There is deliberately no CPU path: a CPU tensor
 is an error.
 """
+import collections
 import os
 
 import torch
@@ -468,7 +469,28 @@ def softmax_rows(x, out=None):
     return out
 
 
-_TILE_CACHE = {}
+class _LRU(collections.OrderedDict):
+    """Bounded table cache (the ragged tables were keyed by every distinct batch of video
+    lengths and never evicted, each entry holding device tensors)."""
+
+    def __init__(self, cap):
+        super().__init__()
+        self.cap = cap
+
+    def get(self, key, default=None):
+        if key in self:
+            self.move_to_end(key)
+            return self[key]
+        return default
+
+    def __setitem__(self, key, value):
+        super().__setitem__(key, value)
+        self.move_to_end(key)
+        while len(self) > self.cap:
+            self.popitem(last=False)
+
+
+_TILE_CACHE = _LRU(int(os.environ.get("SVK_TABLE_CACHE", "64")))
 
 
 def mstcn_tiles(lengths, device):
@@ -511,7 +533,7 @@ def mstcn_layer(x, wdT, bd, w1T, b1, dilation, causal, out=None, tiles=None):
     return out
 
 
-_MAMBA_RAGGED = {}
+_MAMBA_RAGGED = _LRU(int(os.environ.get("SVK_TABLE_CACHE", "64")))
 MAMBA_RAGGED_SEG = int(os.environ.get("SVK_MAMBA_RAGGED_SEG", "256"))
 
 

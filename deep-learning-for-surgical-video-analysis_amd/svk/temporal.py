@@ -19,6 +19,8 @@ CrossEntropy (phase) + SmoothL1 (anticipation), backward, clip_grad_norm_(1.0), 
 * the drop-in path: ``model.train(); y = model(x); loss.backward()`` in the reference's own loop runs
   the same forward/backward through one autograd Function per model (``autograd_forward``).
 """
+import collections
+
 import torch
 from torch.autograd.graph import increment_version
 
@@ -263,7 +265,7 @@ class MambaTrainer(_TrainerBase):
         P = self.fl.P
         BT = B * T
         Fm, Di, N, R, K = self.Fm, self.Di, self.N, self.R, self.K
-        self._x = x
+        ws.bufs["x_in"] = x                       # per-call: two forwards before their backwards stay apart
         h = ops.gemm(x, P("in_proj.weight"), P("in_proj.bias"), out=ws.get("h0", (BT, Fm)))
         for l in range(self.L):
             p = f"blocks.{l}."
@@ -312,9 +314,10 @@ class MambaTrainer(_TrainerBase):
             ops.gemm_wgrad(dxz, h_prev, G(p + "in_proj.weight"))
             dh = ops.gemm(dxz, pk[self.k_binT[l]], residual=do, out=ws.get(other, (BT, Fm)))
             other = "dh_a" if other == "dh_b" else "dh_b"
-        ops.gemm_wgrad(dh, self._x, G("in_proj.weight"), G("in_proj.bias"))
+        x_in = ws.bufs["x_in"]
+        ops.gemm_wgrad(dh, x_in, G("in_proj.weight"), G("in_proj.bias"))
         if need_dx:
-            return ops.gemm(dh, pk[self.k_inT], out=ws.get("dx", (BT, self._x.shape[1])))
+            return ops.gemm(dh, pk[self.k_inT], out=ws.get("dx", (BT, x_in.shape[1])))
         return None
 
 
@@ -409,7 +412,7 @@ class TemporalTrainStep:
     (``set_lr`` for ReduceLROnPlateau)."""
 
     def __init__(self, model, class_weights=None, lr=1e-4, weight_decay=1e-3, betas=(0.9, 0.999), eps=1e-8,
-                 grad_clip=1.0, seed=42, graphs=True):
+                 grad_clip=1.0, seed=42, graphs=True, max_graphs=64):
         model.train()
         self.tr = trainer_for(model)
         self.model = model
@@ -425,7 +428,11 @@ class TemporalTrainStep:
         self.cw = None if class_weights is None else torch.as_tensor(class_weights, dtype=torch.float32).to(self.dev)
         self.seed = int(seed)
         self.graphs = graphs
-        self._g = {}        # T -> (graph, ws, static inputs)
+        # T -> (graph, ws, static inputs): one captured graph per video length, each holding its own
+        # activation workspace (MS-TCN S(2L+1)TF f32 + masks, Mamba ~36 KB per frame at 10 blocks, i.e.
+        # ~0.2 GB for a 6000-frame video); least-recently-used lengths beyond max_graphs are dropped
+        self._g = collections.OrderedDict()
+        self.max_graphs = int(max_graphs)
 
     def set_lr(self, lr):
         self.lr.fill_(float(lr))
@@ -477,8 +484,11 @@ class TemporalTrainStep:
             with torch.cuda.graph(g):
                 self._body(sx, sl, sa, ws)
             self._g[T] = (g, ws, sx, sl, sa)
+            while len(self._g) > self.max_graphs:
+                self._g.popitem(last=False)
             self._bump()
             return self.loss
+        self._g.move_to_end(T)
         g, ws, sx, sl, sa = ent
         sx.copy_(x); sl.copy_(labels); sa.copy_(ant)
         g.replay()

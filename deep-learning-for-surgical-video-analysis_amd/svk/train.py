@@ -98,6 +98,7 @@ class EVPTrainStep:
         self.seed = seed
         self.group = process_group
         self.world = world_size
+        self._bn_flat = None
         self.steps = 0
         dev = next(model.parameters()).device
         if dev.type != "cuda":
@@ -114,11 +115,19 @@ class EVPTrainStep:
         self._pending = None
 
     # ---- parameter storage ------------------------------------------------------------------
+    BIND_GRADS = True        # .grad of each trainable parameter = a view into the flat gradient
+
     def _setup_flat(self):
         tr = []
         for n, p in self.model.named_parameters():
-            p.requires_grad_(is_trainable(n))
-            if p.requires_grad:
+            if self.BIND_GRADS:
+                p.requires_grad_(is_trainable(n))
+            elif p.requires_grad != is_trainable(n):
+                raise SvkError(
+                    "MixVisionTransformerEVP train mode on the svk kernels trains the reference's parameter set "
+                    "(train_evp.py:379-382: names containing head / prompt / flow_encoder / cross_attn_s3 / "
+                    f"cross_attn_s4, everything else frozen); parameter {n!r} has requires_grad={p.requires_grad}")
+            if is_trainable(n):
                 tr.append((n, p))
         total = sum(p.numel() for _, p in tr)
         self.flat = torch.empty(total, device=self.dev, dtype=torch.float32)
@@ -131,7 +140,8 @@ class EVPTrainStep:
                 k = p.numel()
                 self.flat[o:o + k].copy_(p.detach().reshape(-1))
                 p.data = self.flat[o:o + k].view_as(p)
-                p.grad = self.grad[o:o + k].view_as(p)
+                if self.BIND_GRADS:
+                    p.grad = self.grad[o:o + k].view_as(p)
                 self.off[n] = o
                 o += k
         self.params = dict(tr)
@@ -147,8 +157,10 @@ class EVPTrainStep:
         return self.params[name]
 
     def G(self, name):
-        """f32 gradient view of a trainable parameter."""
-        return self.params[name].grad
+        """f32 gradient view of a trainable parameter (into the flat gradient buffer)."""
+        p = self.params[name]
+        o = self.off[name]
+        return self.grad[o:o + p.numel()].view_as(p)
 
     # ---- packs --------------------------------------------------------------------------------
     def _setup_packs(self):
@@ -663,14 +675,27 @@ class EVPTrainStep:
             bn.num_batches_tracked.add_(1)
 
     def _broadcast_buffers(self):
+        """The five BatchNorms' running statistics from rank 0 as ONE collective: packed into a flat
+        buffer, broadcast, unpacked (was ten separate broadcasts per step)."""
         import torch.distributed as dist
         m = self.model
+        bufs = []
         for bn in [m.head.linear_fuse.bn] + [getattr(m.flow_encoder, f"bn{i}") for i in range(1, 5)]:
-            dist.broadcast(bn.running_mean, 0, group=self.group)
-            dist.broadcast(bn.running_var, 0, group=self.group)
+            bufs += [bn.running_mean, bn.running_var]
+        flat = getattr(self, "_bn_flat", None)
+        if flat is None:
+            flat = self._bn_flat = torch.empty(sum(b.numel() for b in bufs), device=bufs[0].device,
+                                               dtype=torch.float32)
+        torch.cat([b.reshape(-1).float() for b in bufs], out=flat)
+        dist.broadcast(flat, 0, group=self.group)
+        off = 0
+        for b in bufs:
+            b.copy_(flat[off:off + b.numel()].view_as(b))
+            off += b.numel()
 
     def _ddp(self):
-        return self.group is not None and self.world > 1
+        # a process group means DDP semantics at any world size (world 1 still runs the RCCL calls)
+        return self.group is not None
 
     def sync_buffers(self):
         """DDP's broadcast_buffers: BN running statistics from rank 0, once per step, before the forward
@@ -748,7 +773,7 @@ class EVPTrainStep:
         if self.steps == 0:
             raise SvkError("EVPTrainStep.capture: run one eager step first")
         self._static = (x, y, flow, labels, ant_targets)
-        ddp = self.group is not None and self.world > 1
+        ddp = self._ddp()
         bns = [self.model.head.linear_fuse.bn] + [getattr(self.model.flow_encoder, f"bn{i}") for i in range(1, 5)]
         saved = [(bn.running_mean.clone(), bn.running_var.clone(), bn.num_batches_tracked.clone()) for bn in bns]
         s = torch.cuda.Stream(device=self.dev)
@@ -795,3 +820,100 @@ class EVPTrainStep:
             self.graph_opt.replay()
         self._after_step()
         return self._gout
+
+
+# ---------------------------------------------------------------------------------------------------
+class EVPAutograd(EVPTrainStep):
+    """The train-mode ``MixVisionTransformerEVP.forward`` of the drop-in surface as ONE autograd node
+    over the same forward / backward kernels as EVPTrainStep, so the reference's own loop runs unchanged
+    (train_evp.py:473-515, finetune_evp.py:396/509): ``model.train()``, ``autocast(float16)`` forward ->
+    (y [B, 7], y_ant [B, 7]), torch criteria, ``scaler.scale(loss).backward()``, ``scaler.step(optimizer)``
+    with torch's own SGD over the reference's parameter groups.
+
+    * The trainable parameters are views into one flat f32 buffer (torch's optimizer updates them in
+      place); their ``.grad`` stay autograd's (the node returns one gradient per parameter; the freeze
+      rule of train_evp.py:379-382 is checked, not imposed).  Parameter updates are seen through the
+      version counters: the compute-dtype weight packs are re-derived before the next forward, and a
+      change to a frozen backbone parameter rebuilds the trainer.
+    * Compute dtype = the autocast region's (svk.default_dtype(): f16 under autocast(float16), as the
+      reference trains) or ``model.svk_dtype``; f32 outside autocast.
+    * Train-mode semantics as EVPTrainStep: DropPath / Dropout2d masks from the device counter (a new
+      draw every forward), BatchNorm batch statistics with the running-stat update in the forward.
+    * Each forward keeps its own saved activations in the node (several forwards before a backward —
+      gradient accumulation — are independent)."""
+
+    BIND_GRADS = False
+
+    def __init__(self, model, dtype):
+        super().__init__(model, dtype=dtype, drop=True, seed=0)
+        self.names = list(self.params)
+        self._snap()
+
+    def _snap(self):
+        self._ver_tr = [self.params[n]._version for n in self.names]
+        self._ver_fz = [p._version for n, p in self.model.named_parameters() if not is_trainable(n)]
+
+    def frozen_changed(self):
+        return [p._version for n, p in self.model.named_parameters() if not is_trainable(n)] != self._ver_fz
+
+    def ensure_fresh(self):
+        if [self.params[n]._version for n in self.names] != self._ver_tr:
+            self._refresh_packs()
+            self._snap()
+
+    def forward_saved(self, x, y, flow):
+        B = x.numel() // (3 * 224 * 224)
+        masks = self.make_masks(B)
+        self.counter.add_(1)                         # fresh DropPath / Dropout2d draws next forward
+        sv, logits, ant = self._forward(x, y, flow, masks)
+        self._update_bn_running(sv)                  # nn.BatchNorm2d updates its running stats in forward
+        return sv, logits, ant
+
+    def backward_grads(self, sv, dlogits, dant):
+        self.grad.zero_()
+        self.conv_scratch.zero_()
+        self._backward_rest(sv, self._backward_head(sv, dlogits, dant))
+        self.untab.run(self.conv_scratch, self.grad)
+        return [self.grad[self.off[n]:self.off[n] + self.params[n].numel()].view_as(self.params[n]).clone()
+                for n in self.names]
+
+
+class _EVPFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, tr, x, y, flow, *params):
+        sv, logits, ant = tr.forward_saved(x, y, flow)
+        ctx.tr, ctx.sv = tr, sv
+        ctx.shape = tuple(logits.shape)
+        return logits, ant
+
+    @staticmethod
+    @torch.autograd.function.once_differentiable
+    def backward(ctx, g_logits, g_ant):
+        tr, sv = ctx.tr, ctx.sv
+        ctx.sv = None
+        z = lambda g: (torch.zeros(ctx.shape, device=tr.dev, dtype=torch.float32) if g is None
+                       else g.float().contiguous())
+        grads = tr.backward_grads(sv, z(g_logits), z(g_ant))
+        return (None, None, None, None) + tuple(grads)
+
+
+def evp_trainer(model, dtype):
+    t = model.__dict__.get("_svk_evp_autograd")
+    if t is None or t.dt != dtype or t.frozen_changed():
+        t = EVPAutograd(model, dtype)
+        model.__dict__["_svk_evp_autograd"] = t
+    return t
+
+
+def autograd_forward(model, x, y, flow, dtype):
+    """Train-mode MixVisionTransformerEVP.forward(x, y, flow) -> (y [B, 7], y_ant [B, 7]) f32, one autograd
+    node (EVPAutograd)."""
+    for t in (x, y, flow):
+        if t is None:
+            raise SvkError("MixVisionTransformerEVP train mode: the svk path trains with the optical-flow input "
+                           "(train_evp.py:495 always passes it)")
+        if not t.is_cuda:
+            raise SvkError(f"MixVisionTransformerEVP: inputs must be on the GPU (got {t.device}); there is no CPU path")
+    tr = evp_trainer(model, dtype)
+    tr.ensure_fresh()
+    return _EVPFn.apply(tr, x, y, flow, *[tr.params[n] for n in tr.names])

@@ -143,3 +143,59 @@ def test_graphed_forward_matches_eager_and_recaptures(cuda):
         assert gf.graph is not g0
         m.svk_dtype = torch.float32
         torch.testing.assert_close(gf().clone(), m(x, y, fl, return_features=True), rtol=0, atol=0)
+
+
+def _config5_chain(cuda, b256, dtype):
+    """MiT-b2 + flow features at ``dtype`` -> MultiStageModel_S(2, 8, 32, 2048, 14, causal) ->
+    Transformer(32, 2048, 14, 30).original_forward on the 256-frame chunk (trans_SV_output.py:276-291),
+    and the fp32 oracle chain on the same inputs."""
+    from models import mstcn, adapter_transformer, mix_transformer_evp as mte
+    from oracle import mstcn as MS, trans_sv as TS
+    sd, (x, y, fl), feat, _, _ = b256
+    tc = mstcn.MultiStageModel_S(2, 8, 32, 2048, 14, True)
+    sd_tc = P.make_state_dict({k: v.shape for k, v in tc.state_dict().items()}, 1)
+    tc.load_state_dict(sd_tc)
+    tr = adapter_transformer.Transformer(32, 2048, 14, 30)
+    sd_tr = P.make_state_dict({k: v.shape for k, v in tr.state_dict().items()}, 2)
+    tr.load_state_dict(sd_tr)
+    tc, tr = tc.to(cuda).eval(), tr.to(cuda).eval()
+    m = getattr(mte, VARIANT)()
+    m.load_state_dict(sd)
+    m.svk_dtype = dtype
+    m = m.to(cuda).eval()
+    with torch.no_grad():
+        lfb = m(x.to(cuda), y.to(cuda), fl.to(cuda), return_features=True)[None]      # [1, 256, 2048]
+        out = tc(lfb.transpose(2, 1))[-1]                                             # [1, 14, 256]
+        p_all = tr.original_forward(out, lfb)                                         # [256, 1, 14]
+    torch.cuda.synchronize()
+    with torch.no_grad():
+        rf = feat[None]
+        ro = MS.multi_stage_s(rf.transpose(2, 1), sd_tc, 2, 8, True)[-1]
+        rp = TS.original_forward(ro, rf, sd_tr, 32)
+    got = p_all.float().cpu()
+    d_out = (out.float().cpu() - ro).abs().max().item()
+    d = (got - rp).abs().max().item()
+    agree = (got[:, 0, :7].argmax(-1) == rp[:, 0, :7].argmax(-1)).float().mean().item()
+    print(f"config5 {str(dtype)[6:]} B={B}: MS-TCN logits max|d| {d_out:.3e}, chain logits max|d| {d:.3e} "
+          f"(|ref| max {rp.abs().max():.2f}), phase argmax agreement {agree:.4f}")
+    assert got.shape == (B, 1, 14)
+    return got, rp, d, agree
+
+
+def test_config5_end_to_end_fp32_b256(cuda, b256):
+    """BASELINE config 5's chain on the 256-frame chunk at fp32 (trans_SV_output.py's precision): the
+    north-star bar — per-frame logits within 1e-3 of the oracle chain, phase argmax identical."""
+    got, rp, d, agree = _config5_chain(cuda, b256, torch.float32)
+    np.testing.assert_allclose(got.numpy(), rp.numpy(), rtol=0, atol=1e-3)
+    assert agree == 1.0
+
+
+def test_config5_end_to_end_fp16_b256(cuda, b256):
+    """BASELINE config 5 as specified (fp16 extraction, 256-frame chunk): the fp16 features (within
+    FP16_FEAT_ATOL of fp32) pass through the MS-TCN's 2048 -> 32 input conv and 16 layers, which spreads
+    their rounding to ~3.6e-3 on the MS-TCN logits and ~2.5e-3 on the chain's (measured); the bar is the
+    phase argmax identical for all 256 frames and the chain logits within 5e-3 (fp16 features: the
+    1e-3 logit bar holds at fp32, test above)."""
+    got, rp, d, agree = _config5_chain(cuda, b256, torch.float16)
+    assert agree == 1.0
+    np.testing.assert_allclose(got.numpy(), rp.numpy(), rtol=0, atol=5e-3)

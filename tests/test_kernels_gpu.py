@@ -570,3 +570,15 @@ def test_prompt_ln_vs_unfused(cuda, dt, M, C):
     for got, ref in ((xo, xu), (h, hu)):
         d = (got.float() - ref.float()).abs() / ref.float().abs().clamp_min(1.0)
         assert float(d.max()) <= 2 * ulp, float(d.max())
+    # independent fp64 reference (get_prompt + Block.norm1, mix_transformer_evp.py:776-815, 167-169) on the
+    # same storage-rounded inputs; the kernel rounds the lightweight GEMM's GELU output to the storage
+    # type (as the unfused GEMM does) and normalises the rounded x'
+    d64 = lambda t: t.double().cpu()
+    f64 = torch.nn.functional.gelu(d64(sm) @ d64(wl).t() + d64(bl)).to(dt).double()
+    x64 = d64(x) + f64 @ d64(ws).t() + d64(bs)
+    xr = d64(xo)
+    mu = xr.mean(1, keepdim=True)
+    h64 = (xr - mu) / torch.sqrt(((xr - mu) ** 2).mean(1, keepdim=True) + 1e-6) * d64(g1) + d64(b1)
+    for got, ref in ((xo, x64), (h, h64)):
+        d = (d64(got) - ref).abs() / ref.abs().clamp_min(1.0)
+        assert float(d.max()) <= 2 * ulp, ("fp64", float(d.max()))

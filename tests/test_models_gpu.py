@@ -33,6 +33,26 @@ def test_features_fp32_vs_reference_golden(cuda, golden, variant):
     np.testing.assert_allclose(f.cpu().numpy(), golden[f"{variant}_feat_flow"], rtol=0, atol=1e-3)
 
 
+@pytest.mark.parametrize("variant", ["mit_b1_evp", "mit_b4_evp", "mit_b5_evp"])
+def test_features_fp32_vs_oracle_other_variants(cuda, variant):
+    """The variants the reference defines but no golden pins (mix_transformer_evp.py:893-944): B = 2,
+    fp32, features and logits against the oracle (pinned by the b0/b2/b3 goldens) within 1e-3."""
+    m = _model(variant, cuda, torch.float32)
+    x, y, fl = I.frames(2), I.segmaps(2), I.flow(2)
+    with torch.no_grad():
+        f = m(x.to(cuda), y.to(cuda), fl.to(cuda), return_features=True)
+        yl, _ = m(x.to(cuda), y.to(cuda), fl.to(cuda))
+    torch.cuda.synchronize()
+    sd = P.make_state_dict(SH.mit_evp_shapes(variant), 0)
+    with torch.no_grad():
+        rf = M.forward(x, y, sd, variant, fl, return_features=True)
+        ry, _ = M.forward(x, y, sd, variant, fl)
+    assert f.shape == (2, 2048)
+    np.testing.assert_allclose(f.cpu().numpy(), rf.numpy(), rtol=0, atol=1e-3)
+    np.testing.assert_allclose(yl.cpu().numpy(), ry.numpy(), rtol=0, atol=1e-3)
+    assert (yl.argmax(1).cpu() == ry.argmax(1)).all()
+
+
 def test_b2_logits_fp32_argmax_exact(cuda, golden):
     m = _model("mit_b2_evp", cuda, torch.float32)
     with torch.no_grad():

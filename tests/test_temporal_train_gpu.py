@@ -170,6 +170,57 @@ def test_mamba_train_grads_vs_fp64_autograd(cuda):
 
 
 @pytest.mark.parametrize("kind", ["mstcn", "mamba"])
+def test_two_forwards_then_backward_vs_fp64_autograd(cuda, kind):
+    """Two train-mode forwards (two videos of different lengths) before one backward of the summed
+    loss (gradient accumulation): each autograd node must use its own saved input and activations
+    (the Mamba in_proj gradient once read a trainer-wide attribute the second forward
+    overwrote).  Checked two ways: (1) against the same two videos run forward -> backward one at a
+    time on the GPU with the same dropout draws (the interleaving may change nothing but the f32
+    summation order: relative L2 <= 1e-5), (2) against fp64 autograd through the oracle (the f32 bar of
+    this file, relaxed to 5e-3 for the 600- and 850-frame videos' summed gradients)."""
+    cw = torch.tensor(CW)
+    crit_p = torch.nn.CrossEntropyLoss(weight=cw.float().to(cuda))
+    crit_r = torch.nn.SmoothL1Loss()
+    vids = [(T, seed, I.lfb(T, 256, seed), *_labels(T, seed)) for T, seed in ((600, 31), (850, 32))]
+
+    def loss_of(y_all, lab, ant):
+        S = y_all.shape[0]
+        clc = sum(crit_p(y_all[j, 0, :7].transpose(1, 0), lab.to(cuda)) for j in range(S)) / S
+        antl = sum(crit_r(y_all[j, 0, 7:].transpose(1, 0), ant.to(cuda)) for j in range(S)) / S
+        return clc + antl
+
+    # (1) one video at a time: forward -> backward, gradients accumulated in .grad
+    m1, sd = _mstcn(cuda) if kind == "mstcn" else _mamba(cuda)
+    for T, seed, lfb, lab, ant in vids:
+        torch.manual_seed(seed)
+        loss_of(m1.forward(lfb.to(cuda).transpose(2, 1)), lab, ant).backward()
+    g_seq = {n: p.grad.detach().clone() for n, p in m1.named_parameters()}
+    # (2) both forwards first, one backward of the sum
+    m, _ = _mstcn(cuda) if kind == "mstcn" else _mamba(cuda)
+    sd64 = {k: v.double().requires_grad_(True) for k, v in sd.items()}
+    total, ref_total = 0.0, 0.0
+    for T, seed, lfb, lab, ant in vids:
+        torch.manual_seed(seed)
+        y_all = m.forward(lfb.to(cuda).transpose(2, 1))
+        masks = m._svk_trainer.last_masks
+        total = total + loss_of(y_all, lab, ant)
+        if kind == "mstcn":
+            ref = MS.multi_stage_s(lfb.transpose(2, 1), sd64, 4, 10, True, dtype=torch.float64, masks=masks[0].cpu())
+        else:
+            ref = OM.causal_mamba(lfb.transpose(2, 1), sd64, 10, masks=masks.cpu())
+        rc, ra = MS.tecno_loss(ref, lab, ant, cw.double())
+        ref_total = ref_total + rc + ra
+    total.backward()
+    torch.cuda.synchronize()
+    for n, p in m.named_parameters():
+        _grad_close(n, p.grad, g_seq[n], rel=1e-5, outlier=1e-4)
+    ref_total.backward()
+    assert abs(total.item() - ref_total.item()) < 1e-4 * max(1.0, abs(ref_total.item()))
+    for n, p in m.named_parameters():
+        _grad_close(n, p.grad, sd64[n].grad, rel=5e-3)
+
+
+@pytest.mark.parametrize("kind", ["mstcn", "mamba"])
 def test_native_step_matches_torch_optimizer_and_graph_replay(cuda, kind):
     """TemporalTrainStep (svk loss + clip + AdamW, graph-captured) == the reference loop's
     loss.backward(); clip_grad_norm_(1.0); AdamW(lr 1e-4, wd 1e-3) on the same draws; replays of the
