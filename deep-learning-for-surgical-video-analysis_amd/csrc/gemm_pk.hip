@@ -54,7 +54,11 @@ struct PkCfg {
   // resident workgroups per CU the register budget is held to (LDS allows 3 for 128x64 / 64x128, 2 for
   // 128x128): without the bound the f16 epilogue's conversions cost hipcc ~20-40 more VGPRs than the
   // bf16 one and drop a workgroup per CU
-  static constexpr int OCC = BM * BN <= 64 * 64 ? 5 : (BM * BN <= 128 * 64 ? 3 : 2);
+  // waves per SIMD the LDS allows (workgroups per CU x waves per workgroup / 4 SIMDs): the register
+  // budget __launch_bounds__ holds the kernel to, so hipcc's allocation never costs a resident workgroup
+  static constexpr int WG_PER_CU = (160 * 1024) / LDS;
+  static constexpr int OCC = WG_PER_CU * NT / 256 > 5 ? 5 : (WG_PER_CU * NT / 256 < 1 ? 1 : WG_PER_CU * NT / 256);
+  static constexpr bool ELDS_FITS = BM * BN * 2 <= STAGE;    // the staged epilogue tile fits one stage
   static_assert(A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "tile must split into whole DMA rounds");
   static_assert(LD <= 63, "vmcnt range");
 };
@@ -109,7 +113,7 @@ __device__ __forceinline__ void gload4(float& v, const char* src) {
 // epilogue stores raw f32 partial sums to slab part (p.slab + (part * M + m) * N + n) and a separate
 // reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
 template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
-__global__ __launch_bounds__(Cfg::NT, EXT ? (Cfg::OCC > 2 ? Cfg::OCC - 1 : 1) : Cfg::OCC)
+__global__ __launch_bounds__(Cfg::NT, Cfg::OCC)
 void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   typedef v8_t<T> tx8;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
@@ -130,7 +134,9 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   // this thread's DMA lane covers 16-byte chunk q = (wave * LD + i) * 64 + lane of the stage image
   // ASRC == 1: im2col rows of this thread's A slots (output pixel -> first input tap), per tile
   int crb[Cfg::A_LD], ciy[Cfg::A_LD], cix[Cfg::A_LD];
-  auto issue = [&](int unit, int kt, int buf) {
+  // live == false: past the workgroup's last (tile, K-step) — the same instructions run (branch-free
+  // around the DMA issue) with every source replaced by the zero block
+  auto issue = [&](int unit, int kt, int buf, bool live) {
     const int tile = SPLIT ? unit / ks : unit, part = unit - tile * ks;
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN, k0 = (SPLIT ? part * nk + kt : kt) * Cfg::BK;
     const uint32_t sa = lds0 + buf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
@@ -158,7 +164,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       for (int i = 0; i < Cfg::A_LD; ++i) {
         const int iy = ciy[i] + ti, ix = cix[i] + tj;
         const bool ok = k < p.K && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.Wd;
-        const char* src = ok ? reinterpret_cast<const char*>(A + crb[i] + ((long)iy * p.Wd + ix) * p.Cin + ci) : zero;
+        const char* src = ok && live ? reinterpret_cast<const char*>(A + crb[i] + ((long)iy * p.Wd + ix) * p.Cin + ci) : zero;
         dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
       }
     } else {
@@ -169,6 +175,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
         const int m = min(m0 + r, p.M - 1), k = k0 + c * 8;
         const char* src = reinterpret_cast<const char*>(A + (long)m * p.lda + k);
         if constexpr (KTAIL) src = k < p.K ? src : zero;
+        src = live ? src : zero;
         dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
       }
     }
@@ -179,6 +186,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       const int n = min(n0 + r, p.N - 1), k = k0 + c * 8;
       const char* src = reinterpret_cast<const char*>(Wt + (long)n * p.ldw + k);
       if constexpr (KTAIL) src = k < p.K ? src : zero;
+      src = live ? src : zero;
       dma16(src, __builtin_amdgcn_readfirstlane(sb + (wave * Cfg::B_LD + i) * 1024));
     }
   };
@@ -353,43 +361,42 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
 
   // DMA issue cursor: the (tile, K-step) stream of this workgroup.  Every step issues exactly LD
   // LDS-DMA instructions — the next (tile, K-step)'s, or, past the last one, LD copies of the zero block
-  // into the stage buffer nobody reads any more — so the wait for the stage a step computes is ONE
-  // unconditional counted `s_waitcnt vmcnt(LD)` (only the step just issued may stay in flight): no
-  // data-dependent branch around the wait, and every operation older than that step (the epilogue
-  // loads included) has provably landed once it returns (csrc/isa_check.py audits this on the built
-  // code object).
-  static_assert(NS == 2, "the counted waits assume a two-stage ring: one step in flight beyond the current");
+  // into a stage buffer nobody reads any more — so each wait is ONE unconditional counted
+  // `s_waitcnt vmcnt(n)`: no data-dependent branch around it, and the epilogue loads have provably
+  // landed before their registers are touched (csrc/isa_check.py audits this on the built code object,
+  // counting the vector-memory operations issued after each load on every path).
+  static_assert((NS - 1) * Cfg::LD <= 63, "vmcnt range");
   int itile = first, ikt = 0, ibuf = 0, buf = 0;
   auto issue_next = [&]() {
-    if (itile < ntiles) {
-      issue(itile, ikt, ibuf);
-      if (++ikt == nk) { ikt = 0; itile += G; }
-    } else {
-      const uint32_t sa = lds0 + ibuf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
-#pragma unroll
-      for (int i = 0; i < Cfg::A_LD; ++i) dma16(zero, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
-#pragma unroll
-      for (int i = 0; i < Cfg::B_LD; ++i) dma16(zero, __builtin_amdgcn_readfirstlane(sb + (wave * Cfg::B_LD + i) * 1024));
-    }
-    ibuf ^= 1;
+    const bool live = itile < ntiles;
+    issue(live ? itile : first, live ? ikt : 1, ibuf, live);
+    if (live && ++ikt == nk) { ikt = 0; itile += G; }
+    ibuf = ibuf + 1 == NS ? 0 : ibuf + 1;
   };
   // One pipeline step: top up the DMA ring (into the stage computed one step ago), wait for the
-  // oldest stage `buf`, compute from it.
+  // oldest stage `buf` (the NS - 1 steps issued after it may stay in flight), compute from it.  The
+  // epilogue operands of a tile are issued just before the DMA of its step nk - NS + 1 (NS - 1 steps
+  // before its last step), so on the last step they are older than every step still allowed in
+  // flight: the same unconditional wait retires them (the host keeps nk >= NS - 1).
   auto step = [&](bool last) {
     issue_next();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Cfg::LD) : "memory");   // all but the step just issued
-    if (last) tie_epi();               // the epilogue loads (older than that step) have landed too
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * Cfg::LD) : "memory");
+    if (last) tie_epi();               // the epilogue loads are older than the NS - 1 steps still in flight
     barrier_mem();
     compute(buf);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     barrier_mem();                     // nobody still reads `buf` when a later DMA overwrites it
     stile = smem + buf * Cfg::STAGE;
-    buf ^= 1;
+    buf = buf + 1 == NS ? 0 : buf + 1;
   };
-  issue_next();
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) issue_next();
   for (int tile = first; tile < ntiles; tile += G) {
-    for (int kt = 0; kt < nk - 1; ++kt) step(false);
-    epi_load(tile);                   // epilogue operands fly during the last step's wait and MFMAs
+    for (int kt = 0; kt < nk - 1; ++kt) {
+      if (kt == nk - NS + 1) epi_load(tile);    // (NS > 2) fly during the last NS - 1 steps
+      step(false);
+    }
+    if (NS == 2) epi_load(tile);      // epilogue operands fly during the last step's wait and MFMAs
     step(true);
     switch (EXT ? p.uact : p.act) {
       case SVK_ACT_GELU: epilogue(tile, std::integral_constant<int, SVK_ACT_GELU>{}); break;
@@ -418,6 +425,10 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ks = SPLIT ? a.ksplit : 1;
   const long ntiles = (long)ntm * ntn * ks;
   const int nk = (a.K + 63) / 64 / ks;   // K-steps per unit (the caller makes ks divide them)
+  if (nk < Cfg::NSTAGE - 1) {             // the epilogue loads are issued NSTAGE - 2 steps before a tile's last
+    set_error("gemm_pk: %d K-steps per tile, the %d-stage ring needs %d", nk, Cfg::NSTAGE, Cfg::NSTAGE - 1);
+    return SVK_EUNSUPPORTED;
+  }
   static const int slots =
       pk_slots(reinterpret_cast<const void*>(&gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), Cfg::NT);
   const int grid = (int)std::min<long>(ntiles, slots);
@@ -443,22 +454,36 @@ template <typename T, class Cfg, int ASRC>
 static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   if (g_tune[TUNE_PK_ELDS] >= 0) elds = g_tune[TUNE_PK_ELDS];
-  // the staged epilogue swizzles 16-byte chunks within a power-of-two row of chunks
-  elds = elds && (Cfg::BN & (Cfg::BN - 1)) == 0 && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
+  // the staged epilogue swizzles 16-byte chunks within a power-of-two row of chunks, in one stage buffer
+  elds = elds && Cfg::ELDS_FITS && (Cfg::BN & (Cfg::BN - 1)) == 0 && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
   const bool tail = a.K % 64 != 0, ext = a.rscale || a.U;
-  if (ASRC == 1) {
+  // the extended (training) epilogue holds two more operand sets: with 8 waves or 3 stages it spills, so
+  // it runs on the 4-wave two-stage 128 x 128 tile
+  constexpr bool EXT_OK = Cfg::NT == 256 && Cfg::NSTAGE == 2;
+  if constexpr (ASRC == 1) {
     // the im2col loader zero-fills the A side of a K tail itself, but the weight rows must read the
     // zero block too: the last row's tail would otherwise read past the packed weights, and 0 x a
     // NaN bit pattern found there is NaN.  No extended epilogue for convs.
-    if (elds) return tail ? launch_pk<T, Cfg, true, true, 1, false>(a, st) : launch_pk<T, Cfg, false, true, 1, false>(a, st);
+    if constexpr (Cfg::ELDS_FITS) {
+      if (elds) return tail ? launch_pk<T, Cfg, true, true, 1, false>(a, st) : launch_pk<T, Cfg, false, true, 1, false>(a, st);
+    }
     return tail ? launch_pk<T, Cfg, true, false, 1, false>(a, st) : launch_pk<T, Cfg, false, false, 1, false>(a, st);
+  } else {
+    if (ext) {
+      if constexpr (!EXT_OK) {
+        return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, ASRC>(a, st, elds);
+      } else {
+        if constexpr (Cfg::ELDS_FITS) {
+          if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, true>(a, st) : launch_pk<T, Cfg, false, true, 0, true>(a, st);
+        }
+        return tail ? launch_pk<T, Cfg, true, false, 0, true>(a, st) : launch_pk<T, Cfg, false, false, 0, true>(a, st);
+      }
+    }
+    if constexpr (Cfg::ELDS_FITS) {
+      if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, false>(a, st) : launch_pk<T, Cfg, false, true, 0, false>(a, st);
+    }
+    return tail ? launch_pk<T, Cfg, true, false, 0, false>(a, st) : launch_pk<T, Cfg, false, false, 0, false>(a, st);
   }
-  if (ext) {
-    if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, true>(a, st) : launch_pk<T, Cfg, false, true, 0, true>(a, st);
-    return tail ? launch_pk<T, Cfg, true, false, 0, true>(a, st) : launch_pk<T, Cfg, false, false, 0, true>(a, st);
-  }
-  if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, false>(a, st) : launch_pk<T, Cfg, false, true, 0, false>(a, st);
-  return tail ? launch_pk<T, Cfg, true, false, 0, false>(a, st) : launch_pk<T, Cfg, false, false, 0, false>(a, st);
 }
 
 // Eligible: bf16, K-contiguous operands (16-byte aligned rows, K % 8 == 0; conv: Cin % 8 == 0),
@@ -495,7 +520,11 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     }
   }
   const bool reg_epi = cfg == 0 && (big || a.M < 32768);
-  // cfg: 0 = 128x128, 10 = 128x64, 20 = 64x128, 30 = 64x64, 40 = 128x160 (N % 160 == 0), 50 = 256x128 (8 waves)
+  // cfg: 0 = 128x128, 10 = 128x64, 20 = 64x128, 30 = 64x64, 40 = 128x160 (N % 160 == 0), 50 = 256x128 (8 waves).
+  // Round-3 sweep (profiles/r03/pk_cfg_sweep.txt, every variant interleaved in one process): three-stage
+  // rings (256x128 / 128x64 / 128x128 / 128x256-8-wave) never beat the two-stage tiles on the MiT-b2 shapes
+  // and 256x256 with 8 waves spills (128 accumulator + 96 epilogue-operand VGPRs): not instantiated.  The
+  // kernel keeps NSTAGE generic (epilogue loads issued NSTAGE - 2 steps before a tile's last step).
   if (cfg == 40 && a.N % 160 != 0) cfg = 10;
   if (asrc == 1) {
     switch (cfg) {

@@ -36,7 +36,7 @@ def regs(tok):
     return {int(m.group(1))} if m else set()
 
 
-def disasm(obj):
+def disasm(obj, notes_out=None):
     with tempfile.TemporaryDirectory() as d:
         fat, co = os.path.join(d, "fat.bin"), os.path.join(d, "g.co")
         r = subprocess.run([f"{LLVM}/llvm-objcopy", "--dump-section", f".hip_fatbin={fat}", obj,
@@ -45,6 +45,9 @@ def disasm(obj):
             return ""                                          # host-only object: no device code
         subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--targets={TARGET}",
                         f"--input={fat}", f"--output={co}"], check=True, capture_output=True)
+        if notes_out is not None:
+            notes_out.append(subprocess.run([f"{LLVM}/llvm-readelf", "--notes", co], check=True, capture_output=True,
+                                            text=True).stdout)
         return subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", co], check=True,
                               capture_output=True, text=True).stdout
 
@@ -80,7 +83,15 @@ def check_packed(funcs):
     return bad
 
 
+VMEM_RE = re.compile(r"(global_|buffer_|flat_|scratch_)")
+VMCNT_RE = re.compile(r"vmcnt\((\d+)\)")
+
+
 def check_epilogue_loads(funcs):
+    """For every VGPR-destination global_load of a gemm_pk kernel, on every control-flow path: the first
+    s_waitcnt vmcnt(n) with at least n vector-memory operations issued after the load (so the load is not
+    among the n youngest and has retired) comes before any instruction reading or writing its
+    destination registers."""
     bad = []
     for f, ins in funcs.items():
         if "gemm_pk" not in f:
@@ -90,34 +101,52 @@ def check_epilogue_loads(funcs):
             if not re.match(r"global_load_dword(x2|x4)?$", op):
                 continue
             dst = regs(operands(ops)[0])
-            seen, stack = {}, [(k + 1, None)]
+            seen, stack = {}, [(k + 1, 0, None)]
             while stack:
-                j, prev = stack.pop()
-                if j in seen or j >= len(ins):
+                j, younger, prev = stack.pop()
+                if j >= len(ins):
                     continue
-                seen[j] = prev
+                # the path with the FEWEST younger operations is the one a wait may fail to cover: a visit
+                # with at least as many as an earlier one is dominated
+                if j in seen and seen[j] <= younger:
+                    continue
+                seen[j] = younger
+                key = j
                 a2, op2, ops2, tgt = ins[j]
-                if op2 == "s_waitcnt" and "vmcnt" in ops2:
-                    continue                                  # covered on this path
+                if op2 == "s_waitcnt":
+                    m = VMCNT_RE.search(ops2)
+                    if m and younger >= int(m.group(1)):
+                        continue                              # retired on this path
                 touched = set()
                 for o in operands(ops2):
                     touched |= regs(o)
                 if op2.startswith(("v_", "global_", "ds_", "buffer_", "flat_")) and touched & dst:
-                    path, q = [], prev
-                    while q is not None and len(path) < 400:
-                        path.append(q)
-                        q = seen.get(q)
-                    jumps = [f"0x{ins[q][0]:x}" for q in reversed(path) if ins[q][1].startswith(("s_branch", "s_cbranch"))]
-                    bad.append(f"{f}+0x{addr:x}: {op} {ops} -> touched at +0x{a2:x}: {op2} {ops2} (via {jumps[:12]})")
+                    bad.append(f"{f}+0x{addr:x}: {op} {ops} -> touched at +0x{a2:x}: {op2} {ops2}")
                     continue
+                if VMEM_RE.match(op2):
+                    younger += 1
                 if op2 == "s_endpgm":
                     continue
                 if op2 == "s_branch":
-                    stack.append((at.get(tgt, len(ins)), j))
+                    stack.append((at.get(tgt, len(ins)), younger, key))
                     continue
                 if op2.startswith("s_cbranch") and tgt is not None:
-                    stack.append((at.get(tgt, len(ins)), j))
-                stack.append((j + 1, j))
+                    stack.append((at.get(tgt, len(ins)), younger, key))
+                stack.append((j + 1, younger, key))
+    return bad
+
+
+def check_scratch(notes):
+    """gemm_pk kernels must not use scratch (a spill of a register an inline-asm load is still writing
+    would store garbage; the round-3 256x256 tile that spilled faulted the GPU)."""
+    bad, cur = [], None
+    for line in notes.split("\n"):
+        m = re.match(r"\s+\.name:\s+(\S+)", line)
+        if m:
+            cur = m.group(1)
+        m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count):\s+(\d+)", line)
+        if m and int(m.group(2)) > 0 and cur and "gemm_pk" in cur:
+            bad.append(f"{cur}: .{m.group(1)} {m.group(2)}")
     return bad
 
 
@@ -125,7 +154,11 @@ def main(objs):
     fails = 0
     nload = 0
     for obj in objs:
-        funcs = functions(disasm(obj))
+        notes = []
+        funcs = functions(disasm(obj, notes))
+        for msg in check_scratch(notes[0] if notes else ""):
+            print(f"isa_check: {os.path.basename(obj)}: scratch use in a kernel with inline-asm loads: {msg}")
+            fails += 1
         for msg in check_packed(funcs):
             print(f"isa_check: {os.path.basename(obj)}: packed-FP32 op_sel hazard class: {msg}")
             fails += 1

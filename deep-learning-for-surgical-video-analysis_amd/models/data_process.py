@@ -358,6 +358,29 @@ class CholecFlowDataset(Dataset):
         return len(self.file_paths)
 
 
+class SyntheticDecodedCholecFlow(Dataset):
+    """Seeded synthetic items in CholecFlowDataset(decoded=True)'s contract: decoded uint8 RGB frame and
+    binary segmap [H, W, 3], raw RAFT-style flow [H, W, 2] f32 (N(0, 2 px)), phase, anticipation.  The
+    default frame size is 250x250 (the reference's own data_process.py:493-511 stubs)."""
+
+    def __init__(self, n, seed=0, size=(250, 250)):
+        self.n, self.seed, self.size = n, seed, tuple(size)
+
+    def __len__(self):
+        return self.n
+
+    def __getitem__(self, i):
+        r = np.random.default_rng((self.seed, i))
+        h, w = self.size
+        img = r.integers(0, 256, (h, w, 3), dtype=np.uint8)
+        yy, xx = np.mgrid[0:h, 0:w]
+        cy, cx, ay, ax = r.uniform(0, h), r.uniform(0, w), r.uniform(10, 70), r.uniform(10, 70)
+        m = ((((yy - cy) / ay) ** 2 + ((xx - cx) / ax) ** 2) <= 1).astype(np.uint8) * 255
+        seg = np.repeat(m[:, :, None], 3, axis=2)
+        flow = (2.0 * r.standard_normal((h, w, 2))).astype(np.float32)
+        return img, seg, flow, np.int64(r.integers(0, 7)), r.uniform(0, 1, 7).astype(np.float64)
+
+
 class SyntheticCholecFlowDataset(Dataset):
     """Seeded synthetic frames with CholecFlowDataset's per-item contract."""
 

@@ -214,6 +214,35 @@ def test_lfb_extraction_and_pickle(cuda, tmp_path):
     np.testing.assert_allclose(arr, bank.cpu().numpy().astype(np.float64))
 
 
+@pytest.mark.parametrize("workers", [0, 2])
+def test_lfb_pipeline_decoded_equals_direct_forward(cuda, workers):
+    """The pipelined extraction (svk.lfb: DataLoader workers -> pinned uint8 batches -> H2D on a copy stream
+    -> GPU frame / flow transforms -> graph replay -> async D2H into the pinned bank) over decoded frames
+    equals transforming all frames at once and running the eager forward (10 frames in batches of 4: a
+    partial last batch; 250x250 frames as the reference's data_process.py:493-511 stubs)."""
+    from models.data_process import SyntheticDecodedCholecFlow
+    from svk.lfb import extract_lfb
+    from svk.preproc import frame_transform, flow_transform
+    m = _model("mit_b0_evp", cuda, torch.float16)
+    ds = SyntheticDecodedCholecFlow(10, seed=4)
+    bank = extract_lfb(m, ds, batch_size=4, num_workers=workers)
+    assert bank.shape == (10, 2048) and bank.is_pinned()
+    fr = torch.stack([torch.from_numpy(ds[i][0]) for i in range(10)]).to(cuda)
+    sg = torch.stack([torch.from_numpy(ds[i][1]) for i in range(10)]).to(cuda)
+    fl = torch.stack([torch.from_numpy(ds[i][2]) for i in range(10)]).to(cuda)
+    with torch.no_grad():
+        x, y, f = frame_transform(fr), frame_transform(sg), flow_transform(fl)
+        # the same batch shapes as the pipeline (kernel choices depend on the batch), last one padded
+        refs = []
+        for a in range(0, 10, 4):
+            idx = [min(i, 9) for i in range(a, a + 4)]
+            o = m(x[idx][:, None], y[idx][:, None], f[idx][:, None], return_features=True).float()
+            refs.append(o[:min(4, 10 - a)])
+        ref = torch.cat(refs)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(bank.numpy(), ref.cpu().numpy(), rtol=0, atol=1e-6)
+
+
 def test_end_to_end_chunk(cuda):
     """SegFormer(b2) -> MS-TCN(2,8,32,2048) -> Transformer(30) on one synthetic 64-frame clip, fp32,
     against the oracle chain (config 5 shape at reduced length)."""
