@@ -459,7 +459,7 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   const bool tail = a.K % 64 != 0, ext = a.rscale || a.U;
   // the extended (training) epilogue holds two more operand sets: with 8 waves or 3 stages it spills, so
   // it runs on the 4-wave two-stage 128 x 128 tile
-  constexpr bool EXT_OK = Cfg::NT == 256 && Cfg::NSTAGE == 2;
+  constexpr bool EXT_OK = Cfg::NT == 256 && Cfg::NSTAGE == 2 && Cfg::BM * Cfg::BN <= 128 * 128;
   if constexpr (ASRC == 1) {
     // the im2col loader zero-fills the A side of a K tail itself, but the weight rows must read the
     // zero block too: the last row's tail would otherwise read past the packed weights, and 0 x a

@@ -206,7 +206,7 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
     if (T_ > 0) load_xa(0, xa);
     for (int s = 0; s < T_ + 2; ++s) {
       const int g2 = s - 2;
-      if (g2 >= 0) {
+      if (g2 >= 0 && diag != 3) {   // (diag 3, timing ablation: producers idle, the dwconv waves alone)
         // ---- fc2 partial sums of item g2 (transposed: A = W2 rows, B = G rows)
         const int c2 = g2 % NCH;
         const char* G2 = sG(g2 & 1);
@@ -293,7 +293,7 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
           }
         }
       }
-      if (s < T_) {
+      if (s < T_ && diag != 3) {
         // ---- fc1 of item s -> sH(s & 1): halo tokens x HC hidden channels of chunk c1
         const int c1 = s % NCH;
         int b, y0;
@@ -357,7 +357,7 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
     if (T_ > 0) tload(0);
     for (int s = 0; s < T_ + 2; ++s) {
       const int g = s - 1;
-      if (g >= 0 && g < T_) {
+      if (g >= 0 && g < T_ && diag != 2) {   // (diag 2, timing ablation: dwconv waves idle, the producers alone)
         const int p = g & 1;
         const uint32_t* H0 = sH(p);
         char* G0 = sG(p);
@@ -400,7 +400,8 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
             for (int h = 0; h < 2; ++h) {
               const int o = (dg * K::RV + rr) * W + 2 * dp + h;
               uint2 v;
-              if (diag == 1) {   // timing diagnostic only (svk_tune("ffn_diag", 1)): GELU replaced by ReLU
+              if (diag == 1) {   // timing diagnostics only (svk_tune("ffn_diag", n)): 1 = GELU replaced by ReLU,
+                                 // 2 = dwconv waves idle, 3 = producer waves idle (outputs meaningless)
                 v.x = pack2<T>(fmaxf(acc[rr][0][h], 0.f), fmaxf(acc[rr][1][h], 0.f));
                 v.y = pack2<T>(fmaxf(acc[rr][2][h], 0.f), fmaxf(acc[rr][3][h], 0.f));
               } else {

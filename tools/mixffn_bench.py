@@ -28,13 +28,19 @@ def run(B, H, C, reps, only, dt=torch.float16):
     def fused_ln():
         return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=(b2 + 1, b2, 1e-6))
 
-    def fused_relu():   # timing diagnostic: the whole-MixFFN kernel with its GELU replaced by a ReLU
-        from svk import _lib
-        _lib.load().svk_tune(b"ffn_diag", 1)
-        try:
-            return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2)
-        finally:
-            _lib.load().svk_tune(b"ffn_diag", 0)
+    def diag(n):       # timing diagnostics of the whole-MixFFN kernel (csrc/mixffn.hip: outputs meaningless)
+        def fn():
+            from svk import _lib
+            _lib.load().svk_tune(b"ffn_diag", n)
+            try:
+                return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2)
+            finally:
+                _lib.load().svk_tune(b"ffn_diag", 0)
+        return fn
+
+    fused_relu = diag(1)        # GELU replaced by a ReLU
+    fused_nodw = diag(2)        # dwconv waves idle: the producer waves alone
+    fused_noprod = diag(3)      # producer waves idle: the dwconv waves alone
 
     def fc1dw():
         g = ops.mixffn_fc1_dwconv(xn, w1, b1, taps, db, act="gelu")
@@ -45,8 +51,8 @@ def run(B, H, C, reps, only, dt=torch.float16):
         g = ops.dwconv3x3(h.view(B, H, H, 4 * C), taps, db, act="gelu")
         return ops.gemm(g.view(-1, 4 * C), w2, b2, residual=x.view(-1, C))
 
-    for name, fn in (("fused", fused), ("fused_relu", fused_relu), ("fused_ln", fused_ln), ("fc1dw", fc1dw),
-                     ("unfused", unfused)):
+    for name, fn in (("fused", fused), ("fused_relu", fused_relu), ("fused_nodw", fused_nodw),
+                     ("fused_noprod", fused_noprod), ("fused_ln", fused_ln), ("fc1dw", fc1dw), ("unfused", unfused)):
         if only and name != only:
             continue
         if name.startswith("fused") and not ops.mixffn_supported(H, C):
