@@ -1,0 +1,387 @@
+// Whole MixFFN + Block residual (+ the stage LayerNorm) in one kernel, f16, with the depthwise window
+// held in REGISTERS (mix_transformer_evp.py:32-67, DWConv :19-30, Block :169, stage norm :370-412):
+//
+//   Y  = X + fc2( GELU( dwconv3x3( fc1(XN) ) ) )          NHWC [B, H, W, C] f16, hidden 4C
+//   Yn = LN(Y)                                            (when gamma != nullptr; Y may then be null)
+//
+// Why a second design next to mixffn.hip: the wave-specialised kernel there moves the hidden map
+// through LDS (fc1 waves write it, dwconv waves read 3x3 neighbourhoods back, fc2 waves read the GELU
+// output), with one workgroup per CU and a barrier per 32-channel chunk: its dwconv waves issue VALU
+// ~20 % of the time (LDS latency + barrier waits).  Here nothing of the hidden map touches LDS:
+//
+//   * the MFMA layout IS the conv layout.  fc1 is computed transposed (D = W1 · XNᵀ, 16x16x32), so
+//     lane (fr, fq) ends with hidden channels 4fq .. 4fq+3 (of a 16-channel n-tile) of token fr, and a
+//     16-token m-tile is 16 consecutive pixels x0-1 .. x0+14 of one image row.  Horizontal taps are the
+//     neighbouring lanes (DPP row_shr:1 / row_shl:1 inside each 16-lane row), vertical taps are the
+//     previous / next image rows, which the same lane computed in earlier iterations: a 3-row rolling
+//     window of packed-f16 registers.  Lanes 0 and 15 are the halo columns (14 outputs per m-tile).
+//   * the GELU output lands directly in the fc2 operand layout: lane (fr, fq) holds 8 hidden values of
+//     token fr for each 32-channel k-step — fc2's reduction index is permuted to match (the W2
+//     fragments are gathered accordingly once, in the prologue).  fc2 is transposed too, so a lane ends
+//     with 4 consecutive output channels of one token.
+//   * a workgroup = HID / 64 waves (4 for C = 64) splitting the hidden channels 64 each, so every wave
+//     keeps its W1 / W2 fragments in registers for the whole (persistent) kernel; the per-row fc2
+//     partial sums of the waves meet once in LDS (f32 slabs, double-buffered, ONE barrier per row),
+//     where each wave reduces a quarter of the tokens and runs the epilogue (+ b2 + residual, 16-byte
+//     wide LayerNorm rows over 16 lanes, 8-byte stores).
+//
+// Work unit: (frame, 14-column x-tile, strip of R rows); a wave walks the strip top to bottom
+// computing fc1 one row ahead (one halo row above the strip is recomputed).  Per row and wave:
+// 8 fc1 + 8 fc2 MFMAs and ~16 x 28 VALU (9 fma_mix taps, 3 DPP moves, GELU) per lane.
+// Numerics as mixffn.hip: fc1 output, taps and GELU output rounded to f16 (the reference's autocast
+// stores), accumulation / bias / GELU / LayerNorm statistics in f32.
+#include "svk_common.h"
+
+namespace svk {
+namespace ffnrw {
+
+template <int C_, int W_, int R_, int OCC_ = 2>
+struct Cfg {
+  static constexpr int C = C_, W = W_, R = R_, OCC = OCC_;
+  static constexpr int HID = 4 * C, NW = HID / 64, NT = 64 * NW;
+  static constexpr int KS = C / 32;                 // fc1 k-steps
+  static constexpr int NC2 = C / 16;                // fc2 output n-tiles
+  static constexpr int XT = (W + 13) / 14;          // 14-column x-tiles
+  static constexpr int TPW = 16 / NW;               // epilogue tokens per wave
+  static constexpr int LPT = 64 / TPW;              // epilogue lanes per token (4 channels each)
+  static constexpr int SROW = C + 4;                // slab row (floats): conflict-free 16-byte writes
+  static constexpr int SLAB = 16 * SROW;            // one wave's partial sums of a row
+  static constexpr int TBLK = 96;                   // tap block (wave, n-tile, fq): taps [9][4] f16, pad, dwb [4] f32
+  static constexpr int LDS_TP = HID * 4;             // b1 (f32) | tap blocks | b2, gamma, beta | slabs
+  static constexpr int LDS_EP = LDS_TP + NW * 16 * TBLK;
+  static constexpr int LDS_T = LDS_EP + 3 * C * 4;
+  static constexpr int LDS = LDS_T + 2 * NW * SLAB * 4;
+  static_assert(C % 32 == 0 && NW >= 1 && NW <= 4 && LPT * 4 == C, "shape");
+};
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk(float lo, float hi) { return __builtin_bit_cast(uint32_t, h2{(_Float16)lo, (_Float16)hi}); }
+__device__ __forceinline__ float lo16(uint32_t u) { return (float)__builtin_bit_cast(h2, u).x; }
+__device__ __forceinline__ float hi16(uint32_t u) { return (float)__builtin_bit_cast(h2, u).y; }
+// value of lane l - 1 / l + 1 inside each 16-lane row (0 at the row ends: halo lanes, never stored)
+__device__ __forceinline__ uint32_t from_left(uint32_t v) { return __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true); }
+__device__ __forceinline__ uint32_t from_right(uint32_t v) { return __builtin_amdgcn_update_dpp(0u, v, 0x101, 0xf, 0xf, true); }
+
+// gelu(x) = relu(x) - 0.5 |x| t q(t) exp(-x^2 / 2), 1 - erf(z) = t q(t) exp(-z^2) by Abramowitz & Stegun
+// 7.1.25 (|error| <= 2.5e-5, 40x below the f16 rounding of the output): 9 VALU + 2 transcendental
+__device__ __forceinline__ float gelu_rw(float x) {
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.47047f * 0.70710678118654752f, ax, 1.0f));
+  const float q = fmaf(fmaf(-0.5f * 0.7478556f, t, -0.5f * -0.0958798f), t, -0.5f * 0.3480242f);
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
+  return fmaf(ax * t * q, e, fmaxf(x, 0.f));
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <class K>
+__global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict__ XN, const f16* __restrict__ X,
+                                                     const f16* __restrict__ W1, const float* __restrict__ b1,
+                                                     const float* __restrict__ taps, const float* __restrict__ dwb,
+                                                     const f16* __restrict__ W2, const float* __restrict__ b2,
+                                                     f16* __restrict__ Y, f16* __restrict__ Yn,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     float eps, int H, int nstrip, int total, int diag) {
+  constexpr int C = K::C, W = K::W, R = K::R, HID = K::HID, KS = K::KS, NC2 = K::NC2, NW = K::NW;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  char* const smem = reinterpret_cast<char*>(smem4);
+  float* const slab0 = reinterpret_cast<float*>(smem + K::LDS_T);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- prologue: b1 [HID] f32 and the tap blocks in LDS; W1 / W2 fragments of this wave's 64 hidden
+  // channels in registers (4 n-tiles x KS k-steps; 2 k-steps of 32 hidden x NC2 output n-tiles) with
+  // fc2's reduction index permuted to the GELU output layout: k-slot 8 fq + s of k-step q <-> hidden
+  // 32 q + 4 fq + s (s < 4), 32 q + 16 + 4 fq + s - 4 (s >= 4)
+  for (int e = tid; e < HID; e += K::NT) reinterpret_cast<float*>(smem)[e] = b1[e];
+  for (int e = tid; e < NW * 16 * 40; e += K::NT) {
+    // block blk = (w * 4 + j) * 4 + fq holds channels 4 blk + c: element t * 4 + c of taps, then dwb
+    const int blk = e / 40, r = e % 40, t = r / 4, c = r % 4;
+    char* bp = smem + K::LDS_TP + blk * K::TBLK;
+    if (t < 9) reinterpret_cast<f16*>(bp)[r] = (f16)taps[t * HID + 4 * blk + c];
+    else reinterpret_cast<float*>(bp + 80)[c] = dwb[4 * blk + c];
+  }
+  f16x8 w1f[4][KS], w2f[2][NC2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      w1f[j][ks] = *reinterpret_cast<const f16x8*>(W1 + (long)(64 * w + 16 * j + fr) * C + 32 * ks + 8 * fq);
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int c = 0; c < NC2; ++c) {
+      const f16* src = W2 + (long)(16 * c + fr) * HID + 64 * w + 32 * q + 4 * fq;
+      const f16x4 lo = *reinterpret_cast<const f16x4*>(src), hi = *reinterpret_cast<const f16x4*>(src + 16);
+      w2f[q][c] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  float* const sEp = reinterpret_cast<float*>(smem + K::LDS_EP);   // b2 [C], gamma [C], beta [C]
+  for (int e = tid; e < 3 * C; e += K::NT)
+    sEp[e] = e < C ? b2[e] : (gamma ? (e < 2 * C ? gamma[e - C] : beta[e - 2 * C]) : (e < 2 * C ? 1.f : 0.f));
+  // epilogue lane: token et = TPW w + lane / LPT of the m-tile, channels 4 ec .. 4 ec + 3
+  const int et = K::TPW * w + lane / K::LPT, ec = lane % K::LPT;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  const float* b1l = reinterpret_cast<const float*>(smem) + 64 * w + 4 * fq;   // + 16 j
+  const uint4* tpl = reinterpret_cast<const uint4*>(smem + K::LDS_TP + (w * 16 + fq) * K::TBLK);   // + j * 4 * TBLK / 16
+  const int G = gridDim.x;
+  int buf = 0;
+  for (int u = xcd_remap(blockIdx.x, G); u < total; u += G) {
+    const int xt = u % K::XT, rest = u / K::XT, sidx = rest % nstrip, b = rest / nstrip;
+    const int y0 = sidx * R, x0 = 14 * xt;
+    const int tx = x0 - 1 + fr;                          // this lane's pixel column (fc1 / dwconv)
+    const bool xok = tx >= 0 && tx < W;
+    const f16* XNb = XN + (long)b * H * W * C + (long)min(max(tx, 0), W - 1) * C + 8 * fq;
+    auto load_x = [&](int yy, f16x8 (&xf)[KS]) __attribute__((always_inline)) {
+      const f16* src = XNb + (long)min(max(yy, 0), H - 1) * W * C;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xf[ks] = *reinterpret_cast<const f16x8*>(src + 32 * ks);
+    };
+    // fc1 of hidden row yy: MFMAs issued early, packed (+ b1, f16, zero outside the image) late, so the
+    // dwconv of the current row runs while they are in flight
+    auto fc1_mma = [&](const f16x8 (&wf)[4][KS], const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(wf[j][ks], xf[ks], a[j]);
+      }
+    };
+    auto fc1_pack = [&](int yy, const f32x4 (&a)[4], uint32_t (&hw)[4][2]) __attribute__((always_inline)) {
+      const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 bb = *reinterpret_cast<const float4*>(b1l + 16 * j);
+        hw[j][0] = pk(a[j][0] + bb.x, a[j][1] + bb.y) & m;
+        hw[j][1] = pk(a[j][2] + bb.z, a[j][3] + bb.w) & m;
+      }
+    };
+    uint32_t win[3][4][2];
+    {
+      f16x8 xa[KS], xb[KS], xc[KS];
+      f32x4 a[4];
+      load_x(y0 - 1, xa);
+      load_x(y0, xb);
+      load_x(y0 + 1, xc);
+      fc1_mma(w1f, xa, a);
+      fc1_pack(y0 - 1, a, win[0]);
+      fc1_mma(w1f, xb, a);
+      fc1_pack(y0, a, win[1]);
+      fc1_mma(w1f, xc, a);
+      fc1_pack(y0 + 1, a, win[2]);
+    }
+    // X rows of the next two new hidden rows, two rows ahead (row-parity register sets: the loop is
+    // unrolled by 2 so that no in-flight load is ever copied)
+    f16x8 xA[KS], xB[KS];
+    load_x(y0 + 2, xA);
+    load_x(y0 + 3, xB);
+    // epilogue row operands: residual of (row, token et, channels 4 ec..)
+    const int etx = x0 - 1 + et;
+    const bool eok = et >= 1 && et <= 14 && etx < W;
+    const long eoff0 = ((long)b * H * W + min(max(etx, 0), W - 1)) * C + 4 * ec;   // halo lanes: clamped, never stored
+    // ---- epilogue of row yy from slab buffer bb: token et, channels 4 ec .. 4 ec + 3
+    auto epilogue = [&](int yy, uint2 res, int bb) __attribute__((always_inline)) {
+      float4 v = *reinterpret_cast<const float4*>(slab0 + bb * NW * K::SLAB + et * K::SROW + 4 * ec);
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) {
+        const float4 o = *reinterpret_cast<const float4*>(slab0 + (bb * NW + ww) * K::SLAB + et * K::SROW + 4 * ec);
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+      }
+      const f32x2 r01 = unpack2<f16>(res.x), r23 = unpack2<f16>(res.y);
+      const float4 eb2 = *reinterpret_cast<const float4*>(sEp + 4 * ec);
+      const f16 o0 = (f16)(v.x + eb2.x + r01.x), o1 = (f16)(v.y + eb2.y + r01.y);
+      const f16 o2 = (f16)(v.z + eb2.z + r23.x), o3 = (f16)(v.w + eb2.w + r23.y);
+      const bool st = eok && yy < H;
+      const long oo = eoff0 + (long)yy * W * C;
+      if (Y && st && !(diag & 64)) *reinterpret_cast<f16x4*>(Y + oo) = f16x4{o0, o1, o2, o3};
+      if (gamma) {   // LayerNorm of the token's C channels: LPT lanes (a power of two, aligned)
+        const float f0 = o0, f1 = o1, f2 = o2, f3 = o3;
+        float sm = f0 + f1 + f2 + f3;
+#pragma unroll
+        for (int m = K::LPT / 2; m >= 1; m >>= 1) sm += __shfl_xor(sm, m, 64);
+        const float mean = sm * (1.0f / C);
+        const float d0 = f0 - mean, d1 = f1 - mean, d2 = f2 - mean, d3 = f3 - mean;
+        float q = d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+#pragma unroll
+        for (int m = K::LPT / 2; m >= 1; m >>= 1) q += __shfl_xor(q, m, 64);
+        const float rstd = 1.0f / sqrtf(q * (1.0f / C) + eps);
+        const float4 egam = *reinterpret_cast<const float4*>(sEp + C + 4 * ec);
+        const float4 ebet = *reinterpret_cast<const float4*>(sEp + 2 * C + 4 * ec);
+        if (st)
+          *reinterpret_cast<f16x4*>(Yn + oo) = f16x4{(f16)(d0 * rstd * egam.x + ebet.x), (f16)(d1 * rstd * egam.y + ebet.y),
+                                                     (f16)(d2 * rstd * egam.z + ebet.z), (f16)(d3 * rstd * egam.w + ebet.w)};
+      }
+    };
+    // fc2 partial sums -> this wave's slab of buffer bb, then the workgroup barrier
+    auto slab_sync = [&](const f32x4 (&a2)[NC2], int bb) __attribute__((always_inline)) {
+      float* sl = slab0 + (bb * NW + w) * K::SLAB;
+#pragma unroll
+      for (int c = 0; c < NC2; ++c) *reinterpret_cast<f32x4*>(sl + fr * K::SROW + 16 * c + 4 * fq) = a2[c];
+      if (!(diag & 1)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    // Software pipeline over the strip's rows: row r issues the fc1 MFMAs of hidden row y + 2, writes the
+    // fc2 partial sums of row y - 1 (MFMAs issued a whole dwconv earlier) and runs its epilogue, then the
+    // dwconv + GELU + fc2 MFMAs of row y; the last row's reduction drains after the loop.
+    f32x4 a2[NC2];
+    // residual rows: loaded one row before the epilogue that consumes them (r0: even rows, r1: odd)
+    uint2 rs0 = *reinterpret_cast<const uint2*>(X + eoff0 + (long)min(y0, H - 1) * W * C), rs1 = {0u, 0u};
+    auto row = [&](int r, f16x8 (&xn)[KS], uint2& rs) __attribute__((always_inline)) {
+      const int y = y0 + r;
+      // dwconv 3x3 + bias + GELU of row y (n-tile j), straight into fc2's operand layout; the taps of
+      // n-tile j + 1 are read from LDS while n-tile j computes
+      f16x8 g[2];
+      uint4 tq[2][6];
+      auto tload = [&](int j, uint4 (&t)[6]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) t[i] = tpl[j * 4 * K::TBLK / 16 + i];
+      };
+      auto dwconv = [&](int j, const uint4 (&tb)[6]) __attribute__((always_inline)) {
+        if (diag & 4) {           // timing ablation: no depthwise conv (centre values only), GELU kept
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float v = (c & 1) ? hi16(win[1][j][c >> 1]) : lo16(win[1][j][c >> 1]);
+            g[j >> 1][4 * (j & 1) + c] = (_Float16)((diag & 8) ? v : gelu_rw(v));
+          }
+          return;
+        }
+        const uint32_t tw[18] = {tb[0].x, tb[0].y, tb[0].z, tb[0].w, tb[1].x, tb[1].y, tb[1].z, tb[1].w, tb[2].x,
+                                 tb[2].y, tb[2].z, tb[2].w, tb[3].x, tb[3].y, tb[3].z, tb[3].w, tb[4].x, tb[4].y};
+        float acc[4] = {__uint_as_float(tb[5].x), __uint_as_float(tb[5].y), __uint_as_float(tb[5].z),
+                        __uint_as_float(tb[5].w)};
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int p = 0; p < 2; ++p) {
+            const uint32_t c = win[dy][j][p], l = from_left(c), rt = from_right(c);
+            // tap t = 3 dy + dx of channel 2p (lo) / 2p + 1 (hi): word 2 t + p of the block
+            const uint32_t t0 = tw[2 * (3 * dy) + p], t1 = tw[2 * (3 * dy + 1) + p], t2 = tw[2 * (3 * dy + 2) + p];
+            acc[2 * p] = fmaf(lo16(l), lo16(t0), acc[2 * p]);
+            acc[2 * p] = fmaf(lo16(c), lo16(t1), acc[2 * p]);
+            acc[2 * p] = fmaf(lo16(rt), lo16(t2), acc[2 * p]);
+            acc[2 * p + 1] = fmaf(hi16(l), hi16(t0), acc[2 * p + 1]);
+            acc[2 * p + 1] = fmaf(hi16(c), hi16(t1), acc[2 * p + 1]);
+            acc[2 * p + 1] = fmaf(hi16(rt), hi16(t2), acc[2 * p + 1]);
+          }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)((diag & 8) ? acc[c] : gelu_rw(acc[c]));
+      };
+      tload(0, tq[0]);
+      // fc1 MFMAs of hidden row y + 2 (needed from the next row on), then prefetch row y + 3
+      f32x4 a1[4];
+      if (diag & 16) {            // timing ablation: no fc1 MFMAs
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        fc1_mma(w1f, xn, a1);
+      }
+      if (!(diag & 128)) load_x(y + 4, xn);   // (clamped)
+      // keep the loads here, a row ahead of their use (the scheduler would sink them to save registers)
+      __builtin_amdgcn_sched_barrier(0);
+      tload(1, tq[1]);
+      if (r > 0) {                // row y - 1: its fc2 results are long retired
+        slab_sync(a2, buf ^ 1);
+        epilogue(y - 1, rs, buf ^ 1);
+      }
+      if (!(diag & 128)) rs = *reinterpret_cast<const uint2*>(X + eoff0 + (long)min(y + 1, H - 1) * W * C);   // row y + 1's
+      dwconv(0, tq[0]);
+      tload(2, tq[0]);
+      dwconv(1, tq[1]);
+      tload(3, tq[1]);
+      dwconv(2, tq[0]);
+      dwconv(3, tq[1]);
+      // fc2 partial sums of this wave's 64 hidden channels (lane: channels 16 c + 4 fq + r, token fr)
+      if (diag & 32) {            // timing ablation: no fc2 MFMAs
+#pragma unroll
+        for (int c = 0; c < NC2; ++c) a2[c] = f32x4{(float)g[0][c], (float)g[1][c], 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int c = 0; c < NC2; ++c) {
+          a2[c] = mfma16x16x32(w2f[0][c], g[0], f32x4{0.f, 0.f, 0.f, 0.f});
+          a2[c] = mfma16x16x32(w2f[1][c], g[1], a2[c]);
+        }
+      }
+      // window roll: rows y, y + 1, and the new row y + 2 (its fc1 MFMAs have long retired)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int p = 0; p < 2; ++p) { win[0][j][p] = win[1][j][p]; win[1][j][p] = win[2][j][p]; }
+      fc1_pack(y + 2, a1, win[2]);
+      buf ^= 1;
+    };
+    static_assert(R % 2 == 0, "rows unrolled by 2");
+    for (int r = 0; r < R; r += 2) {
+      row(r, xA, rs1);            // even row: epilogue of the odd row before it (rs1), reloads rs1
+      row(r + 1, xB, rs0);
+    }
+    slab_sync(a2, buf ^ 1);
+    epilogue(y0 + R - 1, rs1, buf ^ 1);
+  }
+}
+
+template <class K>
+static int launch(const void* XN, const void* X, const void* W1, const float* b1, const float* taps, const float* dwb,
+                  const void* W2, const float* b2, void* Y, void* Yn, const float* gamma, const float* beta, float eps,
+                  int B, int H, hipStream_t st) {
+  const int nstrip = (H + K::R - 1) / K::R;
+  const long total = (long)B * nstrip * K::XT;
+  static int slots = 0;
+  if (!slots) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mixffn_rw<K>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              K::LDS);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&mixffn_rw<K>), K::NT, K::LDS);
+    slots = std::max(1, cus) * std::max(1, per);
+  }
+  if (total > 0x7fffffffL) { set_error("svk_mixffn_rw: too many strips"); return SVK_EINVAL; }
+  static const int g_diag = getenv("SVK_RW_DIAG") ? atoi(getenv("SVK_RW_DIAG")) : 0;   // timing ablations
+  static const int force = getenv("SVK_RW_GRID") ? atoi(getenv("SVK_RW_GRID")) : 0;   // debugging: grid size
+  const int grid = (int)std::min<long>(total, force > 0 ? force : slots);
+  hipLaunchKernelGGL((mixffn_rw<K>), dim3(grid), dim3(K::NT), K::LDS, st, (const f16*)XN, (const f16*)X, (const f16*)W1,
+                     b1, taps, dwb, (const f16*)W2, b2, (f16*)Y, (f16*)Yn, gamma, beta, eps, H, nstrip, (int)total, g_diag);
+  static char name[64];
+  if (!name[0]) snprintf(name, sizeof(name), "mixffn_rw<Cfg<%d, %d, %d>>", K::C, K::W, K::R);
+  set_last_kernel(name);
+  return check_launch("mixffn_rw");
+}
+
+}  // namespace ffnrw
+}  // namespace svk
+
+using namespace svk;
+
+extern "C" int svk_mixffn_rw_supported(int dtype, int W, int C) {
+  return dtype == SVK_F16 && W == 56 && C == 64;
+}
+
+extern "C" int svk_mixffn_rw(int dtype, const void* XN, const void* X, const void* W1, const float* b1, const float* taps,
+                             const float* dbias, const void* W2, const float* b2, void* Y, void* Yn, const float* gamma,
+                             const float* beta, float eps, int B, int H, int W, int C, void* stream) {
+  if (B < 0 || H <= 0 || !XN || !X || !W1 || !b1 || !taps || !dbias || !W2 || !b2 || (!Y && !gamma) ||
+      (gamma && (!beta || !Yn))) {
+    set_error("svk_mixffn_rw: bad args"); return SVK_EINVAL;
+  }
+  if ((((uintptr_t)XN) | ((uintptr_t)X) | ((uintptr_t)W1) | ((uintptr_t)W2) | ((uintptr_t)Y) | ((uintptr_t)Yn) |
+       ((uintptr_t)b1) | ((uintptr_t)b2) | ((uintptr_t)gamma) | ((uintptr_t)beta)) & 15) {
+    set_error("svk_mixffn_rw: pointers must be 16-byte aligned"); return SVK_EINVAL;
+  }
+  if (!svk_mixffn_rw_supported(dtype, W, C)) {
+    set_error("svk_mixffn_rw: (dtype=%d, W=%d, C=%d) not instantiated", dtype, W, C); return SVK_EUNSUPPORTED;
+  }
+  if (B == 0) return SVK_OK;
+  static const int var = getenv("SVK_RW_VAR") ? atoi(getenv("SVK_RW_VAR")) : 0;   // tuning variants
+  hipStream_t st = (hipStream_t)stream;
+  switch (var) {
+    case 1: return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 3>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+    case 2: return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+    case 3: return ffnrw::launch<ffnrw::Cfg<64, 56, 8, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+    default: return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  }
+}

@@ -79,6 +79,13 @@ class Mlp(nn.Module):
         p = get_packed(self, x.dtype, self._pack)
         B, N, C = x.shape
         hid = self.fc1.out_features
+        if (ops.MIXFFN_RW and residual is not None and hid == 4 * C and self.fc2.out_features == C
+                and ops.mixffn_rw_supported(x.dtype, W, C)):
+            # the same, with the depthwise window in registers (f16, stage 1)
+            pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
+            y = ops.mixffn_rw(x.contiguous().view(B, H, W, C), residual.contiguous().view(B, H, W, C),
+                              p["w1"], p["b1"], pd["taps"], pd["b"], p["w2"], p["b2"], ln=ln)
+            return y.view(B, N, C)
         if (ops.FUSED_MIXFFN and residual is not None and x.dtype in ops.H16 and hid == 4 * C
                 and self.fc2.out_features == C and ops.mixffn_supported(W, C)):
             # fc1 -> dwconv3x3 -> GELU -> fc2 -> + residual (-> LayerNorm) in one kernel, hidden on chip

@@ -371,6 +371,50 @@ def mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=None):
     return out
 
 
+MIXFFN_RW = os.environ.get("SVK_MIXFFN_RW", "1") == "1"
+
+
+def mixffn_rw_supported(dtype, W, C):
+    """True when svk_mixffn_rw (the register-window whole MixFFN) has an instantiation for the map dtype,
+    width W and channels C."""
+    return dtype in H16 and bool(_lib.load().svk_mixffn_rw_supported(dtype_code(dtype), int(W), int(C)))
+
+
+def mixffn_rw(xn, x, w1, b1, taps, dbias, w2, b2, ln=None):
+    """x + fc2(GELU(dwconv3x3(fc1(xn)))) on NHWC [B, H, W, C] f16 maps with the depthwise window held in
+    registers (svk_mixffn_rw); taps [9, 4C] / dbias [4C] f32 as DWConv packs them.  ``ln = (gamma, beta,
+    eps)`` returns the LayerNorm of that sum instead (the sum is then not written)."""
+    if xn.dtype not in H16:
+        raise _lib.SvkError("svk.mixffn_rw: f16 only")
+    for t, nm in ((xn, "xn"), (x, "x"), (w1, "w1"), (w2, "w2")):
+        _chk(t, nm, xn.dtype)
+        if not t.is_contiguous():
+            raise _lib.SvkError(f"svk.mixffn_rw: {nm} must be contiguous")
+    for t, nm in ((b1, "b1"), (b2, "b2"), (taps, "taps"), (dbias, "dbias")):
+        _chk(t, nm, torch.float32)
+        if not t.is_contiguous():
+            raise _lib.SvkError(f"svk.mixffn_rw: {nm} must be contiguous")
+    B, H, W, C = xn.shape
+    if (x.shape != xn.shape or w1.shape != (4 * C, C) or w2.shape != (C, 4 * C) or taps.shape != (9, 4 * C)
+            or b1.numel() != 4 * C or dbias.numel() != 4 * C or b2.numel() != C):
+        raise _lib.SvkError("svk.mixffn_rw: shape mismatch")
+    out = torch.empty_like(x)
+    g = bt = None
+    eps = 0.0
+    if ln is not None:
+        g, bt, eps = ln
+        _chk(g, "gamma", torch.float32); _chk(bt, "beta", torch.float32)
+    t0 = _prof_begin()
+    _lib.call("svk_mixffn_rw", dtype_code(xn.dtype), _p(xn), _p(x), _p(w1), _p(b1), _p(taps), _p(dbias), _p(w2),
+              _p(b2), None if ln is not None else _p(out), _p(out) if ln is not None else None, _p(g), _p(bt),
+              float(eps), B, H, W, C, _stream())
+    if t0 is not None:
+        M = B * H * W
+        _prof_end(t0, f"mixffn_rw<{C}>", 2.0 * M * C * 4 * C * 2 + 2.0 * 9 * M * 4 * C,
+                  (3 * M * C + 8 * C * C) * 2, (M, C, "mixffn_rw"))
+    return out
+
+
 FC1_DWCONV = os.environ.get("SVK_FC1_DWCONV", "1") == "1"
 
 

@@ -108,6 +108,18 @@ int svk_mixffn_fused(int dtype, const void* XN, const void* X, const void* W1, c
                      const void* W2, const float* b2, void* Y, void* Yn, const float* gamma, const float* beta,
                      float eps, int B, int H, int W, int C, void* stream);
 
+/* The same whole MixFFN (+ LayerNorm) as svk_mixffn_fused, f16, with the depthwise window in registers
+ * (csrc/mixffn_rw.hip: fc1's MFMA output layout is the conv layout — horizontal taps are neighbouring
+ * lanes, vertical taps the rows a lane computed before — and the GELU output is fc2's MFMA operand;
+ * the hidden channels split over the waves of a workgroup, whose fc2 partial sums meet in LDS once per
+ * image row).  Same operands as svk_mixffn_fused except the depthwise conv: taps [9][4C] f32 (row
+ * dy*3+dx) and dbias [4C] f32, rounded to f16 in the kernel.  Instantiated where
+ * svk_mixffn_rw_supported(dtype, W, C) (the MiT-b1..b5 stage-1 shape: W = 56, C = 64, f16). */
+int svk_mixffn_rw_supported(int dtype, int W, int C);
+int svk_mixffn_rw(int dtype, const void* XN, const void* X, const void* W1, const float* b1, const float* taps,
+                  const float* dbias, const void* W2, const float* b2, void* Y, void* Yn, const float* gamma,
+                  const float* beta, float eps, int B, int H, int W, int C, void* stream);
+
 /* MixFFN front half, G = act(dwconv3x3(XN W1^T + b1) + dbias) over NHWC maps (Mlp.fc1 -> DWConv -> GELU,
  * mix_transformer_evp.py:60-63, 24-30): the 4C-wide hidden map stays on chip (fc1 recomputed on one
  * halo row above / below each strip).  bf16, C in {32, 64, 128}, hidden % 64 == 0; W1 [hidden][C] bf16,

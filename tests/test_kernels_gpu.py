@@ -271,6 +271,42 @@ def test_dwconv3x3_gelu(cuda, dt, B, H, W, C):
     _close(got, F.gelu(ref).permute(0, 2, 3, 1), dt)
 
 
+@pytest.mark.parametrize("B,H,ln", [(2, 56, False), (2, 56, True), (1, 10, True), (3, 7, False), (5, 3, False),
+                                    (1, 15, True), (9, 28, False)])
+def test_mixffn_rw(cuda, B, H, ln):
+    """Register-window whole MixFFN (svk_mixffn_rw, f16, W = 56, C = 64) against fp64 torch on the same
+    rounded inputs (rounding points as test_mixffn_fused).  H = 10 / 7 / 3 / 15 leave partial strips
+    (rows past the map are masked, the window's halo rows are zero there); B = 9 gives more units than one
+    pass of the persistent grid when few CUs are free."""
+    from svk import ops
+    dt, W, C = torch.float16, 56, 64
+    assert ops.mixffn_rw_supported(dt, W, C)
+    xn = _rand(B, H, W, C, dt=dt, dev=cuda, seed=40)
+    x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=41)
+    w1 = _rand(4 * C, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=42)
+    b1 = _rand(4 * C, dt=torch.float32, dev=cuda, scale=0.1, seed=43)
+    taps = _rand(9, 4 * C, dt=torch.float32, dev=cuda, scale=0.3, seed=44)
+    db = _rand(4 * C, dt=torch.float32, dev=cuda, scale=0.1, seed=45)
+    w2 = _rand(C, 4 * C, dt=dt, dev=cuda, scale=(4 * C) ** -0.5, seed=46)
+    b2 = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=47)
+    gam = (1 + _rand(C, dt=torch.float32, dev=cuda, scale=0.2, seed=48)) if ln else None
+    bet = _rand(C, dt=torch.float32, dev=cuda, scale=0.1, seed=49) if ln else None
+    got = ops.mixffn_rw(xn, x, w1, b1, taps, db, w2, b2, ln=(gam, bet, 1e-6) if ln else None)
+    torch.cuda.synchronize()
+    h = (xn.cpu().double() @ w1.cpu().double().t() + b1.cpu().double()).to(dt).double()
+    hc = h.permute(0, 3, 1, 2)
+    k = taps.cpu().to(dt).double().t().reshape(4 * C, 1, 3, 3)
+    g = F.gelu(F.conv2d(hc, k, db.cpu().double(), padding=1, groups=4 * C)).permute(0, 2, 3, 1).to(dt).double()
+    ref = x.cpu().double() + g @ w2.cpu().double().t() + b2.cpu().double()
+    if ln:
+        ref = F.layer_norm(ref.to(dt).double(), (C,), gam.cpu().double(), bet.cpu().double(), 1e-6)
+    _close(got, ref, dt)
+    # the register-window kernel and the wave-specialised one compute the same rounded quantities
+    alt = ops.mixffn_fused(xn, x, w1, b1, ops.mixffn_pack_taps(taps, db, dt), w2, b2,
+                           ln=(gam, bet, 1e-6) if ln else None)
+    assert (got.float() - alt.float()).abs().max().item() <= 2e-2
+
+
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,H,W,C,ln", [(2, 56, 56, 64, False), (2, 56, 56, 32, False), (1, 10, 56, 64, True),
                                         (3, 7, 56, 32, True), (2, 56, 56, 64, True), (5, 3, 56, 64, False)])

@@ -25,6 +25,12 @@ def run(B, H, C, reps, only, dt=torch.float16):
     def fused():
         return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2)
 
+    def rw():
+        return ops.mixffn_rw(xn, x, w1, b1, taps, db, w2, b2)
+
+    def rw_ln():
+        return ops.mixffn_rw(xn, x, w1, b1, taps, db, w2, b2, ln=(b2 + 1, b2, 1e-6))
+
     def fused_ln():
         return ops.mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=(b2 + 1, b2, 1e-6))
 
@@ -51,11 +57,13 @@ def run(B, H, C, reps, only, dt=torch.float16):
         g = ops.dwconv3x3(h.view(B, H, H, 4 * C), taps, db, act="gelu")
         return ops.gemm(g.view(-1, 4 * C), w2, b2, residual=x.view(-1, C))
 
-    for name, fn in (("fused", fused), ("fused_relu", fused_relu), ("fused_nodw", fused_nodw),
+    for name, fn in (("rw", rw), ("rw_ln", rw_ln), ("fused", fused), ("fused_relu", fused_relu), ("fused_nodw", fused_nodw),
                      ("fused_noprod", fused_noprod), ("fused_ln", fused_ln), ("fc1dw", fc1dw), ("unfused", unfused)):
         if only and name != only:
             continue
         if name.startswith("fused") and not ops.mixffn_supported(H, C):
+            continue
+        if name.startswith("rw") and not ops.mixffn_rw_supported(dt, H, C):
             continue
         fn()
         torch.cuda.synchronize()
