@@ -59,6 +59,9 @@ struct PkCfg {
   static constexpr int WG_PER_CU = (160 * 1024) / LDS;
   static constexpr int OCC = WG_PER_CU * NT / 256 > 5 ? 5 : (WG_PER_CU * NT / 256 < 1 ? 1 : WG_PER_CU * NT / 256);
   static constexpr bool ELDS_FITS = BM * BN * 2 <= STAGE;    // the staged epilogue tile fits one stage
+  // big tiles (one workgroup per CU, accumulators in the AGPR half of the register file): the epilogue
+  // operands are loaded in the epilogue itself, block by block (held early they would not fit)
+  static constexpr bool LATE = BM * BN > 128 * 160;
   static_assert(A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "tile must split into whole DMA rounds");
   static_assert(LD <= 63, "vmcnt range");
 };
@@ -114,7 +117,7 @@ __device__ __forceinline__ void gload4(float& v, const char* src) {
 // reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
 template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
 __global__ __launch_bounds__(Cfg::NT, Cfg::OCC)
-void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
+void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int diag) {
   typedef v8_t<T> tx8;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
@@ -224,12 +227,14 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   // prefetch, they are covered by the last step's counted wait (vector-memory operations, LDS-DMA
   // included, retire in issue order), after which tie_epi() hands the registers back to the compiler.  Absent operands read the zero block (no branches).
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
-  f32x4 ebias[TN];
-  u32x2 eres[TM][TN], eu[EXT ? TM : 1][EXT ? TN : 1];
+  constexpr bool LATE = Cfg::LATE;
+  static_assert(!(LATE && (EXT || SPLIT)), "big tiles: plain epilogue only");
+  f32x4 ebias[LATE ? 1 : TN];
+  u32x2 eres[LATE ? 1 : TM][LATE ? 1 : TN], eu[EXT ? TM : 1][EXT ? TN : 1];
   float ers[EXT ? TM : 1];
   const T* R = static_cast<const T*>(p.R);
   auto epi_load = [&](int unit) {
-    if constexpr (!SPLIT) {
+    if constexpr (!SPLIT && !LATE) {
       const int m0 = (unit / ntn) * BM, n0 = (unit % ntn) * BN;
       const char* zero = reinterpret_cast<const char*>(g_pk_zero);
 #pragma unroll
@@ -256,6 +261,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
     }
   };
   auto tie_epi = [&]() {
+    if constexpr (LATE) return;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       asm volatile("" : "+v"(ebias[j]));
@@ -301,11 +307,23 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = n0 + wn * WN + j * 16 + fq * 4;
+      f32x4 bj;
+      if constexpr (LATE) {
+        const int nb = min(n, p.N - 4);
+        bj = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + nb) : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+        bj = ebias[j];
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int m = m0 + wm * WM + i * 16 + fr;
-        float v[4] = {acc[i][j][0] + ebias[j].x, acc[i][j][1] + ebias[j].y, acc[i][j][2] + ebias[j].z,
-                      acc[i][j][3] + ebias[j].w};
+        u32x2 rij;
+        if constexpr (LATE) {
+          rij = R ? *reinterpret_cast<const u32x2*>(R + (long)min(m, p.M - 1) * p.ldr + min(n, p.N - 4)) : u32x2{0u, 0u};
+        } else {
+          rij = eres[i][j];
+        }
+        float v[4] = {acc[i][j][0] + bj.x, acc[i][j][1] + bj.y, acc[i][j][2] + bj.z, acc[i][j][3] + bj.w};
         if constexpr (EXT) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], p.act) * ers[i];
@@ -321,7 +339,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
           for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
         }
         {                                  // zero block when there is no residual
-          const f32x2 r01 = unpack2<T>(eres[i][j].x), r23 = unpack2<T>(eres[i][j].y);
+          const f32x2 r01 = unpack2<T>(rij.x), r23 = unpack2<T>(rij.y);
           v[0] += r01.x;
           v[1] += r01.y;
           v[2] += r23.x;
@@ -332,7 +350,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
           const int row = wm * WM + i * 16 + fr, col = wn * WN + j * 16 + fq * 4;
           *reinterpret_cast<uint2*>(stile + row * (BN * 2) + (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col >> 2) & 1) * 8) =
               *reinterpret_cast<const uint2*>(o);
-        } else if (m < p.M && n < p.N) {   // N % 4 == 0: a 4-column group is all-in or all-out
+        } else if (m < p.M && n < p.N && !(diag & 2)) {   // N % 4 == 0: a 4-column group is all-in or all-out
           *reinterpret_cast<uint2*>(C + (long)m * p.ldc + n) = *reinterpret_cast<const uint2*>(o);
         }
       }
@@ -349,7 +367,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
         const int row = idx / CPR, c = idx % CPR;
         const uint4 v = *reinterpret_cast<const uint4*>(stile + row * (BN * 2) + ((c ^ (row & (CPR - 1))) << 4));
         const int m = m0 + row, n = n0 + c * 8;
-        if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
+        if (m < p.M && n < p.N && !(diag & 2)) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
       }
       barrier_mem();   // the next step's DMA overwrites this stage buffer
     }
@@ -404,6 +422,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       case SVK_ACT_TANH: epilogue(tile, std::integral_constant<int, SVK_ACT_TANH>{}); break;
       default: epilogue(tile, std::integral_constant<int, 0>{}); break;
     }
+    if (diag & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // timing ablation: drain the stores
   }
   // the last step's zero-block DMA is still in flight: retire it before the wave (and the workgroup's
   // LDS allocation) ends
@@ -440,7 +459,7 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
   hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
-                     (int)ntiles, nk, ks);
+                     (int)ntiles, nk, ks, g_tune[TUNE_PK_DIAG] > 0 ? g_tune[TUNE_PK_DIAG] : 0);
   static char name[112];
   if (!name[0])
     snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", type_name<T>(), Cfg::BM, Cfg::BN,
@@ -489,6 +508,8 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
 // Eligible: bf16, K-contiguous operands (16-byte aligned rows, K % 8 == 0; conv: Cin % 8 == 0),
 // plain epilogue, C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when
 // not eligible.  asrc: 0 dense A, 1 implicit-GEMM conv (A = NHWC map, GemmArgs conv geometry).
+static const int g_pk_policy = getenv("SVK_PK_POLICY") ? atoi(getenv("SVK_PK_POLICY")) : 1;   // 0: round-2 picks
+
 template <typename T>
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   const int force = g_tune[TUNE_PK_CFG];
@@ -515,6 +536,10 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
       cfg = (t128 < 512 && a.N <= 128) ? 30 : (a.N % 128 == 0 ? 20 : 10);
     } else {
       cfg = (big || (a.N % 128 == 0 && a.M < 32768)) ? 0 : 10;
+      // round 3 (profiles/r03/pk_cfg_sweep_elds.txt): 128 x 128 with the LDS-staged epilogue beats both the
+      // register-epilogue 128 x 128 and 128 x 64 wherever N % 128 == 0 and K >= 320 (s3 kv 15.7 -> 13.7 us,
+      // s4 fc1 50 -> 43, s4 kv 33 -> 29, s2 fc2 79 -> 70, head 80 -> 77, s3 fc1 91 -> 80)
+      if (g_pk_policy && a.N % 128 == 0 && a.K >= 320) cfg = 60;
       // (round-2 sweep: 128 x 128 for the stage-3 fc1 and 128 x 160 for its fc2 win 5-7 us each in
       // isolation but lost 2 % of the whole graph-replayed step: kept 128 x 64)
     }
@@ -540,6 +565,9 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 30: return launch_pk_k<T, PkCfg<64, 64, 2, 2, 2>, 0>(a, st, !big);
     case 40: return launch_pk_k<T, PkCfg<128, 160, 2, 2, 2>, 0>(a, st, false);
     case 50: return launch_pk_k<T, PkCfg<256, 128, 4, 2, 2>, 0>(a, st, false);
+    case 60: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, true);   // 128 x 128, staged epilogue
+    // (256 x 256 with 4 waves: 512 registers and ~15 VGPR spills, which the counted DMA waits cannot tolerate;
+    // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128: not instantiated)
     default: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
   }
 }

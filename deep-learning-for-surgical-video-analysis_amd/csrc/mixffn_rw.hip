@@ -11,10 +11,11 @@
 //
 //   * the MFMA layout IS the conv layout.  fc1 is computed transposed (D = W1 · XNᵀ, 16x16x32), so
 //     lane (fr, fq) ends with hidden channels 4fq .. 4fq+3 (of a 16-channel n-tile) of token fr, and a
-//     16-token m-tile is 16 consecutive pixels x0-1 .. x0+14 of one image row.  Horizontal taps are the
-//     neighbouring lanes (DPP row_shr:1 / row_shl:1 inside each 16-lane row), vertical taps are the
-//     previous / next image rows, which the same lane computed in earlier iterations: a 3-row rolling
-//     window of packed-f16 registers.  Lanes 0 and 15 are the halo columns (14 outputs per m-tile).
+//     16-token m-tile is 16 consecutive pixels x0-1 .. x0+14 of one image row.  Vertical taps are the
+//     previous / next image rows, which the same lane computed in earlier iterations (a 3-row rolling
+//     window, f16-rounded values held as f32); horizontal taps are the neighbouring lanes, read through
+//     v_fmac_f32's DPP source operand (row_shr:1 / row_shl:1 inside each 16-lane row): 9 full-rate
+//     FMAs per output, no shuffle instructions.  Lanes 0 and 15 are the halo columns (14 outputs each).
 //   * the GELU output lands directly in the fc2 operand layout: lane (fr, fq) holds 8 hidden values of
 //     token fr for each 32-channel k-step — fc2's reduction index is permuted to match (the W2
 //     fragments are gathered accordingly once, in the prologue).  fc2 is transposed too, so a lane ends
@@ -22,12 +23,16 @@
 //   * a workgroup = HID / 64 waves (4 for C = 64) splitting the hidden channels 64 each, so every wave
 //     keeps its W1 / W2 fragments in registers for the whole (persistent) kernel; the per-row fc2
 //     partial sums of the waves meet once in LDS (f32 slabs, double-buffered, ONE barrier per row),
-//     where each wave reduces a quarter of the tokens and runs the epilogue (+ b2 + residual, 16-byte
-//     wide LayerNorm rows over 16 lanes, 8-byte stores).
+//     where each wave reduces a quarter of the tokens and runs the epilogue (+ b2 + residual, LayerNorm
+//     over the 16 lanes holding a token, 8-byte stores).  The taps (f32, per n-tile and tap row) stream
+//     from LDS one step ahead of their use.
 //
-// Work unit: (frame, 14-column x-tile, strip of R rows); a wave walks the strip top to bottom
-// computing fc1 one row ahead (one halo row above the strip is recomputed).  Per row and wave:
-// 8 fc1 + 8 fc2 MFMAs and ~16 x 28 VALU (9 fma_mix taps, 3 DPP moves, GELU) per lane.
+// Work unit: (frame, 14-column x-tile, strip of R rows); a wave walks the strip top to bottom, software-
+// pipelined: row r issues the fc1 MFMAs of hidden row y + 2 and the X loads of row y + 3, then writes the
+// fc2 partial sums of row y - 1 and runs its epilogue, then the dwconv + GELU + fc2 MFMAs of row y.
+// Measured (B = 256, stage 1): 335 us vs 348 us for the wave-specialised mixffn_ws; rocprofv3 counters:
+// each wave issues VALU 44 % of its cycles at 2 waves per SIMD (233 VGPRs) — GELU and the dwconv taps are
+// ~60 % of the VALU instructions; the rest of the time is LDS / MFMA latency the two waves do not cover.
 // Numerics as mixffn.hip: fc1 output, taps and GELU output rounded to f16 (the reference's autocast
 // stores), accumulation / bias / GELU / LayerNorm statistics in f32.
 #include "svk_common.h"
@@ -46,7 +51,7 @@ struct Cfg {
   static constexpr int LPT = 64 / TPW;              // epilogue lanes per token (4 channels each)
   static constexpr int SROW = C + 4;                // slab row (floats): conflict-free 16-byte writes
   static constexpr int SLAB = 16 * SROW;            // one wave's partial sums of a row
-  static constexpr int TBLK = 96;                   // tap block (wave, n-tile, fq): taps [9][4] f16, pad, dwb [4] f32
+  static constexpr int TBLK = 160;                  // tap block (wave, n-tile, fq): taps [9][4], dwb [4] (f32)
   static constexpr int LDS_TP = HID * 4;             // b1 (f32) | tap blocks | b2, gamma, beta | slabs
   static constexpr int LDS_EP = LDS_TP + NW * 16 * TBLK;
   static constexpr int LDS_T = LDS_EP + 3 * C * 4;
@@ -62,6 +67,26 @@ __device__ __forceinline__ float hi16(uint32_t u) { return (float)__builtin_bit_
 // value of lane l - 1 / l + 1 inside each 16-lane row (0 at the row ends: halo lanes, never stored)
 __device__ __forceinline__ uint32_t from_left(uint32_t v) { return __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true); }
 __device__ __forceinline__ uint32_t from_right(uint32_t v) { return __builtin_amdgcn_update_dpp(0u, v, 0x101, 0xf, 0xf, true); }
+// acc[c] += h[x-1][c] t[c] + h[x][c] t[4+c] + h[x+1][c] t[8+c]: the horizontal neighbours come through
+// v_fmac_f32's DPP source operand (row_shr:1 / row_shl:1 within each 16-lane row, 0 at the row ends).
+// The four plain FMAs go first: they give the DPP reads of h the two wait states a VALU write needs.
+__device__ __forceinline__ void taps3(float (&acc)[4], const float (&h)[4], const float (&t)[12]) {
+  asm("v_fmac_f32 %0, %4, %12\n\t"    // centre taps t[4..7]
+      "v_fmac_f32 %1, %5, %13\n\t"
+      "v_fmac_f32 %2, %6, %14\n\t"
+      "v_fmac_f32 %3, %7, %15\n\t"
+      "v_fmac_f32_dpp %0, %4, %8 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %1, %5, %9 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %2, %6, %10 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %3, %7, %11 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %0, %4, %16 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %1, %5, %17 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %2, %6, %18 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_fmac_f32_dpp %3, %7, %19 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+      : "v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]), "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "v"(t[4]),
+        "v"(t[5]), "v"(t[6]), "v"(t[7]), "v"(t[8]), "v"(t[9]), "v"(t[10]), "v"(t[11]));
+}
 
 // gelu(x) = relu(x) - 0.5 |x| t q(t) exp(-x^2 / 2), 1 - erf(z) = t q(t) exp(-z^2) by Abramowitz & Stegun
 // 7.1.25 (|error| <= 2.5e-5, 40x below the f16 rounding of the output): 9 VALU + 2 transcendental
@@ -85,7 +110,7 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
                                                      const f16* __restrict__ W2, const float* __restrict__ b2,
                                                      f16* __restrict__ Y, f16* __restrict__ Yn,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                     float eps, int H, int nstrip, int total, int diag) {
+                                                     float eps, int H, int nstrip, int total) {
   constexpr int C = K::C, W = K::W, R = K::R, HID = K::HID, KS = K::KS, NC2 = K::NC2, NW = K::NW;
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   char* const smem = reinterpret_cast<char*>(smem4);
@@ -101,11 +126,11 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
   // 32 q + 4 fq + s (s < 4), 32 q + 16 + 4 fq + s - 4 (s >= 4)
   for (int e = tid; e < HID; e += K::NT) reinterpret_cast<float*>(smem)[e] = b1[e];
   for (int e = tid; e < NW * 16 * 40; e += K::NT) {
-    // block blk = (w * 4 + j) * 4 + fq holds channels 4 blk + c: element t * 4 + c of taps, then dwb
+    // block blk = (w * 4 + j) * 4 + fq holds channels 4 blk + c: float t * 4 + c = tap t (rounded to f16,
+    // as autocast casts the conv weight), then the depthwise bias
     const int blk = e / 40, r = e % 40, t = r / 4, c = r % 4;
-    char* bp = smem + K::LDS_TP + blk * K::TBLK;
-    if (t < 9) reinterpret_cast<f16*>(bp)[r] = (f16)taps[t * HID + 4 * blk + c];
-    else reinterpret_cast<float*>(bp + 80)[c] = dwb[4 * blk + c];
+    reinterpret_cast<float*>(smem + K::LDS_TP + blk * K::TBLK)[r] =
+        t < 9 ? (float)(f16)taps[t * HID + 4 * blk + c] : dwb[4 * blk + c];
   }
   f16x8 w1f[4][KS], w2f[2][NC2];
 #pragma unroll
@@ -153,16 +178,19 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
         for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(wf[j][ks], xf[ks], a[j]);
       }
     };
-    auto fc1_pack = [&](int yy, const f32x4 (&a)[4], uint32_t (&hw)[4][2]) __attribute__((always_inline)) {
+    // hidden values rounded to f16 (the autocast Linear output) and kept as f32: the depthwise taps then
+    // run as full-rate v_fmac_f32 with the horizontal shift folded in as a DPP operand
+    auto fc1_pack = [&](int yy, const f32x4 (&a)[4], float (&hw)[4][4]) __attribute__((always_inline)) {
       const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float4 bb = *reinterpret_cast<const float4*>(b1l + 16 * j);
-        hw[j][0] = pk(a[j][0] + bb.x, a[j][1] + bb.y) & m;
-        hw[j][1] = pk(a[j][2] + bb.z, a[j][3] + bb.w) & m;
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hw[j][c] = __uint_as_float(__float_as_uint((float)(f16)(a[j][c] + bv[c])) & m);
       }
     };
-    uint32_t win[3][4][2];
+    float win[3][4][4];
     {
       f16x8 xa[KS], xb[KS], xc[KS];
       f32x4 a[4];
@@ -176,11 +204,8 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
       fc1_mma(w1f, xc, a);
       fc1_pack(y0 + 1, a, win[2]);
     }
-    // X rows of the next two new hidden rows, two rows ahead (row-parity register sets: the loop is
-    // unrolled by 2 so that no in-flight load is ever copied)
-    f16x8 xA[KS], xB[KS];
-    load_x(y0 + 2, xA);
-    load_x(y0 + 3, xB);
+    f16x8 xn[KS];                 // X row of the next new hidden row (y + 2), prefetched a row ahead
+    load_x(y0 + 2, xn);
     // epilogue row operands: residual of (row, token et, channels 4 ec..)
     const int etx = x0 - 1 + et;
     const bool eok = et >= 1 && et <= 14 && etx < W;
@@ -199,7 +224,7 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
       const f16 o2 = (f16)(v.z + eb2.z + r23.x), o3 = (f16)(v.w + eb2.w + r23.y);
       const bool st = eok && yy < H;
       const long oo = eoff0 + (long)yy * W * C;
-      if (Y && st && !(diag & 64)) *reinterpret_cast<f16x4*>(Y + oo) = f16x4{o0, o1, o2, o3};
+      if (Y && st) *reinterpret_cast<f16x4*>(Y + oo) = f16x4{o0, o1, o2, o3};
       if (gamma) {   // LayerNorm of the token's C channels: LPT lanes (a power of two, aligned)
         const float f0 = o0, f1 = o1, f2 = o2, f3 = o3;
         float sm = f0 + f1 + f2 + f3;
@@ -223,104 +248,71 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
       float* sl = slab0 + (bb * NW + w) * K::SLAB;
 #pragma unroll
       for (int c = 0; c < NC2; ++c) *reinterpret_cast<f32x4*>(sl + fr * K::SROW + 16 * c + 4 * fq) = a2[c];
-      if (!(diag & 1)) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    };
+    // taps of (n-tile j, tap row dy): 12 floats [dx][c]
+    auto tload = [&](int jd, float (&t)[12]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const uint4 v = tpl[(jd / 3) * 4 * K::TBLK / 16 + (jd % 3) * 3 + i];
+        t[4 * i] = __uint_as_float(v.x); t[4 * i + 1] = __uint_as_float(v.y);
+        t[4 * i + 2] = __uint_as_float(v.z); t[4 * i + 3] = __uint_as_float(v.w);
+      }
     };
     // Software pipeline over the strip's rows: row r issues the fc1 MFMAs of hidden row y + 2, writes the
     // fc2 partial sums of row y - 1 (MFMAs issued a whole dwconv earlier) and runs its epilogue, then the
     // dwconv + GELU + fc2 MFMAs of row y; the last row's reduction drains after the loop.
     f32x4 a2[NC2];
-    // residual rows: loaded one row before the epilogue that consumes them (r0: even rows, r1: odd)
-    uint2 rs0 = *reinterpret_cast<const uint2*>(X + eoff0 + (long)min(y0, H - 1) * W * C), rs1 = {0u, 0u};
-    auto row = [&](int r, f16x8 (&xn)[KS], uint2& rs) __attribute__((always_inline)) {
+    uint2 res_prev = {0u, 0u};
+    for (int r = 0; r < R; ++r) {
       const int y = y0 + r;
-      // dwconv 3x3 + bias + GELU of row y (n-tile j), straight into fc2's operand layout; the taps of
-      // n-tile j + 1 are read from LDS while n-tile j computes
-      f16x8 g[2];
-      uint4 tq[2][6];
-      auto tload = [&](int j, uint4 (&t)[6]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) t[i] = tpl[j * 4 * K::TBLK / 16 + i];
-      };
-      auto dwconv = [&](int j, const uint4 (&tb)[6]) __attribute__((always_inline)) {
-        if (diag & 4) {           // timing ablation: no depthwise conv (centre values only), GELU kept
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const float v = (c & 1) ? hi16(win[1][j][c >> 1]) : lo16(win[1][j][c >> 1]);
-            g[j >> 1][4 * (j & 1) + c] = (_Float16)((diag & 8) ? v : gelu_rw(v));
-          }
-          return;
-        }
-        const uint32_t tw[18] = {tb[0].x, tb[0].y, tb[0].z, tb[0].w, tb[1].x, tb[1].y, tb[1].z, tb[1].w, tb[2].x,
-                                 tb[2].y, tb[2].z, tb[2].w, tb[3].x, tb[3].y, tb[3].z, tb[3].w, tb[4].x, tb[4].y};
-        float acc[4] = {__uint_as_float(tb[5].x), __uint_as_float(tb[5].y), __uint_as_float(tb[5].z),
-                        __uint_as_float(tb[5].w)};
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-          for (int p = 0; p < 2; ++p) {
-            const uint32_t c = win[dy][j][p], l = from_left(c), rt = from_right(c);
-            // tap t = 3 dy + dx of channel 2p (lo) / 2p + 1 (hi): word 2 t + p of the block
-            const uint32_t t0 = tw[2 * (3 * dy) + p], t1 = tw[2 * (3 * dy + 1) + p], t2 = tw[2 * (3 * dy + 2) + p];
-            acc[2 * p] = fmaf(lo16(l), lo16(t0), acc[2 * p]);
-            acc[2 * p] = fmaf(lo16(c), lo16(t1), acc[2 * p]);
-            acc[2 * p] = fmaf(lo16(rt), lo16(t2), acc[2 * p]);
-            acc[2 * p + 1] = fmaf(hi16(l), hi16(t0), acc[2 * p + 1]);
-            acc[2 * p + 1] = fmaf(hi16(c), hi16(t1), acc[2 * p + 1]);
-            acc[2 * p + 1] = fmaf(hi16(rt), hi16(t2), acc[2 * p + 1]);
-          }
-#pragma unroll
-        for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)((diag & 8) ? acc[c] : gelu_rw(acc[c]));
-      };
-      tload(0, tq[0]);
-      // fc1 MFMAs of hidden row y + 2 (needed from the next row on), then prefetch row y + 3
+      // this row's residual (its epilogue runs one row later), then the fc1 MFMAs of hidden row y + 2
+      // and the X row of hidden row y + 3, a row ahead of its use
+      const uint2 res = *reinterpret_cast<const uint2*>(X + eoff0 + (long)min(y, H - 1) * W * C);
       f32x4 a1[4];
-      if (diag & 16) {            // timing ablation: no fc1 MFMAs
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      } else {
-        fc1_mma(w1f, xn, a1);
-      }
-      if (!(diag & 128)) load_x(y + 4, xn);   // (clamped)
-      // keep the loads here, a row ahead of their use (the scheduler would sink them to save registers)
+      fc1_mma(w1f, xn, a1);
+      load_x(y + 3, xn);          // (clamped; unconditional: no branch for the waitcnt pass to merge)
+      // keep the loads here (the scheduler would sink them to save registers)
       __builtin_amdgcn_sched_barrier(0);
-      tload(1, tq[1]);
+      float tq[2][12];
+      tload(0, tq[0]);
       if (r > 0) {                // row y - 1: its fc2 results are long retired
         slab_sync(a2, buf ^ 1);
-        epilogue(y - 1, rs, buf ^ 1);
+        epilogue(y - 1, res_prev, buf ^ 1);
       }
-      if (!(diag & 128)) rs = *reinterpret_cast<const uint2*>(X + eoff0 + (long)min(y + 1, H - 1) * W * C);   // row y + 1's
-      dwconv(0, tq[0]);
-      tload(2, tq[0]);
-      dwconv(1, tq[1]);
-      tload(3, tq[1]);
-      dwconv(2, tq[0]);
-      dwconv(3, tq[1]);
-      // fc2 partial sums of this wave's 64 hidden channels (lane: channels 16 c + 4 fq + r, token fr)
-      if (diag & 32) {            // timing ablation: no fc2 MFMAs
+      // dwconv 3x3 + bias + GELU of row y, straight into fc2's operand layout; the taps of the next
+      // (n-tile, tap row) are read from LDS while the current one computes
+      f16x8 g[2];
 #pragma unroll
-        for (int c = 0; c < NC2; ++c) a2[c] = f32x4{(float)g[0][c], (float)g[1][c], 0.f, 0.f};
-      } else {
+      for (int j = 0; j < 4; ++j) {
+        const float4 db = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(tpl + j * 4 * K::TBLK / 16) + 36);
+        float acc[4] = {db.x, db.y, db.z, db.w};
 #pragma unroll
-        for (int c = 0; c < NC2; ++c) {
-          a2[c] = mfma16x16x32(w2f[0][c], g[0], f32x4{0.f, 0.f, 0.f, 0.f});
-          a2[c] = mfma16x16x32(w2f[1][c], g[1], a2[c]);
+        for (int dy = 0; dy < 3; ++dy) {
+          const int jd = 3 * j + dy;
+          if (jd + 1 < 12) tload(jd + 1, tq[(jd + 1) & 1]);
+          taps3(acc, win[dy][j], tq[jd & 1]);
         }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)gelu_rw(acc[c]);
+      }
+      // fc2 partial sums of this wave's 64 hidden channels (lane: channels 16 c + 4 fq + r, token fr)
+#pragma unroll
+      for (int c = 0; c < NC2; ++c) {
+        a2[c] = mfma16x16x32(w2f[0][c], g[0], f32x4{0.f, 0.f, 0.f, 0.f});
+        a2[c] = mfma16x16x32(w2f[1][c], g[1], a2[c]);
       }
       // window roll: rows y, y + 1, and the new row y + 2 (its fc1 MFMAs have long retired)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int p = 0; p < 2; ++p) { win[0][j][p] = win[1][j][p]; win[1][j][p] = win[2][j][p]; }
+        for (int c = 0; c < 4; ++c) { win[0][j][c] = win[1][j][c]; win[1][j][c] = win[2][j][c]; }
       fc1_pack(y + 2, a1, win[2]);
+      res_prev = res;
       buf ^= 1;
-    };
-    static_assert(R % 2 == 0, "rows unrolled by 2");
-    for (int r = 0; r < R; r += 2) {
-      row(r, xA, rs1);            // even row: epilogue of the odd row before it (rs1), reloads rs1
-      row(r + 1, xB, rs0);
     }
     slab_sync(a2, buf ^ 1);
-    epilogue(y0 + R - 1, rs1, buf ^ 1);
+    epilogue(y0 + R - 1, res_prev, buf ^ 1);
   }
 }
 
@@ -339,13 +331,13 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
                               K::LDS);
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&mixffn_rw<K>), K::NT, K::LDS);
     slots = std::max(1, cus) * std::max(1, per);
+    if (getenv("SVK_RW_VERBOSE")) fprintf(stderr, "mixffn_rw: %d CUs x %d workgroups, LDS %d B\n", cus, per, K::LDS);
   }
   if (total > 0x7fffffffL) { set_error("svk_mixffn_rw: too many strips"); return SVK_EINVAL; }
-  static const int g_diag = getenv("SVK_RW_DIAG") ? atoi(getenv("SVK_RW_DIAG")) : 0;   // timing ablations
   static const int force = getenv("SVK_RW_GRID") ? atoi(getenv("SVK_RW_GRID")) : 0;   // debugging: grid size
   const int grid = (int)std::min<long>(total, force > 0 ? force : slots);
   hipLaunchKernelGGL((mixffn_rw<K>), dim3(grid), dim3(K::NT), K::LDS, st, (const f16*)XN, (const f16*)X, (const f16*)W1,
-                     b1, taps, dwb, (const f16*)W2, b2, (f16*)Y, (f16*)Yn, gamma, beta, eps, H, nstrip, (int)total, g_diag);
+                     b1, taps, dwb, (const f16*)W2, b2, (f16*)Y, (f16*)Yn, gamma, beta, eps, H, nstrip, (int)total);
   static char name[64];
   if (!name[0]) snprintf(name, sizeof(name), "mixffn_rw<Cfg<%d, %d, %d>>", K::C, K::W, K::R);
   set_last_kernel(name);
@@ -378,10 +370,7 @@ extern "C" int svk_mixffn_rw(int dtype, const void* XN, const void* X, const voi
   if (B == 0) return SVK_OK;
   static const int var = getenv("SVK_RW_VAR") ? atoi(getenv("SVK_RW_VAR")) : 0;   // tuning variants
   hipStream_t st = (hipStream_t)stream;
-  switch (var) {
-    case 1: return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 3>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
-    case 2: return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
-    case 3: return ffnrw::launch<ffnrw::Cfg<64, 56, 8, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
-    default: return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
-  }
+  // strips of 28 rows (two per 56-row frame): measured 335 us vs 341 (14 rows), 342 (8 rows) at B = 256
+  if (var == 1) return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
 }

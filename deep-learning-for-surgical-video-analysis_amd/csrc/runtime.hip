@@ -31,13 +31,13 @@ int check_launch(const char* what) {
 
 // Tuning knobs (tile configuration / kernel variant overrides for A/B measurements in one process);
 // initial values from the environment, -1 = automatic choice.
-static const char* const k_knob_names[TUNE_NKNOBS] = {"pk_cfg", "pk_elds", "dw_lds", "dw_rows", "ffn_diag"};
-static const char* const k_knob_env[TUNE_NKNOBS] = {"SVK_PK_CFG", "SVK_PK_ELDS", "SVK_DW_LDS", "SVK_DW_LR", "SVK_FFN_DIAG"};
+static const char* const k_knob_names[TUNE_NKNOBS] = {"pk_cfg", "pk_elds", "dw_lds", "dw_rows", "ffn_diag", "pk_diag"};
+static const char* const k_knob_env[TUNE_NKNOBS] = {"SVK_PK_CFG", "SVK_PK_ELDS", "SVK_DW_LDS", "SVK_DW_LR", "SVK_FFN_DIAG", "SVK_PK_DIAG"};
 static int init_knob(int i) {
   const char* e = getenv(k_knob_env[i]);
   return e ? atoi(e) : -1;
 }
-int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3), init_knob(4)};
+int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3), init_knob(4), init_knob(5)};
 
 }  // namespace svk
 

@@ -22,7 +22,7 @@ namespace svk {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // Tuning knobs set through svk_tune (runtime.hip); -1 = automatic.
-enum { TUNE_PK_CFG = 0, TUNE_PK_ELDS = 1, TUNE_DW_LDS = 2, TUNE_DW_ROWS = 3, TUNE_FFN_DIAG = 4, TUNE_NKNOBS = 5 };
+enum { TUNE_PK_CFG = 0, TUNE_PK_ELDS = 1, TUNE_DW_LDS = 2, TUNE_DW_ROWS = 3, TUNE_FFN_DIAG = 4, TUNE_PK_DIAG = 5, TUNE_NKNOBS = 6 };
 extern int g_tune[TUNE_NKNOBS];
 // Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
 void set_last_kernel(const char* name);
