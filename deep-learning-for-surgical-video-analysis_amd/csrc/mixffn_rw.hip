@@ -316,6 +316,138 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
   }
 }
 
+// ---- MixFFN front half in the same register-window form: G = GELU(dwconv3x3(fc1(XN))) written to HBM
+// (stage 2, C = 128, hidden 512: the whole-MixFFN form would need 128 weight VGPRs per wave).  A wave owns
+// 64 hidden channels of a (frame, 14-column x-tile, R-row strip); a workgroup = 4 waves = 256 channels
+// and keeps its W1 fragments in registers and its taps / b1 in LDS for the whole persistent kernel (it
+// walks only units of its own hidden block).  No cross-wave reduction, no per-row barrier.  Per row and
+// wave: 4 KS fc1 MFMAs (hidden row y + 2, X loaded a row ahead), the 3x3 taps as DPP-fused v_fmac (taps
+// streamed from LDS one step ahead), GELU, 8-byte f16 stores of the 4 x 4 channels of the lane's token.
+template <int C_, int W_, int R_>
+struct DwCfg {
+  static constexpr int C = C_, W = W_, R = R_;
+  static constexpr int KS = C / 32, XT = (W + 13) / 14, NT = 256;
+  static constexpr int TBLK = 160;                  // tap block (wave, n-tile, fq): taps [9][4], dwb [4] (f32)
+  static constexpr int LDS_TP = 256 * 4;            // b1 of the workgroup's 256 channels | tap blocks
+  static constexpr int LDS = LDS_TP + 4 * 16 * TBLK;
+};
+
+template <class K>
+__global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN, const f16* __restrict__ W1,
+                                                    const float* __restrict__ b1, const float* __restrict__ taps,
+                                                    const float* __restrict__ dwb, f16* __restrict__ G, int H,
+                                                    int hid, int nstrip, int nspatial) {
+  constexpr int C = K::C, W = K::W, R = K::R, KS = K::KS;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  char* const smem = reinterpret_cast<char*>(smem4);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nhb = hid / 256, hb = blockIdx.x % nhb, ch0 = 256 * hb;   // this workgroup's hidden block
+  for (int e = tid; e < 256; e += K::NT) reinterpret_cast<float*>(smem)[e] = b1[ch0 + e];
+  for (int e = tid; e < 4 * 16 * 40; e += K::NT) {
+    const int blk = e / 40, r = e % 40, t = r / 4, c = r % 4;   // channel ch0 + 4 blk + c
+    reinterpret_cast<float*>(smem + K::LDS_TP + blk * K::TBLK)[r] =
+        t < 9 ? (float)(f16)taps[t * hid + ch0 + 4 * blk + c] : dwb[ch0 + 4 * blk + c];
+  }
+  f16x8 w1f[4][KS];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      w1f[j][ks] = *reinterpret_cast<const f16x8*>(W1 + (long)(ch0 + 64 * w + 16 * j + fr) * C + 32 * ks + 8 * fq);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  const float* b1l = reinterpret_cast<const float*>(smem) + 64 * w + 4 * fq;
+  const uint4* tpl = reinterpret_cast<const uint4*>(smem + K::LDS_TP + (w * 16 + fq) * K::TBLK);
+  const int gs = gridDim.x / nhb;                       // workgroups per hidden block (host: grid % nhb == 0)
+  for (int u = blockIdx.x / nhb; u < nspatial; u += gs) {
+    const int xt = u % K::XT, rest = u / K::XT, sidx = rest % nstrip, b = rest / nstrip;
+    const int y0 = sidx * R, x0 = 14 * xt;
+    const int tx = x0 - 1 + fr;
+    const bool xok = tx >= 0 && tx < W;
+    const bool sok = fr >= 1 && fr <= 14 && tx < W;     // this lane's token is stored
+    const f16* XNb = XN + (long)b * H * W * C + (long)min(max(tx, 0), W - 1) * C + 8 * fq;
+    f16* Gb = G + ((long)b * H * W + min(max(tx, 0), W - 1)) * hid + ch0 + 64 * w + 4 * fq;
+    auto load_x = [&](int yy, f16x8 (&xf)[KS]) __attribute__((always_inline)) {
+      const f16* src = XNb + (long)min(max(yy, 0), H - 1) * W * C;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xf[ks] = *reinterpret_cast<const f16x8*>(src + 32 * ks);
+    };
+    auto fc1_mma = [&](const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(w1f[j][ks], xf[ks], a[j]);
+      }
+    };
+    auto fc1_pack = [&](int yy, const f32x4 (&a)[4], float (&hw)[4][4]) __attribute__((always_inline)) {
+      const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 bb = *reinterpret_cast<const float4*>(b1l + 16 * j);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hw[j][c] = __uint_as_float(__float_as_uint((float)(f16)(a[j][c] + bv[c])) & m);
+      }
+    };
+    auto tload = [&](int jd, float (&t)[12]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const uint4 v = tpl[(jd / 3) * 4 * K::TBLK / 16 + (jd % 3) * 3 + i];
+        t[4 * i] = __uint_as_float(v.x); t[4 * i + 1] = __uint_as_float(v.y);
+        t[4 * i + 2] = __uint_as_float(v.z); t[4 * i + 3] = __uint_as_float(v.w);
+      }
+    };
+    float win[3][4][4];
+    {
+      f16x8 xa[KS], xb[KS], xc[KS];
+      f32x4 a[4];
+      load_x(y0 - 1, xa);
+      load_x(y0, xb);
+      load_x(y0 + 1, xc);
+      fc1_mma(xa, a);
+      fc1_pack(y0 - 1, a, win[0]);
+      fc1_mma(xb, a);
+      fc1_pack(y0, a, win[1]);
+      fc1_mma(xc, a);
+      fc1_pack(y0 + 1, a, win[2]);
+    }
+    f16x8 xn[KS];
+    load_x(y0 + 2, xn);
+    for (int r = 0; r < R; ++r) {
+      const int y = y0 + r;
+      f32x4 a1[4];
+      fc1_mma(xn, a1);
+      load_x(y + 3, xn);
+      __builtin_amdgcn_sched_barrier(0);
+      float tq[2][12];
+      tload(0, tq[0]);
+      f16* gy = Gb + (long)min(y, H - 1) * W * hid;
+      const bool st = sok && y < H;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 db = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(tpl + j * 4 * K::TBLK / 16) + 36);
+        float acc[4] = {db.x, db.y, db.z, db.w};
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          const int jd = 3 * j + dy;
+          if (jd + 1 < 12) tload(jd + 1, tq[(jd + 1) & 1]);
+          taps3(acc, win[dy][j], tq[jd & 1]);
+        }
+        if (st)
+          *reinterpret_cast<f16x4*>(gy + 16 * j) =
+              f16x4{(f16)gelu_rw(acc[0]), (f16)gelu_rw(acc[1]), (f16)gelu_rw(acc[2]), (f16)gelu_rw(acc[3])};
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) { win[0][j][c] = win[1][j][c]; win[1][j][c] = win[2][j][c]; }
+      fc1_pack(y + 2, a1, win[2]);
+    }
+  }
+}
+
 template <class K>
 static int launch(const void* XN, const void* X, const void* W1, const float* b1, const float* taps, const float* dwb,
                   const void* W2, const float* b2, void* Y, void* Yn, const float* gamma, const float* beta, float eps,
@@ -345,6 +477,32 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
 }
 
 }  // namespace ffnrw
+
+// svk_mixffn_fc1_dwconv's f16 GELU path for the instantiated shapes; 1 = not eligible
+int fc1dw_rw_try(int dtype, const void* XN, const void* W1, const float* b1, const float* taps, const float* dbias,
+                 void* G, int B, int H, int W, int C, int hidden, int act, hipStream_t st) {
+  using K = ffnrw::DwCfg<128, 28, 28>;
+  if (dtype != SVK_F16 || act != SVK_ACT_GELU || W != K::W || C != K::C || hidden % 256 || B <= 0 ||
+      ((((uintptr_t)b1) | ((uintptr_t)dbias) | ((uintptr_t)taps)) & 15) || getenv("SVK_NO_FC1DW_RW"))
+    return 1;
+  const int nstrip = (H + K::R - 1) / K::R, nhb = hidden / 256;
+  const long nspatial = (long)B * nstrip * K::XT;
+  static int slots = 0;
+  if (!slots) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&ffnrw::fc1dw_rw<K>), K::NT,
+                                                       K::LDS);
+    slots = std::max(1, cus) * std::max(1, per);
+  }
+  if (nspatial * nhb > 0x7fffffffL) return 1;
+  const int grid = (int)std::min<long>(nspatial, std::max(1, slots / nhb)) * nhb;
+  hipLaunchKernelGGL((ffnrw::fc1dw_rw<K>), dim3(grid), dim3(K::NT), K::LDS, st, (const f16*)XN, (const f16*)W1, b1, taps,
+                     dbias, (f16*)G, H, hidden, nstrip, (int)nspatial);
+  set_last_kernel("fc1dw_rw<DwCfg<128, 28, 28>>");
+  return check_launch("fc1dw_rw");
+}
 }  // namespace svk
 
 using namespace svk;

@@ -755,6 +755,7 @@ extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, 
     return SVK_EUNSUPPORTED;
   }
   if (B == 0) return SVK_OK;
+  if (fc1dw_rw_try(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, (hipStream_t)stream) == 0) return SVK_OK;
   // strip height: halo tile <= 44 KiB (measured best at B = 256 against 48 KiB for W1 + tile), strips
   // of equal height; the svk_tune "dw_rows" knob overrides it
   int rmax = std::max(1, std::min(H, 45056 / ((W + 2) * 128) - 2));

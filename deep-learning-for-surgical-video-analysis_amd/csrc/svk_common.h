@@ -35,6 +35,10 @@ int wgrad_batched(int dtype, const void* dY, long ldy, long sa_o, long sa_i, con
                   long sx_i, float* dW, long lddw, long sw_o, long sw_i, int Z, int nzi, int M, int N, int K,
                   hipStream_t st);
 
+// mixffn_rw.hip: register-window fc1 + dwconv3x3 + GELU (f16, stage-2 shape); returns 1 when not eligible
+int fc1dw_rw_try(int dtype, const void* XN, const void* W1, const float* b1, const float* taps, const float* dbias,
+                 void* G, int B, int H, int W, int C, int hidden, int act, hipStream_t st);
+
 __device__ __forceinline__ float to_f(float x) { return x; }
 __device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
 __device__ __forceinline__ float to_f(f16 x) { return (float)x; }

@@ -520,7 +520,8 @@ def test_conv2d_ln_sequence_reduction(cuda, dt, B, H, Cin, r):
 
 
 @pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (3, 28, 28, 128), (2, 14, 14, 128), (4, 7, 7, 64),
-                                     (1, 9, 13, 32), (2, 30, 17, 64)])
+                                     (1, 9, 13, 32), (2, 30, 17, 64), (9, 28, 28, 128), (2, 13, 28, 128),
+                                     (1, 33, 28, 128)])
 @pytest.mark.parametrize("dt", H16)
 def test_mixffn_fc1_dwconv(cuda, B, H, W, C, dt):
     """fc1 -> dwconv3x3 -> GELU in one kernel (hidden kept on chip) against the unfused svk kernels
