@@ -476,6 +476,35 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ X, T* __restrict__
   }
 }
 
+// 4 pixels per thread (H*W % 4 == 0, C <= 8, Cpad == 8): one float4 load per channel plane and four
+// 16-byte NHWC stores, so a wave moves 1 KB per instruction instead of 256 B (the input packing of
+// frames / flow runs at the HBM rate instead of the one-pixel kernel's load-issue rate)
+template <typename T>
+__global__ __launch_bounds__(256) void nchw_to_nhwc8_x4_kernel(const float* __restrict__ X, T* __restrict__ Y, int C,
+                                                              long hw, long npix4) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= npix4) return;
+  const long pix = q * 4, b = pix / hw, p = pix - b * hw;
+  const float* src = X + b * C * hw + p;
+  float v[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if (c < C) {
+      const float4 f = *reinterpret_cast<const float4*>(src + (long)c * hw);
+      v[c][0] = f.x; v[c][1] = f.y; v[c][2] = f.z; v[c][3] = f.w;
+    } else {
+      v[c][0] = v[c][1] = v[c][2] = v[c][3] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    T o[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) o[c] = from_f<T>(v[c][k]);
+    store_vec8(Y + (pix + k) * 8, o);
+  }
+}
+
 // ---- GaussianFilter.conv_gauss: reflect pad 2 + binomial 5x5 / 256 (mix_transformer_evp.py:501-514)
 __device__ __forceinline__ int reflect(int i, int n) {
   if (i < 0) i = -i;
@@ -555,7 +584,7 @@ __global__ void gauss5x5_kernel(const float* __restrict__ X, T* __restrict__ Y, 
 // owns 4 consecutive columns x GR rows; each input row piece is three aligned float4 loads (columns x0 - 4 ..
 // x0 + 7, reflected at the image edges from the middle block) instead of 5 scalar loads per column, and
 // each output pixel leaves as one 16-byte store.  Same arithmetic order as gauss5x5_kernel (bitwise equal).
-template <typename T>
+template <typename T, int GR>
 __global__ __launch_bounds__(256) void gauss5x5_x4_kernel(const float* __restrict__ X, T* __restrict__ Y, int B, int C, int H, int W,
                                    int nstrip) {
   const int W4 = W >> 2;
@@ -791,6 +820,13 @@ extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, i
   if (B < 0 || C <= 0 || Cpad < C || H <= 0 || W <= 0 || !X || !Y) { set_error("svk_nchw_to_nhwc: bad args"); return SVK_EINVAL; }
   if (B == 0) return SVK_OK;
   const long n = (long)B * H * W;   // one thread per pixel
+  if (Cpad == 8 && ((long)H * W) % 4 == 0 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0) {
+    SVK_DISPATCH_DTYPE(dtype_out, T, {
+      hipLaunchKernelGGL((nchw_to_nhwc8_x4_kernel<T>), grid1d(n / 4), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, C,
+                         (long)H * W, n / 4);
+      return check_launch("nchw_to_nhwc");
+    });
+  }
   SVK_DISPATCH_DTYPE(dtype_out, T, {
     hipLaunchKernelGGL((nchw_to_nhwc_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W, Cpad);
     return check_launch("nchw_to_nhwc");
@@ -806,9 +842,18 @@ extern "C" int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int 
   const int nstrip = (H + GR - 1) / GR;
   const long n = (long)B * nstrip * W;   // one thread per (column, strip of GR rows)
   if (W % 4 == 0 && W >= 8 && C <= 3 && Cpad == 8 && ((uintptr_t)X & 15) == 0 && ((uintptr_t)Y & 15) == 0) {
+    // rows per thread: 4 measured 169 us vs 179 (8) and 269 (16) at B = 256 (tools/pack_bench.py)
+    static const int gr = getenv("SVK_GAUSS_GR") ? atoi(getenv("SVK_GAUSS_GR")) : 4;
     SVK_DISPATCH_DTYPE(dtype_out, T, {
-      hipLaunchKernelGGL((gauss5x5_x4_kernel<T>), grid1d(n / 4), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H,
-                         W, nstrip);
+      auto go = [&](auto g) {
+        constexpr int G = decltype(g)::value;
+        const int ns = (H + G - 1) / G;
+        hipLaunchKernelGGL((gauss5x5_x4_kernel<T, G>), grid1d((long)B * ns * W / 4), dim3(256), 0, (hipStream_t)stream, X,
+                           (T*)Y, B, C, H, W, ns);
+      };
+      if (gr == 4) go(std::integral_constant<int, 4>{});
+      else if (gr == 16) go(std::integral_constant<int, 16>{});
+      else go(std::integral_constant<int, 8>{});
       return check_launch("gauss5x5_reflect");
     });
   }
