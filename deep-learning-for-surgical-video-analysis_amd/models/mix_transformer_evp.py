@@ -15,6 +15,7 @@ torch.float16 / torch.bfloat16 -> 16-bit MFMA with f32 accumulation), default: t
 dtype inside a CUDA autocast region (float16, as the reference's train_evp.py:493/637/760
 regions use), else f32 (generate_evp_LFB.py / trans_SV_output.py run fp32).  Eval-mode forward only (see models._common.check_inference).
 """
+import os
 from functools import partial
 
 import torch
@@ -563,14 +564,41 @@ class MixVisionTransformerEVP(nn.Module):
             from svk.train import autograd_forward
             return autograd_forward(self, x, y, flow, compute_dtype(self))
         check_inference(self, x, y, flow)
+        side = None
+        self._propagate_dtype(compute_dtype(self))   # (also done by _stages; the flow branch may start first)
+        if flow is not None and FLOW_STREAM:
+            # the flow encoder (input packing + 4 convs, ~5 % of the step) depends only on the flow input:
+            # it runs on a side stream concurrently with stages 1-3 (a parallel branch of a captured graph),
+            # filling their launch gaps and last-wave tails; joined before the stage-3 cross-attention
+            main = torch.cuda.current_stream(flow.device)
+            side = _side_stream(flow.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                f3, f4 = self.flow_encoder(flow)
         outs = self._stages(x, y)
         if flow is not None:
-            f3, f4 = self.flow_encoder(flow)
+            if side is not None:
+                main.wait_stream(side)
+                f3.record_stream(main)
+                f4.record_stream(main)
+            else:
+                f3, f4 = self.flow_encoder(flow)
             c3, H3, W3 = outs[2]
             outs[2] = (self.cross_attn_s3(c3, f3), H3, W3)
             c4, H4, W4 = outs[3]
             outs[3] = (self.cross_attn_s4(c4, f4), H4, W4)
         return self.head.forward_tokens(outs, return_features=return_features)
+
+
+FLOW_STREAM = os.environ.get("SVK_FLOW_STREAM", "1") == "1"
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
 
 
 def _variant(embed_dims, depths):
