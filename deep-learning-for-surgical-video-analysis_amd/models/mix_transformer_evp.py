@@ -518,17 +518,21 @@ class MixVisionTransformerEVP(nn.Module):
                 m.svk_dtype = dt
 
     # -- forward --------------------------------------------------------------------------------------
-    def _stages(self, x, y):
-        """Token-level forward_features: returns [(tokens [B, H*W, C], H, W)] for the 4 stages."""
+    def _stages(self, x, y, hcs=None, hc_ready=None):
+        """Token-level forward_features: returns [(tokens [B, H*W, C], H, W)] for the 4 stages.  ``hcs``:
+        handcrafted prompt maps computed elsewhere (a side stream), usable once ``hc_ready`` (an event)."""
         dt = compute_dtype(self)
         self._propagate_dtype(dt)
         x = x.reshape(-1, 3, x.shape[-2], x.shape[-1])
-        y = y.reshape(-1, 3, y.shape[-2], y.shape[-1])
-        hcs = self.prompt_generator.init_prompts(y)
+        if hcs is None:
+            y = y.reshape(-1, 3, y.shape[-2], y.shape[-1])
+            hcs = self.prompt_generator.init_prompts(y)
         h = to_nhwc(x, dt)
         outs = []
         for s in range(4):
             t, H, W = getattr(self, f"patch_embed{s + 1}").embed_nhwc(h)
+            if s == 0 and hc_ready is not None:
+                torch.cuda.current_stream(t.device).wait_event(hc_ready)
             prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1)
             norm = getattr(self, f"norm{s + 1}")
             pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
@@ -567,20 +571,28 @@ class MixVisionTransformerEVP(nn.Module):
         side = None
         self._propagate_dtype(compute_dtype(self))   # (also done by _stages; the flow branch may start first)
         if flow is not None and FLOW_STREAM:
-            # the flow encoder (input packing + 4 convs, ~5 % of the step) depends only on the flow input:
-            # it runs on a side stream concurrently with stages 1-3 (a parallel branch of a captured graph),
-            # filling their launch gaps and last-wave tails; joined before the stage-3 cross-attention
+            # the handcrafted prompt cascade (Gaussian filter + 4 patch embeds of the segmap) and the flow
+            # encoder (input packing + 4 convs) depend only on the segmap / flow inputs: together ~9 % of the
+            # step, they run on a side stream (a parallel branch of a captured graph) concurrently with the
+            # main stream's patch embedding and stages 1-3, filling launch gaps and last-wave tails; the main
+            # stream waits for the prompts at stage 1's first block and for the flow before the stage-3
+            # cross-attention
             main = torch.cuda.current_stream(flow.device)
             side = _side_stream(flow.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
+                hcs = self.prompt_generator.init_prompts(y.reshape(-1, 3, y.shape[-2], y.shape[-1]))
+                hc_ready = torch.cuda.Event()
+                hc_ready.record(side)
                 f3, f4 = self.flow_encoder(flow)
-        outs = self._stages(x, y)
+            outs = self._stages(x, y, hcs=tuple(hcs), hc_ready=hc_ready)
+        else:
+            outs = self._stages(x, y)
         if flow is not None:
             if side is not None:
                 main.wait_stream(side)
-                f3.record_stream(main)
-                f4.record_stream(main)
+                for t in (f3, f4) + tuple(h for h in hcs if h is not None):
+                    t.record_stream(main)
             else:
                 f3, f4 = self.flow_encoder(flow)
             c3, H3, W3 = outs[2]
