@@ -567,7 +567,9 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 50: return launch_pk_k<T, PkCfg<256, 128, 4, 2, 2>, 0>(a, st, false);
     case 60: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, true);   // 128 x 128, staged epilogue
     // (256 x 256 with 4 waves: 512 registers and ~15 VGPR spills, which the counted DMA waits cannot tolerate;
-    // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128: not instantiated)
+    // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128, and 256 x 256 with 8 waves of
+    // 128 x 64 (225 VGPRs, one workgroup per CU) 1.2-2x slower: per-tile prologue / epilogue / store drain
+    // are no longer covered by a second workgroup; not instantiated)
     default: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, !reg_epi);
   }
 }
