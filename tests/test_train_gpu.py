@@ -190,6 +190,32 @@ def test_attention_bwd(cuda, dt, Nq, Nk, heads, hd):
     _close(dkv[:, :, C:], vr.grad, tol)
 
 
+@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("B,Nq,Nk,heads,hd", [(3, 3136, 49, 8, 64), (5, 257, 49, 5, 64), (4, 700, 33, 6, 32)])
+def test_attention_bwd_fused_multichunk(cuda, monkeypatch, fused, B, Nq, Nk, heads, hd):
+    """The fused bf16 backward (<= 64 keys) with several 64-query chunks per workgroup and a partial last
+    chunk: dQ, dK, dV against fp64 autograd (dK / dV are reduced in registers over a workgroup's chunks and
+    across workgroups by f32 atomics)."""
+    from svk import ops
+    monkeypatch.setenv("SVK_ATTN_BWD_FUSED", fused)   # read by svk_attention_bwd at every call
+    dt, C = torch.bfloat16, heads * hd
+    q, k, v = _rand(B, Nq, C, seed=11), _rand(B, Nk, C, seed=12), _rand(B, Nk, C, seed=13)
+    do = _rand(B, Nq, C, seed=14)
+    scale = hd ** -0.5
+    qr, kr, vr = (t.to(dt).double().requires_grad_(True) for t in (q, k, v))
+    sp = lambda t, n: t.reshape(B, n, heads, hd).transpose(1, 2)
+    a = (sp(qr, Nq) @ sp(kr, Nk).transpose(-1, -2) * scale).softmax(-1)
+    o = (a @ sp(vr, Nk)).transpose(1, 2).reshape(B, Nq, C)
+    o.backward(do.to(dt).double())
+    qc, kc, vc = (t.to(cuda, dt) for t in (q, k, v))
+    oc = ops.attention(qc, kc, vc, heads, scale)
+    dkv = torch.zeros(B, Nk, 2 * C, device=cuda, dtype=dt)
+    dq, _, _ = ops.attention_bwd(qc, kc, vc, oc, do.to(cuda, dt), heads, scale, dkv[:, :, :C], dkv[:, :, C:])
+    _close(dq, qr.grad, 3e-2)
+    _close(dkv[:, :, :C], kr.grad, 3e-2)
+    _close(dkv[:, :, C:], vr.grad, 3e-2)
+
+
 def test_phase_loss_and_sgd(cuda):
     from svk import ops
     B = 88
