@@ -12,7 +12,7 @@ W=${W:-extract}
 DT=${DT:-fp16}
 B="python bench.py --no-cpu-baseline --other-dtypes none --workload $W --dtype $DT"
 step prof timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$W -o run -- $B --steps 10 --warmup 2 > $O/prof_$W.log 2>&1
-python tools/prof_stats.py $O/prof_$W/run_kernel_stats.csv 17 45 > $O/profiles_$R/rocprof_${W}_${DT}_stats.txt
+python tools/prof_stats.py $O/prof_$W/run_kernel_stats.csv auto:mean_rows_kernel 45 > $O/profiles_$R/rocprof_${W}_${DT}_stats.txt
 cp $O/prof_$W/run_kernel_stats.csv $O/profiles_$R/rocprof_${W}_${DT}_kernel_stats.csv
 tail -1 $O/prof_$W.log | cut -c1-300
 python tools/trace_gaps.py $O/prof_$W/run_kernel_trace.csv 2600 | tee $O/profiles_$R/trace_gaps_${W}_${DT}.txt

@@ -1,14 +1,21 @@
 """Summarise a rocprofv3 ``--kernel-trace --stats --output-format csv`` kernel_stats.csv into
-per-step kernel times.  Usage: python tools/prof_stats.py run_kernel_stats.csv STEPS [TOP]"""
+per-step kernel times.  Usage: python tools/prof_stats.py run_kernel_stats.csv STEPS [TOP]
+STEPS = a number, or auto:NAME_SUBSTR: the call count of the (first) kernel whose name contains
+NAME_SUBSTR and which runs exactly once per step (e.g. mean_rows_kernel for extraction, sgd for training)."""
 import csv
 import sys
 
 
 def main():
-    path, steps = sys.argv[1], float(sys.argv[2])
+    path, steps_arg = sys.argv[1], sys.argv[2]
     top = int(sys.argv[3]) if len(sys.argv) > 3 else 40
     with open(path) as f:
         rows = list(csv.DictReader(f))
+    if steps_arg.startswith("auto:"):
+        sub = steps_arg[5:]
+        steps = float(next(int(r["Calls"]) for r in rows if sub in r["Name"]))
+    else:
+        steps = float(steps_arg)
     tot = sum(float(r["TotalDurationNs"]) for r in rows) / 1e6
     print(f"total kernel time {tot / steps:.3f} ms per step ({steps:g} steps; rocprofv3 kernel_stats)")
     for r in rows[:top]:
