@@ -129,6 +129,80 @@ __global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, 
   }
 }
 
+// Rolling-window strip with 8 channels per thread (16-bit, C % 8 == 0): the strip kernel's lane mapping and
+// 16-byte loads, but only the three window rows (3 columns each) plus the next row in flight are live —
+// ~130 VGPRs instead of ~240, so 3-4 waves per SIMD hide the load latency on the small late-stage maps
+// (14 x 14 x 1280, 7 x 7 x 2048) where the strip kernel's two waves per SIMD leave HBM idle.  Same
+// arithmetic order as dwconv3x3_strip (bias, then taps dy-major, f32 FMAs), so the outputs are identical.
+template <typename T, int R>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 4))) void dwconv3x3_roll8(const T* __restrict__ X, const float* __restrict__ w,
+                                                       const float* __restrict__ bias, T* __restrict__ Y,
+                                                       T* __restrict__ Ypre, int B, int H, int W, int C, int act,
+                                                       int nstrip) {
+  const int CG = C >> 3;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * nstrip * W * CG;
+  if (idx >= total) return;
+  const int cg = (int)(idx % CG);
+  long t = idx / CG;
+  const int x = (int)(t % W);
+  t /= W;
+  const int s = (int)(t % nstrip);
+  const int b = (int)(t / nstrip);
+  const int c0 = cg * 8, y0 = s * R;
+  const T* base = X + (long)b * H * W * C + c0;
+  const int xl = x > 0 ? x - 1 : 0, xr = x < W - 1 ? x + 1 : W - 1;
+  auto load_row = [&](int yy, Vec8<T>* v) {
+    const bool oky = yy >= 0 && yy < H;
+    const T* row = base + (long)min(max(yy, 0), H - 1) * W * C;
+    load8_masked(row + (long)xl * C, oky && x > 0, v[0]);
+    load8_masked(row + (long)x * C, oky, v[1]);
+    load8_masked(row + (long)xr * C, oky && x < W - 1, v[2]);
+  };
+  Vec8<T> win[4][3];
+  load_row(y0 - 1, win[0]);
+  load_row(y0, win[1]);
+  f32x2 wt[9][4], bs[4];
+#pragma unroll
+  for (int k = 0; k < 9; ++k)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wt[k][j] = *reinterpret_cast<const f32x2*>(w + k * C + c0 + 2 * j);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f32x2*>(bias + c0 + 2 * j);
+  load_row(y0 + 1, win[2]);
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int y = y0 + r;
+    if (y >= H) break;
+    if (r + 1 < R) load_row(y + 2, win[(r + 3) & 3]);   // next row in flight while this one is computed
+    f32x2 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = bs[j];
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[j] = pair(win[(r + dy) & 3][dx], j) * wt[dy * 3 + dx][j] + acc[j];
+    const long off = (((long)b * H + y) * W + x) * C + c0;
+    T o[8];
+    if (Ypre) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[2 * j] = from_f<T>(acc[j].x); o[2 * j + 1] = from_f<T>(acc[j].y); }
+      store_vec8(Ypre + off, o);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x2 g;
+      if (act == SVK_ACT_GELU) g = gelu_fast2(acc[j]);
+      else g = f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
+      o[2 * j] = from_f<T>(g.x);
+      o[2 * j + 1] = from_f<T>(g.y);
+    }
+    store_vec8(Y + off, o);
+  }
+}
+
 // Rolling-window variant (bf16, C % 4 == 0): one thread per (4-channel group, column x, strip of R
 // rows).  Only three input rows (3 columns x 4 channels, 8-byte loads) are live at a time — the next
 // row is loaded while the current output row is computed — and the taps are 9 x 4 floats, so the
@@ -220,8 +294,9 @@ __global__ __launch_bounds__(256) void dwconv3x3_roll_bf16(const bf16* __restric
 template <typename T, int KS>   // T = bf16 / f16; K = 32 * KS (fc1 input channels)
 __global__ __launch_bounds__(256) void fc1_dwconv(const T* __restrict__ XN, const T* __restrict__ W1,
                                                   const float* __restrict__ b1, const float* __restrict__ taps,
-                                                  const float* __restrict__ db, T* __restrict__ G, int H, int W,
-                                                  int K, int HID, int R, int nstrip, int act) {
+                                                  const float* __restrict__ db, T* __restrict__ G,
+                                                  T* __restrict__ Gpre, int H, int W, int K, int HID, int R,
+                                                  int nstrip, int act) {
   typedef v8_t<T> tx8;
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   char* smem = reinterpret_cast<char*>(smem4);
@@ -315,6 +390,7 @@ __global__ __launch_bounds__(256) void fc1_dwconv(const T* __restrict__ XN, cons
   const uint4* tile = reinterpret_cast<const uint4*>(sH);
   const int rows = min(R, H - y0);
   T* Gb = G + (long)b * H * W * HID + c0;
+  T* Gpb = Gpre ? Gpre + (long)b * H * W * HID + c0 : nullptr;
   for (int q = pl; q < rows * W; q += 32) {
     const int r = q / W, x = q - r * W;
     f32x2 acc[4];
@@ -330,13 +406,19 @@ __global__ __launch_bounds__(256) void fc1_dwconv(const T* __restrict__ XN, cons
         for (int j = 0; j < 4; ++j) acc[j] = pair(v, j) * wt[dy * 3 + dx][j] + acc[j];
       }
     T o[8];
+    const long off = ((long)(y0 + r) * W + x) * HID;
+    if (Gpre) {   // pre-activation copy (training: the GELU backward reads it), rounded like dwconv3x3_strip's
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { o[2 * j] = (T)acc[j].x; o[2 * j + 1] = (T)acc[j].y; }
+      store_vec8(Gpb + off, o);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const f32x2 g = act == SVK_ACT_GELU ? gelu_fast2(acc[j]) : f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
       o[2 * j] = (T)g.x;
       o[2 * j + 1] = (T)g.y;
     }
-    store_vec8(Gb + ((long)(y0 + r) * W + x) * HID, o);
+    store_vec8(Gb + off, o);
   }
 }
 
@@ -724,6 +806,9 @@ inline dim3 grid1d(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) /
 
 using namespace svk;
 
+// maps no wider than this take dwconv3x3_roll8 (0 = never; env SVK_DW_ROLL8_MAXW)
+static const int g_dw_roll8_maxw = getenv("SVK_DW_ROLL8_MAXW") ? atoi(getenv("SVK_DW_ROLL8_MAXW")) : 0;
+
 extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const float* bias, void* Y, void* Ypre,
                                 int B, int H, int W, int C, int act, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || C <= 0 || !X || !w || !bias || !Y) { set_error("svk_dwconv3x3: bad args"); return SVK_EINVAL; }
@@ -756,6 +841,16 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
         }
       }
     }
+    if (sizeof(T) == 2 && vec && (lds_env == 3 || (lds_env < 0 && g_dw_roll8_maxw > 0 && W <= g_dw_roll8_maxw))) {
+      // rolling 8-channel window (svk_tune dw_lds = 3 forces it; by default for maps no wider than
+      // SVK_DW_ROLL8_MAXW columns)
+      constexpr int RR = 7;
+      const int nstrip = (H + RR - 1) / RR;
+      const long n = (long)B * nstrip * W * (C / 8);
+      hipLaunchKernelGGL((dwconv3x3_roll8<T, RR>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre,
+                         B, H, W, C, act, nstrip);
+      return check_launch("dwconv3x3_roll8");
+    }
     if (vec) {
       constexpr int R = sizeof(T) == 2 ? 7 : 2;   // 16-bit: 56 / 28 / 14 / 7-row maps in whole strips
       const int nstrip = (H + R - 1) / R;
@@ -772,19 +867,21 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
 }
 
 // fc1 + depthwise conv + activation (MixFFN front half) in one pass; see fc1_dwconv.
-extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
-                                     const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act,
-                                     void* stream) {
+extern "C" int svk_mixffn_fc1_dwconv_ex(int dtype, const void* XN, const void* W1, const float* b1,
+                                        const float* taps, const float* dbias, void* G, void* Gpre, int B, int H,
+                                        int W, int C, int hidden, int act, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || C <= 0 || hidden <= 0 || !XN || !W1 || !b1 || !taps || !dbias || !G) {
     set_error("svk_mixffn_fc1_dwconv: bad args"); return SVK_EINVAL;
   }
-  if ((dtype != SVK_BF16 && dtype != SVK_F16) || (C != 32 && C != 64 && C != 128) || hidden % 64 ||
-      ((((uintptr_t)XN) | ((uintptr_t)W1) | ((uintptr_t)G)) & 15)) {
-    set_error("svk_mixffn_fc1_dwconv: needs bf16 / f16, C in {32, 64, 128}, hidden %% 64 == 0, 16-byte aligned maps");
+  if ((dtype != SVK_BF16 && dtype != SVK_F16) || (C != 32 && C != 64 && C != 128 && C != 320 && C != 512) ||
+      hidden % 64 || ((((uintptr_t)XN) | ((uintptr_t)W1) | ((uintptr_t)G) | ((uintptr_t)Gpre)) & 15)) {
+    set_error("svk_mixffn_fc1_dwconv: needs bf16 / f16, C in {32, 64, 128, 320, 512}, hidden %% 64 == 0, "
+              "16-byte aligned maps");
     return SVK_EUNSUPPORTED;
   }
   if (B == 0) return SVK_OK;
-  if (fc1dw_rw_try(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, (hipStream_t)stream) == 0) return SVK_OK;
+  if (!Gpre &&
+      fc1dw_rw_try(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, (hipStream_t)stream) == 0) return SVK_OK;
   // strip height: halo tile <= 44 KiB (measured best at B = 256 against 48 KiB for W1 + tile), strips
   // of equal height; the svk_tune "dw_rows" knob overrides it
   int rmax = std::max(1, std::min(H, 45056 / ((W + 2) * 128) - 2));
@@ -801,13 +898,21 @@ extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, 
       if (lds > 65536)
         (void)hipFuncSetAttribute((const void*)fc1_dwconv<T, KS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL((fc1_dwconv<T, KS>), dim3((unsigned)nwg), dim3(256), lds, st, (const T*)XN, (const T*)W1, b1,
-                         taps, dbias, (T*)G, H, W, C, hidden, R, nstrip, act);
+                         taps, dbias, (T*)G, (T*)Gpre, H, W, C, hidden, R, nstrip, act);
     };
     if (C == 32) go(std::integral_constant<int, 1>{});
     else if (C == 64) go(std::integral_constant<int, 2>{});
-    else go(std::integral_constant<int, 4>{});
+    else if (C == 128) go(std::integral_constant<int, 4>{});
+    else if (C == 320) go(std::integral_constant<int, 10>{});
+    else go(std::integral_constant<int, 16>{});
     return check_launch("fc1_dwconv");
   });
+}
+
+extern "C" int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
+                                     const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act,
+                                     void* stream) {
+  return svk_mixffn_fc1_dwconv_ex(dtype, XN, W1, b1, taps, dbias, G, nullptr, B, H, W, C, hidden, act, stream);
 }
 
 extern "C" int svk_dwconv3x3(int dtype, const void* X, const float* w, const float* bias, void* Y, int B, int H,

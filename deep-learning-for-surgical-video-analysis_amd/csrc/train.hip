@@ -406,6 +406,33 @@ __global__ void pack_params_kernel(const PackDesc* __restrict__ d, int nd, long 
   dst[e.dst + (i - e.start)] = from_f<T>(ok ? src[off] : 0.f);
 }
 
+// ---- transposed 2-D packs: one workgroup per 64 x 64 tile of a row-major [N, K] f32 master ----------
+struct PackTile {
+  long src, dst;     // element offsets of the master matrix / the packed [K, N] view
+  int K, N, n0, k0;  // master shape, tile origin
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void pack_transpose_kernel(const PackTile* __restrict__ tl, const float* __restrict__ src,
+                                                             T* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const PackTile t = tl[blockIdx.x];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  // master rows n0 + r, columns k0 + tx: 256 B per wave-row, coalesced
+#pragma unroll 4
+  for (int r = ty; r < 64; r += 4) {
+    const int n = t.n0 + r, k = t.k0 + tx;
+    tile[r][tx] = (n < t.N && k < t.K) ? src[t.src + (long)n * t.K + k] : 0.f;
+  }
+  __syncthreads();
+  // packed rows k0 + r, columns n0 + tx
+#pragma unroll 4
+  for (int r = ty; r < 64; r += 4) {
+    const int k = t.k0 + r, n = t.n0 + tx;
+    if (k < t.K && n < t.N) dst[t.dst + (long)k * t.N + n] = from_f<T>(tile[tx][r]);
+  }
+}
+
 // ---- per-row scale (stochastic depth / Dropout2d masks): Y[r, c] = X[r, c] * s[r / rows_per] ---
 template <typename T>
 __global__ void row_scale_kernel(const T* __restrict__ X, const float* __restrict__ s, T* __restrict__ Y, long n,
@@ -486,6 +513,82 @@ __global__ void unpatchify_kernel(const T* __restrict__ P, T* __restrict__ Y, in
   const long dst = ((b * PH * s + (long)py * s + ii) * ((long)PW * s) + (long)px * s + j) * C + c;
   const float v = to_f(P[i]);
   Y[dst] = from_f<T>(accumulate ? to_f(Y[dst]) + v : v);
+}
+
+// 8 channels per thread (C % 8 == 0, 16-byte aligned maps): one 16-byte load of P, one 16-byte
+// read-modify-write of Y; consecutive threads walk a patch row's contiguous s*C run of a pixel row
+template <typename T>
+__global__ void unpatchify8_kernel(const T* __restrict__ P, T* __restrict__ Y, long n8, int PH, int PW, int s, int C8,
+                                   int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const int c8 = (int)(i % C8);
+  long t = i / C8;
+  const int j = (int)(t % s); t /= s;
+  const int ii = (int)(t % s); t /= s;
+  const int px = (int)(t % PW); t /= PW;
+  const int py = (int)(t % PH);
+  const long b = t / PH;
+  const long dst = (((b * PH * s + (long)py * s + ii) * ((long)PW * s) + (long)px * s + j) * C8 + c8) * 8;
+  uint4 pv = reinterpret_cast<const uint4*>(P)[i];
+  if (accumulate) {
+    const uint4 yv = *reinterpret_cast<const uint4*>(Y + dst);
+    const T* pe = reinterpret_cast<const T*>(&pv);
+    const T* ye = reinterpret_cast<const T*>(&yv);
+    T o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = from_f<T>(to_f(ye[e]) + to_f(pe[e]));
+    pv = *reinterpret_cast<const uint4*>(o);
+  }
+  *reinterpret_cast<uint4*>(Y + dst) = pv;
+}
+
+// ---- col2im: conv data gradient from the per-tap products P = dY Wc^T ------------------------------
+// P [B*OH*OW, k*k*Cin] (column (ky*k + kx)*Cin + ci) -> dX NHWC [B, H, W, Cin] (+ residual): each input
+// pixel gathers the taps that reached it, dX[y, x] = sum over (ky, kx) with y + pad - ky = stride*oy (and
+// likewise x) of P[(oy, ox), (ky, kx)].  The GEMM producing P does exactly k*k*Cin*Cout MACs per output
+// pixel (a direct transposed-conv GEMM over dX pixels multiplies stride^2 - 1 of every stride^2 taps by zero).
+// 8 channels per thread, 16-byte loads / stores, f32 sums.
+template <typename T>
+__global__ void col2im8_kernel(const T* __restrict__ P, const T* __restrict__ Rs, T* __restrict__ Y, long n8, int H,
+                               int W, int C8, int OH, int OW, int k, int stride, int pad) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n8) return;
+  const int c8 = (int)(i % C8);
+  long t = i / C8;
+  const int x = (int)(t % W); t /= W;
+  const int y = (int)(t % H);
+  const long b = t / H;
+  float acc[8];
+  if (Rs) {
+    const uint4 rv = reinterpret_cast<const uint4*>(Rs)[i];
+    const T* re = reinterpret_cast<const T*>(&rv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = to_f(re[e]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  }
+  const long ldp = (long)k * k * C8;   // P row stride in 8-element chunks
+  const uint4* P4 = reinterpret_cast<const uint4*>(P);
+  for (int ky = (y + pad) % stride; ky < k; ky += stride) {
+    const int oy = (y + pad - ky) / stride;
+    if (oy < 0) break;
+    if (oy >= OH) continue;
+    for (int kx = (x + pad) % stride; kx < k; kx += stride) {
+      const int ox = (x + pad - kx) / stride;
+      if (ox < 0) break;
+      if (ox >= OW) continue;
+      const uint4 pv = P4[((b * OH + oy) * OW + ox) * ldp + (long)(ky * k + kx) * C8 + c8];
+      const T* pe = reinterpret_cast<const T*>(&pv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += to_f(pe[e]);
+    }
+  }
+  T o[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = from_f<T>(acc[e]);
+  reinterpret_cast<uint4*>(Y)[i] = *reinterpret_cast<const uint4*>(o);
 }
 
 inline dim3 g1(long n) { return dim3((unsigned)((n + 255) / 256)); }
@@ -666,9 +769,31 @@ extern "C" int svk_unpatchify(int dtype, const void* P, void* Y, int B, int PH, 
   if (B == 0) return SVK_OK;
   const long n = (long)B * PH * PW * s * s * C;
   SVK_DISPATCH_DTYPE(dtype, T, {
+    if (sizeof(T) == 2 && C % 8 == 0 && ((((uintptr_t)P) | ((uintptr_t)Y)) & 15) == 0) {
+      hipLaunchKernelGGL((unpatchify8_kernel<T>), g1(n / 8), dim3(256), 0, (hipStream_t)stream, (const T*)P, (T*)Y, n / 8,
+                         PH, PW, s, C / 8, accumulate);
+      return check_launch("unpatchify8");
+    }
     hipLaunchKernelGGL((unpatchify_kernel<T>), g1(n), dim3(256), 0, (hipStream_t)stream, (const T*)P, (T*)Y, B, PH, PW,
                        s, C, accumulate);
     return check_launch("unpatchify");
+  });
+}
+
+extern "C" int svk_col2im_nhwc(int dtype, const void* P, const void* R, void* Y, int B, int H, int W, int Cin, int OH,
+                               int OW, int k, int stride, int pad, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || Cin <= 0 || OH <= 0 || OW <= 0 || k <= 0 || stride <= 0 || pad < 0 || !P || !Y) {
+    set_error("svk_col2im_nhwc: bad args"); return SVK_EINVAL;
+  }
+  if ((dtype != SVK_BF16 && dtype != SVK_F16) || Cin % 8 || ((((uintptr_t)P) | ((uintptr_t)R) | ((uintptr_t)Y)) & 15)) {
+    set_error("svk_col2im_nhwc: needs bf16 / f16, Cin %% 8 == 0, 16-byte aligned maps"); return SVK_EUNSUPPORTED;
+  }
+  if (B == 0) return SVK_OK;
+  const long n8 = (long)B * H * W * (Cin / 8);
+  SVK_DISPATCH_H16(dtype, T, {
+    hipLaunchKernelGGL((col2im8_kernel<T>), g1(n8), dim3(256), 0, (hipStream_t)stream, (const T*)P, (const T*)R, (T*)Y,
+                       n8, H, W, Cin / 8, OH, OW, k, stride, pad);
+    return check_launch("col2im");
   });
 }
 
@@ -687,6 +812,16 @@ extern "C" int svk_bn_update_running(const float* sum, const float* sumsq, int M
   hipLaunchKernelGGL(bn_running_kernel, dim3((C + 255) / 256), dim3(256), 0, (hipStream_t)stream, sum, sumsq, M, C,
                      momentum, running_mean, running_var);
   return check_launch("bn_update_running");
+}
+
+extern "C" int svk_pack_transpose(int dtype, const void* tiles, int ntiles, const float* src, void* dst, void* stream) {
+  if (ntiles < 0 || !tiles || !src || !dst) { set_error("svk_pack_transpose: bad args"); return SVK_EINVAL; }
+  if (ntiles == 0) return SVK_OK;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((pack_transpose_kernel<T>), dim3((unsigned)ntiles), dim3(256), 0, (hipStream_t)stream,
+                       (const PackTile*)tiles, src, (T*)dst);
+    return check_launch("pack_transpose");
+  });
 }
 
 extern "C" int svk_pack_params(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,

@@ -96,7 +96,7 @@ class Mlp(nn.Module):
             return y.view(B, N, C)
         # measured: wins where the hidden map is largest (stages 1-2, C <= 128); at C = 320 / 512 the
         # recomputed halo fc1 work outweighs the saved traffic
-        if ops.FC1_DWCONV and x.dtype in ops.H16 and C in (32, 64, 128) and hid % 64 == 0:
+        if ops.FC1_DWCONV and x.dtype in ops.H16 and C in ops.FC1_DWCONV_C and hid % 64 == 0:
             # fc1 -> DWConv -> GELU in one kernel, the hidden map kept on chip (Mlp.forward :60-63)
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")

@@ -26,6 +26,7 @@ SIGNATURES = {
                       c_int, c_int, c_int, c_int, c_int, c_float, P],
     "svk_dwconv3x3": [c_int, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_mixffn_fc1_dwconv": [c_int, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_mixffn_fc1_dwconv_ex": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_nchw_to_nhwc": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_gauss5x5_reflect": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_resize_bilinear": [c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P],
@@ -75,6 +76,7 @@ SIGNATURES = {
     "svk_conv2d_dgrad_nhwc": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, c_int, c_int, c_int, c_int, c_int,
                               c_int, P],
     "svk_unpatchify": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_col2im_nhwc": [c_int, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_attention_bwd": [c_int, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long, P, c_long, c_long,
                           P, c_long, c_long, P, c_long, c_long, P, P, c_long, c_long, P, c_long, c_int, c_int, c_int,
                           c_int, c_int, c_float, P],
@@ -92,6 +94,7 @@ SIGNATURES = {
     "svk_phase_loss": [P, P, P, P, c_int, c_int, P, P, P, P],
     "svk_sgd": [P, P, P, c_long, c_float, c_float, c_float, c_float, c_int, c_int, P],
     "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],
+    "svk_pack_transpose": [c_int, P, c_int, P, P, P],
 }
 STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
 LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],

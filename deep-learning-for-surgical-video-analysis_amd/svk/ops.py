@@ -416,11 +416,14 @@ def mixffn_rw(xn, x, w1, b1, taps, dbias, w2, b2, ln=None):
 
 
 FC1_DWCONV = os.environ.get("SVK_FC1_DWCONV", "1") == "1"
+# channel widths routed to it in inference (A/B knob; 320 / 512 are stages 3-4 of MiT-b1..b5)
+FC1_DWCONV_C = tuple(int(c) for c in os.environ.get("SVK_FC1_DWCONV_C", "32,64,128").split(","))
 
 
-def mixffn_fc1_dwconv(xn, w1, b1, taps, dbias, act="gelu"):
+def mixffn_fc1_dwconv(xn, w1, b1, taps, dbias, act="gelu", pre_out=None):
     """act(dwconv3x3(xn @ w1.T + b1) + dbias) on an NHWC [B, H, W, C] bf16 / f16 map -> [B, H, W, hidden];
-    the hidden map never leaves the chip (svk_mixffn_fc1_dwconv)."""
+    the hidden map never leaves the chip (svk_mixffn_fc1_dwconv_ex).  ``pre_out`` ([B, H, W, hidden], same
+    dtype) also receives the pre-activation, as ``dwconv3x3(..., pre_out=)`` writes it."""
     _chk(xn, "xn"); _chk(w1, "w1", xn.dtype)
     if xn.dtype not in H16:
         raise _lib.SvkError("svk.mixffn_fc1_dwconv: bf16 / f16 only")
@@ -433,13 +436,17 @@ def mixffn_fc1_dwconv(xn, w1, b1, taps, dbias, act="gelu"):
     if w1.shape[1] != C or taps.shape != (9, hid) or b1.numel() != hid or dbias.numel() != hid:
         raise _lib.SvkError("svk.mixffn_fc1_dwconv: shape mismatch")
     out = torch.empty(B, H, W, hid, device=xn.device, dtype=xn.dtype)
+    if pre_out is not None:
+        _chk(pre_out, "pre_out", xn.dtype)
+        if pre_out.shape != out.shape or not pre_out.is_contiguous():
+            raise _lib.SvkError("svk.mixffn_fc1_dwconv: pre_out must be a contiguous [B, H, W, hidden] map")
     t0 = _prof_begin()
-    _lib.call("svk_mixffn_fc1_dwconv", dtype_code(xn.dtype), _p(xn), _p(w1), _p(b1), _p(taps), _p(dbias), _p(out), B, H, W, C, hid,
-              ACT[act], _stream())
+    _lib.call("svk_mixffn_fc1_dwconv_ex", dtype_code(xn.dtype), _p(xn), _p(w1), _p(b1), _p(taps), _p(dbias), _p(out),
+              _p(pre_out), B, H, W, C, hid, ACT[act], _stream())
     if t0 is not None:
         M = B * H * W
-        _prof_end(t0, "fc1_dwconv", 2.0 * M * C * hid, (xn.numel() + out.numel() + w1.numel()) * 2,
-                  (M, hid, C, "fc1dw"))
+        _prof_end(t0, "fc1_dwconv", 2.0 * M * C * hid,
+                  (xn.numel() + out.numel() * (1 if pre_out is None else 2) + w1.numel()) * 2, (M, hid, C, "fc1dw"))
     return out
 
 
@@ -917,6 +924,28 @@ def conv2d_dgrad(dy, wd_packed, H, W, Cin, k, stride, pad, residual=None, out=No
     return out
 
 
+def conv2d_dgrad_col2im(dy, wc, H, W, Cin, k, stride, pad, residual=None, out=None):
+    """Conv data gradient as the per-tap product GEMM P = dy @ wc.T ([B*OH*OW, k*k*Cin], exactly the
+    k*k*Cin*Cout MACs per output pixel) followed by the col2im gather (svk_col2im_nhwc) -> dx [B, H, W, Cin]
+    (+ residual).  wc [(ky, kx, ci), co]; bf16 / f16, Cin % 8 == 0."""
+    _chk(dy, "dy"); _chk(wc, "wc", dy.dtype)
+    B, OH, OW, Cout = dy.shape
+    if not dy.is_contiguous() or wc.shape != (k * k * Cin, Cout) or not wc.is_contiguous():
+        raise _lib.SvkError("svk.conv2d_dgrad_col2im: layout mismatch")
+    if out is None:
+        out = torch.empty(B, H, W, Cin, device=dy.device, dtype=dy.dtype)
+    for t, nm in ((out, "out"), (residual, "residual")):
+        if t is not None and (t.shape != (B, H, W, Cin) or not t.is_contiguous() or t.dtype != dy.dtype):
+            raise _lib.SvkError(f"svk.conv2d_dgrad_col2im: {nm} mismatch")
+    p = gemm(dy.view(B * OH * OW, Cout), wc)
+    t0 = _prof_begin()
+    _lib.call("svk_col2im_nhwc", dtype_code(dy.dtype), _p(p), _p(residual), _p(out), B, H, W, Cin, OH, OW, k, stride,
+              pad, _stream())
+    _prof_end(t0, "col2im", 0.0, (p.numel() + out.numel() * (1 if residual is None else 2)) * dy.element_size(),
+              (B * H * W, Cin, k * k, f"col2im{k}s{stride}"))
+    return out
+
+
 def gemm_unpatchify(a, w, out, s, residual=None):
     """out NHWC [B, H, W, C] = unpatchify(a [B*(H/s)*(W/s), K] @ w.T) + residual (adjoint of the k = s
     patchify conv; w [(i, j, ci), K]).  residual may alias out."""
@@ -1093,6 +1122,10 @@ def sgd(p, g, buf, lr, momentum, dampening, wd, nesterov, first):
 
 def pack_params(desc, ndesc, total, src, dst):
     _lib.call("svk_pack_params", dtype_code(dst.dtype), _p(desc), ndesc, total, _p(src), _p(dst), _stream())
+
+
+def pack_transpose(tiles, ntiles, src, dst):
+    _lib.call("svk_pack_transpose", dtype_code(dst.dtype), _p(tiles), ntiles, _p(src), _p(dst), _stream())
 
 
 def tecno_loss(logits, labels, ant_targets, class_w=None, out=None, dlogits=None):

@@ -23,6 +23,8 @@ SmoothL1(sum) loss, backward, SGD step.  Every op is an svk kernel with an expli
 
 Frames per step B = 88 at the reference setting (train_evp.py:28).
 """
+import os
+
 import numpy as np
 import torch
 from torch.autograd.graph import increment_version
@@ -30,6 +32,16 @@ from torch.autograd.graph import increment_version
 from . import ops
 from ._lib import SvkError
 from .pack import pad_channels, conv_w
+
+# MixFFN front half of the training forward through svk_mixffn_fc1_dwconv_ex (A/B switch; channel widths it
+# is used for: stages 1-2 by default, "64,128,320,512" adds stages 3-4)
+TRAIN_FC1_DWCONV = os.environ.get("SVK_TRAIN_FC1_DWCONV", "1") == "1"
+# sequence-reduction conv data gradient as GEMM + vectorised scatter-add (A/B switch; 0 = fused scatter epilogue)
+TRAIN_UNPATCHIFY_SPLIT = os.environ.get("SVK_TRAIN_UNPATCHIFY_SPLIT", "1") == "1"
+# conv data gradients (frozen patch embeds, handcrafted-prompt convs) as per-tap GEMM + col2im gather (A/B
+# switch; 0 = the transposed-conv gather GEMM over input pixels)
+TRAIN_COL2IM = os.environ.get("SVK_TRAIN_COL2IM", "1") == "1"
+TRAIN_FC1_DWCONV_C = tuple(int(c) for c in os.environ.get("SVK_TRAIN_FC1_DWCONV_C", "32,64,128").split(","))
 
 TRAINABLE = ("head", "prompt", "flow_encoder", "cross_attn_s3", "cross_attn_s4")
 _BN_BUFFERS = ("running_mean", "running_var", "num_batches_tracked")
@@ -39,6 +51,10 @@ BLOCK_EPS, LN_EPS, BN_EPS, BN_MOMENTUM = 1e-6, 1e-5, 1e-5, 0.1
 
 _DESC = np.dtype([("src", "<i8"), ("dst", "<i8"), ("n", "<i4", 4), ("s", "<i8", 4), ("lim", "<i4", 4),
                   ("start", "<i8")])      # csrc/train.hip PackDesc
+_TILE = np.dtype([("src", "<i8"), ("dst", "<i8"), ("K", "<i4"), ("N", "<i4"), ("n0", "<i4"),
+                  ("k0", "<i4")])         # csrc/train.hip PackTile
+# transposed weight packs through the tiled transpose kernel (A/B switch; 0 = the generic strided gather)
+PACK_TRANSPOSE = os.environ.get("SVK_PACK_TRANSPOSE", "1") == "1"
 
 
 def is_trainable(name):
@@ -51,7 +67,9 @@ class _PackTable:
     def __init__(self, dtype):
         self.dtype = dtype
         self.rows = []
-        self.total = 0
+        self.trows = []          # transposed 2-D packs (svk_pack_transpose)
+        self.total = 0           # packed buffer size
+        self.gtotal = 0          # linear index space of the generic gather launch
         self.views = []
 
     def add(self, src, shape, strides, lims=None, view=None):
@@ -60,7 +78,11 @@ class _PackTable:
         lim = [1] * (4 - len(shape)) + list(lims if lims is not None else shape)
         numel = int(np.prod(shape))
         off = self.total
-        self.rows.append((src, off, n, s, lim, off))
+        if PACK_TRANSPOSE and len(shape) == 2 and tuple(strides) == (1, shape[0]) and lims is None:
+            self.trows.append((src, off, shape[0], shape[1]))      # [K, N] view of a row-major [N, K] master
+        else:
+            self.rows.append((src, off, n, s, lim, self.gtotal))
+            self.gtotal += numel
         self.total += (numel + 7) // 8 * 8      # keep every packed tensor 16-byte aligned
         self.views.append((off, tuple(view or shape)))
         return len(self.views) - 1
@@ -71,12 +93,20 @@ class _PackTable:
             arr[i] = (src, dst, n, s, lim, start)
         raw = torch.from_numpy(arr.view(np.uint8).copy())
         self.desc = raw.to(device)
+        tiles = [(src, dst, K, N, n0, k0) for src, dst, K, N in self.trows
+                 for n0 in range(0, N, 64) for k0 in range(0, K, 64)]
+        self.ntiles = len(tiles)
+        tarr = np.array(tiles, dtype=_TILE) if tiles else np.zeros(1, dtype=_TILE)
+        self.tiles = torch.from_numpy(tarr.view(np.uint8).copy()).to(device)
         self.buf = torch.zeros(max(self.total, 8), device=device, dtype=self.dtype)
         self.tensors = [self.buf[o:o + int(np.prod(sh))].view(sh) for o, sh in self.views]
 
     def run(self, master, dst=None):
+        out = self.buf if dst is None else dst
         if self.rows:
-            ops.pack_params(self.desc, len(self.rows), self.total, master, self.buf if dst is None else dst)
+            ops.pack_params(self.desc, len(self.rows), self.gtotal, master, out)
+        if self.ntiles:
+            ops.pack_transpose(self.tiles, self.ntiles, master, out)
 
 
 def _t(w):
@@ -185,6 +215,7 @@ class EVPTrainStep:
             self.pk[name] = tab.add(o, (co, k, k, cp), (ci * k * k, k, 1, k * k), (co, k, k, ci), view=(co, k * k * cp))
             if dgrad:
                 self.pk[name + ".D"] = tab.add(o, (ci, k, k, co), (k * k, k, 1, ci * k * k), view=(ci, k * k * co))
+                self.pk[name + ".C"] = tab.add(o, (k, k, ci, co), (k, 1, k * k, ci * k * k), view=(k * k * ci, co))
             # weight-gradient scratch in the packed layout, unpacked into the flat grad after backward
             n = co * k * k * cp
             self.conv_grad[name] = (conv_scratch, (co, k * k * cp))
@@ -262,6 +293,8 @@ class EVPTrainStep:
                 st = dict(k=k, stride=pe.stride, pad=k // 2)
                 st["w"] = conv_w(w, dt, pad_channels(ci))
                 st["wd"] = w.permute(1, 2, 3, 0).reshape(ci, k * k * co).to(dt).contiguous() if s > 0 else None
+                # col2im adjoint layout [(ky, kx, ci), co]
+                st["wc"] = w.permute(2, 3, 1, 0).reshape(k * k * ci, co).to(dt).contiguous() if s > 0 else None
                 st["b"] = pe.proj.bias.detach().float().contiguous()
                 st["g"], st["beta"] = pe.norm.weight.detach().float().contiguous(), pe.norm.bias.detach().float().contiguous()
                 norm = getattr(m, f"norm{s + 1}")
@@ -417,10 +450,16 @@ class EVPTrainStep:
         o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], b["heads"], b["scale"])
         x1 = ops.gemm(o, b["wp"], b["bp"], residual=xp, row_scale=ma, rows_per=N)
         xn2 = ops.layernorm(x1, b["g2"], b["b2"], BLOCK_EPS)
-        h = ops.gemm(xn2, b["w1"], b["bf1"])
-        hid = h.shape[-1]
+        hid = b["w1"].shape[0]
         u = torch.empty(B, H, W, hid, device=self.dev, dtype=self.dt)
-        g = ops.dwconv3x3(h.view(B, H, W, hid), b["taps"], b["dwb"], act="gelu", pre_out=u)
+        if TRAIN_FC1_DWCONV and self.dt in ops.H16 and C in TRAIN_FC1_DWCONV_C and hid % 64 == 0:
+            # fc1 -> DWConv (+ pre-activation for the GELU backward) -> GELU in one kernel: the frozen fc1's
+            # output is never needed by the backward, so it stays on chip (Mlp.forward :60-63)
+            g = ops.mixffn_fc1_dwconv(xn2.view(B, H, W, C), b["w1"], b["bf1"], b["taps"], b["dwb"], act="gelu",
+                                      pre_out=u)
+        else:
+            h = ops.gemm(xn2, b["w1"], b["bf1"])
+            g = ops.dwconv3x3(h.view(B, H, W, hid), b["taps"], b["dwb"], act="gelu", pre_out=u)
         out = ops.gemm(g.view(B, N, hid), b["w2"], b["bf2"], residual=x1, row_scale=mm, rows_per=N)
         sv.update(q=q, kv=kv, o=o, x1=x1, u=u, out=out)
         return sv
@@ -546,8 +585,13 @@ class EVPTrainStep:
                 dz = ops.layernorm_bwd(st["z"].view(B, st["N"], st["C"]), d, fz["g"], LN_EPS)
                 Hp, Wp, Cp = st["in_hw"]
                 prev = dtok[s - 1].reshape(B, Hp, Wp, Cp).contiguous()
-                dnext = ops.conv2d_dgrad(dz.view(B, st["H"], st["W"], st["C"]), fz["wd"], Hp, Wp, Cp, fz["k"],
-                                         fz["stride"], fz["pad"], residual=prev).view(B, Hp * Wp, Cp)
+                dzm = dz.view(B, st["H"], st["W"], st["C"])
+                if TRAIN_COL2IM and self.dt in ops.H16 and Cp % 8 == 0:
+                    dnext = ops.conv2d_dgrad_col2im(dzm, fz["wc"], Hp, Wp, Cp, fz["k"], fz["stride"], fz["pad"],
+                                                    residual=prev).view(B, Hp * Wp, Cp)
+                else:
+                    dnext = ops.conv2d_dgrad(dzm, fz["wd"], Hp, Wp, Cp, fz["k"], fz["stride"], fz["pad"],
+                                             residual=prev).view(B, Hp * Wp, Cp)
         # handcrafted cascade backward (trainable convs + LNs)
         dh = dhc[3]
         for s in range(3, -1, -1):
@@ -561,9 +605,11 @@ class EVPTrainStep:
                              self.G(nm + ".proj.bias"))
             if s > 0:
                 pin = h["inp"]
-                dh = ops.conv2d_dgrad(dzm, self.W(nm + ".proj.weight.D"), pin.shape[1], pin.shape[2], pin.shape[3],
-                                      h["k"], h["st"], h["k"] // 2,
-                                      residual=dhc[s - 1].view(pin.shape).contiguous())
+                dg = (ops.conv2d_dgrad_col2im if TRAIN_COL2IM and self.dt in ops.H16 and pin.shape[3] % 8 == 0
+                      else ops.conv2d_dgrad)
+                dh = dg(dzm, self.W(nm + ".proj.weight." + ("C" if dg is ops.conv2d_dgrad_col2im else "D")),
+                        pin.shape[1], pin.shape[2], pin.shape[3], h["k"], h["st"], h["k"] // 2,
+                        residual=dhc[s - 1].view(pin.shape).contiguous())
 
     def _block_bwd(self, d, b, sb, B, H, W, C):
         """Data gradient through one frozen block (given d = dL/d out) -> dL/d xp."""
@@ -584,7 +630,15 @@ class EVPTrainStep:
             r = b["sr"]
             dxs_pre = ops.layernorm_bwd(sb["xs_pre"], dxs, b["gn"], LN_EPS)
             dxn1 = ops.gemm(dq, b["wqT"])
-            ops.gemm_unpatchify(dxs_pre.view(-1, C), b["wsrD"], dxn1.view(B, H, W, C), r, residual=dxn1.view(B, H, W, C))
+            if TRAIN_UNPATCHIFY_SPLIT and self.dt in ops.H16:
+                # sequence-reduction conv data gradient: the patch-row GEMM on the persistent kernel, then one
+                # vectorised scatter-add into the pixel map (the fused scatter epilogue of the register-staged
+                # GEMM ran at ~1 TB/s)
+                pr = ops.gemm(dxs_pre.view(-1, C), b["wsrD"])
+                ops.unpatchify(pr, B, H // r, W // r, r, C, dxn1.view(B, H, W, C), accumulate=True)
+            else:
+                ops.gemm_unpatchify(dxs_pre.view(-1, C), b["wsrD"], dxn1.view(B, H, W, C), r,
+                                    residual=dxn1.view(B, H, W, C))
         else:
             dxn1 = ops.gemm(dq, b["wqT"], residual=dxs)
         return ops.layernorm_bwd(sb["xp"], dxn1, b["g1"], BLOCK_EPS, dres=d1)
@@ -626,8 +680,12 @@ class EVPTrainStep:
             if i > 1:
                 pin = L["inp"]
                 res = dflow[3].reshape(pin.shape).contiguous() if i == 4 else None
-                dy = ops.conv2d_dgrad(dz, self.W(nm + ".weight.D"), pin.shape[1], pin.shape[2], pin.shape[3], L["k"],
-                                      L["st"], L["pad"], residual=res)
+                if TRAIN_COL2IM and self.dt in ops.H16 and pin.shape[3] % 8 == 0:
+                    dy = ops.conv2d_dgrad_col2im(dz, self.W(nm + ".weight.C"), pin.shape[1], pin.shape[2],
+                                                 pin.shape[3], L["k"], L["st"], L["pad"], residual=res)
+                else:
+                    dy = ops.conv2d_dgrad(dz, self.W(nm + ".weight.D"), pin.shape[1], pin.shape[2], pin.shape[3],
+                                          L["k"], L["st"], L["pad"], residual=res)
 
     # ---- the step ---------------------------------------------------------------------------------
     def forward_backward(self, x, y, flow, labels, ant_targets, masks=None):

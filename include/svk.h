@@ -126,6 +126,12 @@ int svk_mixffn_rw(int dtype, const void* XN, const void* X, const void* W1, cons
  * b1 [hidden], taps [9][hidden], dbias [hidden] f32; G [B, H, W, hidden]. */
 int svk_mixffn_fc1_dwconv(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
                           const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act, void* stream);
+/* The same with C in {32, 64, 128, 320, 512} and an optional pre-activation output Gpre (dwconv3x3(...) +
+ * dbias rounded to the storage type, before act; nullptr = none): the training forward's MixFFN front half,
+ * whose GELU backward reads it (train_evp.py's frozen backbone: fc1's output itself is never needed). */
+int svk_mixffn_fc1_dwconv_ex(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
+                             const float* dbias, void* G, void* Gpre, int B, int H, int W, int C, int hidden,
+                             int act, void* stream);
 
 /* NCHW f32 -> NHWC dtype with the channel dim zero-padded to Cpad >= C (input packing of frames /
  * flow, view(-1,3,224,224) at :354; padding to 8 lets the first convs take the vector path). */
@@ -377,6 +383,13 @@ int svk_conv2d_dgrad_nhwc(int dtype, const void* dY, int B, int OH, int OW, int 
 int svk_unpatchify(int dtype, const void* P, void* Y, int B, int PH, int PW, int s, int C, int accumulate,
                    void* stream);
 
+/* Conv data gradient, second half (train_evp.py's loss.backward through the frozen OverlapPatchEmbed convs,
+ * mix_transformer_evp.py:226-241, and the trainable handcrafted-prompt convs): P [B*OH*OW, k*k*Cin] holds
+ * the per-tap products dY Wc^T (Wc [(ky, kx, ci), co]); dX NHWC [B, H, W, Cin] = the sum of the taps that
+ * reached each input pixel, + R if non-null.  bf16 / f16, Cin % 8 == 0. */
+int svk_col2im_nhwc(int dtype, const void* P, const void* R, void* dX, int B, int H, int W, int Cin, int OH, int OW,
+                    int k, int stride, int pad, void* stream);
+
 /* Scaled-dot-product attention backward (recomputes P): dQ, dK, dV written in the compute dtype
  * (dK/dV [B, Nk, heads*hd] with row stride lddk and batch stride sbdk).  bf16 with hd % 8 == 0,
  * hd <= 64, Nk <= 256: MFMA path (dQ kernel that also stores P and scale*dS, then batched MFMA
@@ -445,6 +458,11 @@ int svk_sgd(float* p, const float* grad, float* buf, long n, float lr, float mom
  * {long src, dst; int n[4]; long s[4]; int lim[4]; long start} (see csrc/train.hip PackDesc). */
 int svk_pack_params(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,
                     void* stream);
+
+/* The transposed 2-D packs of the same refresh (dst[k * N + n] = src[n * K + k] for a row-major [N, K] f32
+ * master matrix): tiles of 64 x 64 through LDS so both the master reads and the packed writes are
+ * coalesced.  tiles: device array of ntiles {long src, dst; int K, N, n0, k0} (one per tile). */
+int svk_pack_transpose(int dtype, const void* tiles, int ntiles, const float* src, void* dst, void* stream);
 
 #ifdef __cplusplus
 }

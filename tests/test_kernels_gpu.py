@@ -521,7 +521,7 @@ def test_conv2d_ln_sequence_reduction(cuda, dt, B, H, Cin, r):
 
 @pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (3, 28, 28, 128), (2, 14, 14, 128), (4, 7, 7, 64),
                                      (1, 9, 13, 32), (2, 30, 17, 64), (9, 28, 28, 128), (2, 13, 28, 128),
-                                     (1, 33, 28, 128)])
+                                     (1, 33, 28, 128), (3, 14, 14, 320), (2, 7, 7, 512), (1, 17, 9, 320)])
 @pytest.mark.parametrize("dt", H16)
 def test_mixffn_fc1_dwconv(cuda, B, H, W, C, dt):
     """fc1 -> dwconv3x3 -> GELU in one kernel (hidden kept on chip) against the unfused svk kernels
@@ -542,6 +542,36 @@ def test_mixffn_fc1_dwconv(cuda, B, H, W, C, dt):
     k = taps.cpu().double().t().reshape(hid, 1, 3, 3)
     ref = F.gelu(F.conv2d(hr.permute(0, 3, 1, 2), k, db.cpu().double(), padding=1, groups=hid)).permute(0, 2, 3, 1)
     _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("B,H,W,C", [(2, 56, 56, 64), (3, 28, 28, 128), (2, 14, 14, 320), (2, 7, 7, 512),
+                                     (1, 30, 17, 64)])
+@pytest.mark.parametrize("dt", H16)
+def test_mixffn_fc1_dwconv_pre_out(cuda, B, H, W, C, dt):
+    """The training forward's fused MixFFN front half: G and the pre-activation map equal the unfused chain the
+    train step ran before (fc1 GEMM -> dwconv3x3(pre_out=) -> GELU) within one storage ulp, and the
+    pre-activation equals fp64 torch on the same 16-bit-rounded hidden."""
+    from svk import ops
+    hid = 4 * C
+    xn = _rand(B, H, W, C, dt=dt, dev=cuda, seed=91)
+    w1 = _rand(hid, C, dt=dt, dev=cuda, scale=C ** -0.5, seed=92)
+    b1 = _rand(hid, dt=torch.float32, dev=cuda, scale=0.1, seed=93)
+    taps = _rand(9, hid, dt=torch.float32, dev=cuda, scale=0.3, seed=94)
+    db = _rand(hid, dt=torch.float32, dev=cuda, scale=0.1, seed=95)
+    pre = torch.full((B, H, W, hid), float("nan"), device=cuda, dtype=dt)
+    got = ops.mixffn_fc1_dwconv(xn, w1, b1, taps, db, act="gelu", pre_out=pre)
+    h = ops.gemm(xn.view(B, H * W, C), w1, b1).view(B, H, W, hid)
+    pre_u = torch.empty_like(pre)
+    unfused = ops.dwconv3x3(h, taps, db, act="gelu", pre_out=pre_u)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(pre).all())
+    _close(got, unfused.double().cpu(), dt)
+    _close(pre, pre_u.double().cpu(), dt)
+    hr = (xn.cpu().double() @ w1.cpu().double().t() + b1.cpu().double()).to(dt).double()
+    k = taps.cpu().double().t().reshape(hid, 1, 3, 3)
+    ref = F.conv2d(hr.permute(0, 3, 1, 2), k, db.cpu().double(), padding=1, groups=hid).permute(0, 2, 3, 1)
+    _close(pre, ref, dt)
+    _close(got, F.gelu(ref), dt)
 
 
 @pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16])

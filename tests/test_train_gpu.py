@@ -145,6 +145,32 @@ def test_conv_wgrad_dgrad(cuda, dt, B, Cin, H, Cout, k, s):
         _close(dx, xr.grad.permute(0, 2, 3, 1) + res.double().cpu(), tol)
 
 
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,Cin,H,Cout,k,s", [(2, 64, 56, 128, 3, 2), (3, 128, 28, 320, 3, 2), (2, 320, 14, 512, 3, 2),
+                                              (2, 16, 56, 32, 3, 2), (2, 8, 64, 16, 7, 4), (1, 24, 15, 40, 3, 2),
+                                              (2, 16, 13, 8, 3, 1), (1, 8, 17, 16, 5, 2)])
+@pytest.mark.parametrize("residual", [True, False])
+def test_conv_dgrad_col2im(cuda, dt, B, Cin, H, Cout, k, s, residual):
+    """The train step's conv data gradient as per-tap GEMM + col2im gather (exact MAC count) == fp64 autograd
+    and == the transposed-conv gather GEMM it replaces, at the 16-bit tolerance (odd sizes: output maps whose
+    last input rows / columns receive fewer taps)."""
+    from svk import ops
+    x, w = _conv_case(B, Cin, H, Cout, k, s, 5)
+    xr, wr = x.to(dt).double().requires_grad_(True), w.to(dt).double()
+    y = F.conv2d(xr, wr, stride=s, padding=k // 2)
+    dy = _rand(*y.shape, seed=13).to(dt).double()
+    y.backward(dy)
+    dyn = dy.permute(0, 2, 3, 1).contiguous().to(cuda, dt)
+    wc = w.permute(2, 3, 1, 0).reshape(k * k * Cin, Cout).to(cuda, dt).contiguous()
+    res = _rand(B, H, H, Cin, seed=17).to(cuda, dt) if residual else None
+    dx = ops.conv2d_dgrad_col2im(dyn, wc, H, H, Cin, k, s, k // 2, residual=res)
+    ref = xr.grad.permute(0, 2, 3, 1) + (res.double().cpu() if residual else 0.0)
+    _close(dx, ref, 2e-2)
+    wd = w.permute(1, 2, 3, 0).reshape(Cin, k * k * Cout).to(cuda, dt).contiguous()
+    old = ops.conv2d_dgrad(dyn, wd, H, H, Cin, k, s, k // 2, residual=res)
+    _close(dx, old.double().cpu(), 2e-2)
+
+
 def test_patchify_adjoint(cuda):
     """sr-conv data gradient: GEMM with the (i, j, ci) x co packed weight + unpatchify."""
     from svk import ops
@@ -165,6 +191,32 @@ def test_patchify_adjoint(cuda):
     dx2 = res.clone()
     ops.gemm_unpatchify(dyt, wd, dx2, r, residual=dx2)
     _close(dx2, x.grad.permute(0, 2, 3, 1) + res.cpu(), 1e-5)
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("B,C,H,r", [(3, 64, 56, 8), (2, 128, 28, 4), (2, 320, 14, 2), (1, 24, 12, 3)])
+def test_unpatchify_split_vs_fused(cuda, dt, B, C, H, r):
+    """The training step's split sr-conv data gradient (GEMM -> 16-byte scatter-add, svk_unpatchify's
+    vectorised path; C = 24 takes it too) == the fused scatter epilogue of svk_gemm_unpatchify: both round the
+    GEMM output to the storage type and add the residual in f32, so the results agree to one ulp."""
+    from svk import ops
+    K = C
+    dyt = _rand(B * (H // r) ** 2, K, seed=5).to(cuda, dt)
+    wd = (_rand(r * r * C, K, seed=6) * K ** -0.5).to(cuda, dt)
+    res = _rand(B, H, H, C, seed=7).to(cuda, dt)
+    fused = res.clone()
+    ops.gemm_unpatchify(dyt, wd, fused, r, residual=fused)
+    split = res.clone()
+    ops.unpatchify(ops.gemm(dyt, wd), B, H // r, H // r, r, C, split, accumulate=True)
+    plain = torch.zeros_like(res)
+    ops.unpatchify(ops.gemm(dyt, wd), B, H // r, H // r, r, C, plain)
+    torch.cuda.synchronize()
+    ref = (dyt.double() @ wd.double().t()).view(B, H // r, H // r, r, r, C).permute(0, 1, 3, 2, 4, 5)
+    ref = ref.reshape(B, H, H, C)
+    ulp = 2.0 ** -7 if dt == torch.bfloat16 else 2.0 ** -10
+    for got, want in ((split, fused.double()), (plain, ref), (split, ref + res.double())):
+        d = (got.double() - want).abs() / want.abs().clamp_min(1.0)
+        assert float(d.max()) <= 2 * ulp, float(d.max())
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
