@@ -129,80 +129,6 @@ __global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, 
   }
 }
 
-// Rolling-window strip with 8 channels per thread (16-bit, C % 8 == 0): the strip kernel's lane mapping and
-// 16-byte loads, but only the three window rows (3 columns each) plus the next row in flight are live —
-// ~130 VGPRs instead of ~240, so 3-4 waves per SIMD hide the load latency on the small late-stage maps
-// (14 x 14 x 1280, 7 x 7 x 2048) where the strip kernel's two waves per SIMD leave HBM idle.  Same
-// arithmetic order as dwconv3x3_strip (bias, then taps dy-major, f32 FMAs), so the outputs are identical.
-template <typename T, int R>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 4))) void dwconv3x3_roll8(const T* __restrict__ X, const float* __restrict__ w,
-                                                       const float* __restrict__ bias, T* __restrict__ Y,
-                                                       T* __restrict__ Ypre, int B, int H, int W, int C, int act,
-                                                       int nstrip) {
-  const int CG = C >> 3;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long total = (long)B * nstrip * W * CG;
-  if (idx >= total) return;
-  const int cg = (int)(idx % CG);
-  long t = idx / CG;
-  const int x = (int)(t % W);
-  t /= W;
-  const int s = (int)(t % nstrip);
-  const int b = (int)(t / nstrip);
-  const int c0 = cg * 8, y0 = s * R;
-  const T* base = X + (long)b * H * W * C + c0;
-  const int xl = x > 0 ? x - 1 : 0, xr = x < W - 1 ? x + 1 : W - 1;
-  auto load_row = [&](int yy, Vec8<T>* v) {
-    const bool oky = yy >= 0 && yy < H;
-    const T* row = base + (long)min(max(yy, 0), H - 1) * W * C;
-    load8_masked(row + (long)xl * C, oky && x > 0, v[0]);
-    load8_masked(row + (long)x * C, oky, v[1]);
-    load8_masked(row + (long)xr * C, oky && x < W - 1, v[2]);
-  };
-  Vec8<T> win[4][3];
-  load_row(y0 - 1, win[0]);
-  load_row(y0, win[1]);
-  f32x2 wt[9][4], bs[4];
-#pragma unroll
-  for (int k = 0; k < 9; ++k)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wt[k][j] = *reinterpret_cast<const f32x2*>(w + k * C + c0 + 2 * j);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) bs[j] = *reinterpret_cast<const f32x2*>(bias + c0 + 2 * j);
-  load_row(y0 + 1, win[2]);
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    const int y = y0 + r;
-    if (y >= H) break;
-    if (r + 1 < R) load_row(y + 2, win[(r + 3) & 3]);   // next row in flight while this one is computed
-    f32x2 acc[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = bs[j];
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = pair(win[(r + dy) & 3][dx], j) * wt[dy * 3 + dx][j] + acc[j];
-    const long off = (((long)b * H + y) * W + x) * C + c0;
-    T o[8];
-    if (Ypre) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) { o[2 * j] = from_f<T>(acc[j].x); o[2 * j + 1] = from_f<T>(acc[j].y); }
-      store_vec8(Ypre + off, o);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f32x2 g;
-      if (act == SVK_ACT_GELU) g = gelu_fast2(acc[j]);
-      else g = f32x2{apply_act(acc[j].x, act), apply_act(acc[j].y, act)};
-      o[2 * j] = from_f<T>(g.x);
-      o[2 * j + 1] = from_f<T>(g.y);
-    }
-    store_vec8(Y + off, o);
-  }
-}
-
 // Rolling-window variant (bf16, C % 4 == 0): one thread per (4-channel group, column x, strip of R
 // rows).  Only three input rows (3 columns x 4 channels, 8-byte loads) are live at a time — the next
 // row is loaded while the current output row is computed — and the taps are 9 x 4 floats, so the
@@ -587,6 +513,46 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc8_x4_kernel(const float* __re
   }
 }
 
+// ---- stem input as space-to-depth blocks (the k = 7, s = 4 OverlapPatchEmbed / flow conv1 stems) -----
+// NCHW f32 [B, C, H, W] -> [B, NBH, NBW, S*S*C]: block (by, bx) holds input rows S*by - pad .. + S - 1 and
+// the same columns, channel (dy*S + dx)*C + c, zeros outside the image.  A k <= 2S, stride-S conv with
+// padding `pad` is then a 2 x 2, stride-1, unpadded conv over the blocks (weights zero beyond k, see
+// svk.pack.conv_w_s2d): K = 4*S*S*C (192 for RGB, 128 for flow) instead of k*k*8 = 392 with the 3 real
+// channels padded to 8, and the packed map is 16*C/8*... = 2.7x smaller than the 8-channel NHWC one.
+template <typename T, int S, int C>
+__global__ __launch_bounds__(256) void nchw_to_s2d_kernel(const float* __restrict__ X, T* __restrict__ Y, int H, int W,
+                                                          int pad, int NBH, int NBW, long nblk) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nblk) return;
+  const int bx = (int)(q % NBW);
+  const long t = q / NBW;
+  const int by = (int)(t % NBH);
+  const long b = t / NBH;
+  const float* src = X + b * C * (long)H * W;
+  constexpr int NCH = S * S * C;
+  T o[NCH];
+#pragma unroll
+  for (int dy = 0; dy < S; ++dy) {
+    const int y = S * by - pad + dy;
+    const bool oky = y >= 0 && y < H;
+    const int yc = min(max(y, 0), H - 1);
+#pragma unroll
+    for (int dx = 0; dx < S; ++dx) {
+      const int x = S * bx - pad + dx;
+      const bool ok = oky && x >= 0 && x < W;
+      const int xc = min(max(x, 0), W - 1);
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const float v = src[((long)c * H + yc) * W + xc];
+        o[(dy * S + dx) * C + c] = from_f<T>(ok ? v : 0.f);
+      }
+    }
+  }
+  T* dst = Y + q * NCH;
+#pragma unroll
+  for (int k = 0; k < NCH / 8; ++k) store_vec8(dst + 8 * k, o + 8 * k);
+}
+
 // ---- GaussianFilter.conv_gauss: reflect pad 2 + binomial 5x5 / 256 (mix_transformer_evp.py:501-514)
 __device__ __forceinline__ int reflect(int i, int n) {
   if (i < 0) i = -i;
@@ -806,9 +772,6 @@ inline dim3 grid1d(long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) /
 
 using namespace svk;
 
-// maps no wider than this take dwconv3x3_roll8 (0 = never; env SVK_DW_ROLL8_MAXW)
-static const int g_dw_roll8_maxw = getenv("SVK_DW_ROLL8_MAXW") ? atoi(getenv("SVK_DW_ROLL8_MAXW")) : 0;
-
 extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const float* bias, void* Y, void* Ypre,
                                 int B, int H, int W, int C, int act, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || C <= 0 || !X || !w || !bias || !Y) { set_error("svk_dwconv3x3: bad args"); return SVK_EINVAL; }
@@ -840,16 +803,6 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
           return check_launch("dwconv3x3_lds");
         }
       }
-    }
-    if (sizeof(T) == 2 && vec && (lds_env == 3 || (lds_env < 0 && g_dw_roll8_maxw > 0 && W <= g_dw_roll8_maxw))) {
-      // rolling 8-channel window (svk_tune dw_lds = 3 forces it; by default for maps no wider than
-      // SVK_DW_ROLL8_MAXW columns)
-      constexpr int RR = 7;
-      const int nstrip = (H + RR - 1) / RR;
-      const long n = (long)B * nstrip * W * (C / 8);
-      hipLaunchKernelGGL((dwconv3x3_roll8<T, RR>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre,
-                         B, H, W, C, act, nstrip);
-      return check_launch("dwconv3x3_roll8");
     }
     if (vec) {
       constexpr int R = sizeof(T) == 2 ? 7 : 2;   // 16-bit: 56 / 28 / 14 / 7-row maps in whole strips
@@ -935,6 +888,27 @@ extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, i
   SVK_DISPATCH_DTYPE(dtype_out, T, {
     hipLaunchKernelGGL((nchw_to_nhwc_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, B, C, H, W, Cpad);
     return check_launch("nchw_to_nhwc");
+  });
+}
+
+extern "C" int svk_nchw_to_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int s, int pad,
+                               int NBH, int NBW, void* stream) {
+  if (B < 0 || H <= 0 || W <= 0 || NBH <= 0 || NBW <= 0 || pad < 0 || !X || !Y) {
+    set_error("svk_nchw_to_s2d: bad args"); return SVK_EINVAL;
+  }
+  if (s != 4 || (C != 2 && C != 3) || (dtype_out != SVK_BF16 && dtype_out != SVK_F16) || ((uintptr_t)Y & 15)) {
+    set_error("svk_nchw_to_s2d: needs s = 4, C in {2, 3}, bf16 / f16, 16-byte aligned output"); return SVK_EUNSUPPORTED;
+  }
+  if (B == 0) return SVK_OK;
+  const long nblk = (long)B * NBH * NBW;
+  SVK_DISPATCH_H16(dtype_out, T, {
+    if (C == 3)
+      hipLaunchKernelGGL((nchw_to_s2d_kernel<T, 4, 3>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, H, W,
+                         pad, NBH, NBW, nblk);
+    else
+      hipLaunchKernelGGL((nchw_to_s2d_kernel<T, 4, 2>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, H, W,
+                         pad, NBH, NBW, nblk);
+    return check_launch("nchw_to_s2d");
   });
 }
 

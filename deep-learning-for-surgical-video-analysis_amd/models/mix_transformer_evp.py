@@ -22,7 +22,7 @@ import torch
 import torch.nn as nn
 
 from svk import ops
-from svk.pack import get_packed, lin_w, lin_b, conv_w, fold_bn, pad_channels
+from svk.pack import get_packed, lin_w, lin_b, conv_w, conv_w_s2d, fold_bn, pad_channels
 from visualizer import get_local
 import svk
 from ._common import pair, compute_dtype, check_inference, to_nhwc, DropPath
@@ -228,8 +228,25 @@ class OverlapPatchEmbed(nn.Module):
     def _pack(self, dt):
         g, b = _ln_params(self.norm)
         cin = self.proj.weight.shape[1]
-        return dict(w=conv_w(self.proj.weight, dt, pad_channels(cin)), b=self.proj.bias.detach().float().contiguous(),
-                    g=g, beta=b)
+        p = dict(w=conv_w(self.proj.weight, dt, pad_channels(cin)), b=self.proj.bias.detach().float().contiguous(),
+                 g=g, beta=b)
+        if ops.stem_s2d_ok(dt, cin, self.patch_size[0], self.stride):
+            p["w_s2d"] = conv_w_s2d(self.proj.weight, dt, self.stride)
+        return p
+
+    def embed_image(self, x):
+        """x [B, Cin, H, W] NCHW (any float) -> (tokens [B, OH*OW, C], OH, OW): the stem conv over
+        space-to-depth blocks when eligible (16-bit, k = 7 / stride 4 on 2-3 channels), else via embed_nhwc."""
+        dt = compute_dtype(self)
+        k = self.patch_size[0]
+        if not ops.stem_s2d_ok(dt, x.shape[1], k, self.stride) or x.shape[1] != self.proj.weight.shape[1]:
+            return self.embed_nhwc(to_nhwc(x, dt))
+        p = get_packed(self, dt, self._pack)
+        y = ops.conv2d_stem_s2d(x, p["w_s2d"], k, self.stride, k // 2, bias=p["b"])
+        B, OH, OW, C = y.shape
+        y = y.view(B, OH * OW, C)
+        ops.layernorm(y, p["g"], p["beta"], self.norm.eps, out=y)
+        return y, OH, OW
 
     def embed_nhwc(self, x):
         """x [B, H, W, Cin'] NHWC (compute dtype, Cin' = pad_channels(Cin)) -> (tokens [B, OH*OW, C], OH, OW)."""
@@ -247,7 +264,7 @@ class OverlapPatchEmbed(nn.Module):
     def forward(self, x):
         """Reference signature: NCHW map -> (tokens, H, W)."""
         check_inference(self, x)
-        return self.embed_nhwc(to_nhwc(x, compute_dtype(self)))
+        return self.embed_image(x)
 
 
 class GaussianFilter(nn.Module):
@@ -395,6 +412,8 @@ class OpticalFlowEncoder(nn.Module):
             w, b = fold_bn(getattr(self, f"conv{i}").weight, getattr(self, f"conv{i}").bias, getattr(self, f"bn{i}"))
             p[f"w{i}"] = conv_w(w, dt, pad_channels(w.shape[1]))
             p[f"b{i}"] = b.float().contiguous()
+            if i == 1 and ops.stem_s2d_ok(dt, w.shape[1], 7, 4):
+                p["w1_s2d"] = conv_w_s2d(w, dt, 4)
         return p
 
     def forward(self, x):
@@ -405,10 +424,15 @@ class OpticalFlowEncoder(nn.Module):
             x = x.reshape(B * T, C, H, W)
         dt = compute_dtype(self)
         p = get_packed(self, dt, self._pack)
-        h = to_nhwc(x, dt)
         feats = []
         for i, (k, s, pad) in enumerate(((7, 4, 3), (3, 2, 1), (3, 2, 1), (3, 2, 1)), start=1):
-            h = ops.conv2d_nhwc(h, p[f"w{i}"], k, s, pad, bias=p[f"b{i}"], act="relu")
+            if i == 1:
+                if "w1_s2d" in p:      # conv1 over space-to-depth blocks of the raw flow (no 8-channel packing)
+                    h = ops.conv2d_stem_s2d(x, p["w1_s2d"], k, s, pad, bias=p["b1"], act="relu")
+                else:
+                    h = ops.conv2d_nhwc(to_nhwc(x, dt), p["w1"], k, s, pad, bias=p["b1"], act="relu")
+            else:
+                h = ops.conv2d_nhwc(h, p[f"w{i}"], k, s, pad, bias=p[f"b{i}"], act="relu")
             feats.append(h)
         f3, f4 = feats[2], feats[3]
         return f3.view(f3.shape[0], -1, f3.shape[3]), f4.view(f4.shape[0], -1, f4.shape[3])
@@ -527,10 +551,10 @@ class MixVisionTransformerEVP(nn.Module):
         if hcs is None:
             y = y.reshape(-1, 3, y.shape[-2], y.shape[-1])
             hcs = self.prompt_generator.init_prompts(y)
-        h = to_nhwc(x, dt)
         outs = []
         for s in range(4):
-            t, H, W = getattr(self, f"patch_embed{s + 1}").embed_nhwc(h)
+            pe = getattr(self, f"patch_embed{s + 1}")
+            t, H, W = pe.embed_image(x) if s == 0 else pe.embed_nhwc(h)
             if s == 0 and hc_ready is not None:
                 torch.cuda.current_stream(t.device).wait_event(hc_ready)
             prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1)

@@ -478,6 +478,33 @@ def nchw_to_nhwc(x, dtype, cpad=None):
     return out
 
 
+# stem convs (k = 7, stride 4, 2/3 input channels) over space-to-depth blocks (A/B switch)
+STEM_S2D = os.environ.get("SVK_STEM_S2D", "1") == "1"
+
+
+def stem_s2d_ok(dtype, cin, k, stride):
+    return STEM_S2D and dtype in H16 and cin in (2, 3) and stride == 4 and k <= 2 * stride
+
+
+def nchw_to_s2d(x, dtype, s, pad, nbh, nbw):
+    """[B, C, H, W] f32 -> space-to-depth blocks [B, nbh, nbw, s*s*C] in ``dtype`` (svk_nchw_to_s2d)."""
+    _chk(x, "x", torch.float32)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty(B, nbh, nbw, s * s * C, device=x.device, dtype=dtype)
+    _lib.call("svk_nchw_to_s2d", dtype_code(dtype), _p(x), _p(out), B, C, H, W, s, pad, nbh, nbw, _stream())
+    return out
+
+
+def conv2d_stem_s2d(x, w_s2d, k, stride, pad, bias=None, act=None):
+    """A k <= 2*stride, stride-4 conv of an NCHW f32 map with 2/3 channels, as the space-to-depth packing + a
+    2x2 unpadded conv over the blocks -> NHWC [B, OH, OW, Cout]; w_s2d from svk.pack.conv_w_s2d."""
+    B, C, H, W = x.shape
+    OH, OW = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    xs = nchw_to_s2d(x if x.dtype == torch.float32 else x.float(), w_s2d.dtype, stride, pad, OH + 1, OW + 1)
+    return conv2d_nhwc(xs, w_s2d, 2, 1, 0, bias=bias, act=act)
+
+
 def gauss5x5_reflect(x, dtype, cpad=None):
     _chk(x, "x", torch.float32)
     x = x.contiguous()

@@ -58,6 +58,16 @@ def conv_w(weight, dtype, cin_pad=None):
     return w.reshape(co, -1).to(dtype).contiguous()
 
 
+def conv_w_s2d(weight, dtype, s):
+    """[Cout, Cin, k, k] (k <= 2s) -> [Cout, 2*2*s*s*Cin] for the 2x2 conv over space-to-depth blocks
+    (svk_nchw_to_s2d): K order (by, bx, dy, dx, ci) with tap (ky, kx) = (s*by + dy, s*bx + dx); taps
+    beyond k are zero."""
+    co, ci, k, _ = weight.shape
+    w = torch.nn.functional.pad(weight.detach(), (0, 2 * s - k, 0, 2 * s - k))       # [co, ci, 2s, 2s]
+    w = w.reshape(co, ci, 2, s, 2, s).permute(0, 2, 4, 3, 5, 1)                    # [co, by, bx, dy, dx, ci]
+    return w.reshape(co, -1).to(dtype).contiguous()
+
+
 def fold_bn(weight, bias, bn):
     """Fold an eval-mode BatchNorm into the preceding conv: returns fp64 (w', b')."""
     w = weight.detach().double()

@@ -31,7 +31,7 @@ from torch.autograd.graph import increment_version
 
 from . import ops
 from ._lib import SvkError
-from .pack import pad_channels, conv_w
+from .pack import pad_channels, conv_w, conv_w_s2d
 
 # MixFFN front half of the training forward through svk_mixffn_fc1_dwconv_ex (A/B switch; channel widths it
 # is used for: stages 1-2 by default, "64,128,320,512" adds stages 3-4)
@@ -292,6 +292,8 @@ class EVPTrainStep:
                 co, ci, k, _ = w.shape
                 st = dict(k=k, stride=pe.stride, pad=k // 2)
                 st["w"] = conv_w(w, dt, pad_channels(ci))
+                if s == 0 and ops.stem_s2d_ok(dt, ci, k, pe.stride):
+                    st["w_s2d"] = conv_w_s2d(w, dt, pe.stride)
                 st["wd"] = w.permute(1, 2, 3, 0).reshape(ci, k * k * co).to(dt).contiguous() if s > 0 else None
                 # col2im adjoint layout [(ky, kx, ci), co]
                 st["wc"] = w.permute(2, 3, 1, 0).reshape(k * k * ci, co).to(dt).contiguous() if s > 0 else None
@@ -376,11 +378,16 @@ class EVPTrainStep:
             prev = h.view(B, OH, OW, C)
         sv["hc"] = hc
         # backbone with prompts (frozen weights; mix_transformer_evp.py:352-416)
-        cur = ops.nchw_to_nhwc(x.reshape(B, 3, 224, 224).float(), dt, cpad=8)
+        x4 = x.reshape(B, 3, 224, 224).float()
+        cur = None if "w_s2d" in self.fz[0] else ops.nchw_to_nhwc(x4, dt, cpad=8)
         stages = []
         for s in range(4):
             fz = self.fz[s]
-            z = ops.conv2d_nhwc(cur, fz["w"], fz["k"], fz["stride"], fz["pad"], bias=fz["b"])
+            if cur is None:     # frozen stem over space-to-depth blocks (no data / weight gradient needed)
+                z = ops.conv2d_stem_s2d(x4, fz["w_s2d"], fz["k"], fz["stride"], fz["pad"], bias=fz["b"])
+                cur = x4.permute(0, 2, 3, 1)         # shape-only stand-in for in_hw (read for s > 0 only)
+            else:
+                z = ops.conv2d_nhwc(cur, fz["w"], fz["k"], fz["stride"], fz["pad"], bias=fz["b"])
             _, H, W, C = z.shape
             N = H * W
             t = ops.layernorm(z.view(B, N, C), fz["g"], fz["beta"], LN_EPS)

@@ -140,6 +140,14 @@ int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H
 
 /* GaussianFilter.conv_gauss (mix_transformer_evp.py:511-514): reflect-pad 2 + binomial 5x5/256,
  * NCHW f32 in -> NHWC dtype out, channels zero-padded to Cpad >= C. */
+/* Stem input packing for the k = 7, stride-4 convs (OverlapPatchEmbed 1 and the flow encoder's conv1,
+ * mix_transformer_evp.py:226-229, 838-840): NCHW f32 [B, C, H, W] -> space-to-depth blocks [B, NBH, NBW,
+ * s*s*C] in dtype_out (block (by, bx) = input rows / columns s*by - pad .. s*by - pad + s - 1, channel
+ * (dy*s + dx)*C + c, zeros outside the image), so the conv becomes a 2x2 stride-1 unpadded conv over the
+ * blocks with NBH = OH + 1, NBW = OW + 1.  s = 4, C in {2, 3}, bf16 / f16. */
+int svk_nchw_to_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int s, int pad, int NBH,
+                    int NBW, void* stream);
+
 int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
                          void* stream);
 

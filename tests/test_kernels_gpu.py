@@ -649,3 +649,24 @@ def test_prompt_ln_vs_unfused(cuda, dt, M, C):
     for got, ref in ((xo, x64), (h, h64)):
         d = (d64(got) - ref).abs() / ref.abs().clamp_min(1.0)
         assert float(d.max()) <= 2 * ulp, ("fp64", float(d.max()))
+
+
+@pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,C,H,W,Cout", [(2, 3, 224, 224, 64), (2, 2, 224, 224, 64), (3, 3, 224, 224, 16),
+                                          (1, 3, 36, 20, 32), (2, 2, 12, 28, 8)])
+def test_stem_conv_s2d(cuda, dt, B, C, H, W, Cout):
+    """The k = 7 / stride-4 stem conv (OverlapPatchEmbed 1, flow conv1) over space-to-depth blocks == the
+    8-channel NHWC implicit-GEMM conv it replaces and fp64 torch (same storage-rounded inputs and weights)."""
+    from svk import ops
+    from svk.pack import conv_w, conv_w_s2d
+    x = torch.randn(B, C, H, W, generator=torch.Generator().manual_seed(61))
+    w = torch.randn(Cout, C, 7, 7, generator=torch.Generator().manual_seed(62)) * 0.1
+    b = torch.randn(Cout, generator=torch.Generator().manual_seed(63)) * 0.1
+    xd, wd, bd = x.to(cuda), w.to(cuda), b.to(cuda)
+    got = ops.conv2d_stem_s2d(xd, conv_w_s2d(wd, dt, 4), 7, 4, 3, bias=bd, act="relu")
+    old = ops.conv2d_nhwc(ops.nchw_to_nhwc(xd, dt, cpad=8), conv_w(wd, dt, 8), 7, 4, 3, bias=bd, act="relu")
+    torch.cuda.synchronize()
+    assert got.shape == old.shape == (B, (H - 1) // 4 + 1, (W - 1) // 4 + 1, Cout)
+    ref = F.relu(F.conv2d(x.to(dt).double(), w.to(dt).double(), b.double(), stride=4, padding=3)).permute(0, 2, 3, 1)
+    _close(got, ref, dt)
+    _close(got, old.double().cpu(), dt)
