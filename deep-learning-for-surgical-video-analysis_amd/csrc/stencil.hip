@@ -891,6 +891,78 @@ extern "C" int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, i
   });
 }
 
+// GaussianFilter.conv_gauss written straight into the stem's space-to-depth blocks (4 x 4 pixels, block
+// (by, bx) = rows / columns 4*by - pad .., zeros outside the image): one thread per block filters its 16
+// pixels from an 8 x 8 reflect-indexed input window per channel, with gauss5x5_x4_kernel's arithmetic
+// (horizontal 5-tap sums, then vertical, same order: bitwise equal values).  The handcrafted prompt
+// stem then runs as the 2x2 block conv like the frame's stem.
+template <typename T>
+__global__ __launch_bounds__(256) void gauss5x5_s2d_kernel(const float* __restrict__ X, T* __restrict__ Y, int C, int H,
+                                                           int W, int pad, int NBH, int NBW, long nblk) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nblk) return;
+  const int bx = (int)(q % NBW);
+  const long t = q / NBW;
+  const int by = (int)(t % NBH);
+  const long b = t / NBH;
+  const int py0 = 4 * by - pad, px0 = 4 * bx - pad;        // first output pixel of the block
+  const float k1[5] = {1.f / 16.f, 4.f / 16.f, 6.f / 16.f, 4.f / 16.f, 1.f / 16.f};
+  int cx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cx[j] = min(max(reflect(min(max(px0 - 2 + j, -2), W + 1), W), 0), W - 1);
+  T o[48];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float* src = X + ((long)b * C + min(c, C - 1)) * H * W;
+    float h[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int yy = min(max(reflect(min(max(py0 - 2 + r, -2), H + 1), H), 0), H - 1);
+      const float* row = src + (long)yy * W;
+      float w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = row[cx[j]];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) a += w[k + j] * k1[j];
+        h[r][k] = a;
+      }
+    }
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) a += h[dy + i][k] * k1[i];
+        const bool ok = c < C && py0 + dy >= 0 && py0 + dy < H && px0 + k >= 0 && px0 + k < W;
+        o[(dy * 4 + k) * 3 + c] = from_f<T>(ok ? a : 0.f);
+      }
+  }
+  T* dst = Y + q * 48;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) store_vec8(dst + 8 * k, o + 8 * k);
+}
+
+extern "C" int svk_gauss5x5_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int pad, int NBH,
+                                int NBW, void* stream) {
+  if (B < 0 || C < 1 || C > 3 || H < 3 || W < 3 || NBH <= 0 || NBW <= 0 || pad < 0 || !X || !Y) {
+    set_error("svk_gauss5x5_s2d: bad args (1 <= C <= 3)"); return SVK_EINVAL;
+  }
+  if ((dtype_out != SVK_BF16 && dtype_out != SVK_F16) || ((uintptr_t)Y & 15)) {
+    set_error("svk_gauss5x5_s2d: needs bf16 / f16, 16-byte aligned output"); return SVK_EUNSUPPORTED;
+  }
+  if (B == 0) return SVK_OK;
+  const long nblk = (long)B * NBH * NBW;
+  SVK_DISPATCH_H16(dtype_out, T, {
+    hipLaunchKernelGGL((gauss5x5_s2d_kernel<T>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, C, H, W, pad,
+                       NBH, NBW, nblk);
+    return check_launch("gauss5x5_s2d");
+  });
+}
+
 extern "C" int svk_nchw_to_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int s, int pad,
                                int NBH, int NBW, void* stream) {
   if (B < 0 || H <= 0 || W <= 0 || NBH <= 0 || NBW <= 0 || pad < 0 || !X || !Y) {

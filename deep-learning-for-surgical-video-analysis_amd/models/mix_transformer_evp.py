@@ -243,6 +243,18 @@ class OverlapPatchEmbed(nn.Module):
             return self.embed_nhwc(to_nhwc(x, dt))
         p = get_packed(self, dt, self._pack)
         y = ops.conv2d_stem_s2d(x, p["w_s2d"], k, self.stride, k // 2, bias=p["b"])
+        return self._tokens(y, p)
+
+    def s2d_ok(self, dt):
+        return ops.stem_s2d_ok(dt, self.proj.weight.shape[1], self.patch_size[0], self.stride)
+
+    def embed_blocks(self, xs):
+        """xs: the input already as space-to-depth blocks [B, OH + 1, OW + 1, 16 * Cin] (e.g. the Gaussian
+        filter's s2d output) -> (tokens, OH, OW)."""
+        p = get_packed(self, xs.dtype, self._pack)
+        return self._tokens(ops.conv2d_nhwc(xs, p["w_s2d"], 2, 1, 0, bias=p["b"]), p)
+
+    def _tokens(self, y, p):
         B, OH, OW, C = y.shape
         y = y.view(B, OH * OW, C)
         ops.layernorm(y, p["g"], p["beta"], self.norm.eps, out=y)
@@ -332,12 +344,22 @@ class PromptGenerator(nn.Module):
     def init_prompts(self, segmap):
         """Gaussian-filtered segmap -> handcrafted cascade (mix_transformer_evp.py:718-747);
         returns the 4 token maps [B, N_s, C_s/4]."""
-        x = self.gaussian_filter.conv_gauss(segmap)
+        hg1 = self.handcrafted_generator1
+        dt = compute_dtype(self)
+        blocks = hg1.s2d_ok(dt) and segmap.shape[1] == hg1.proj.weight.shape[1] and segmap.shape[1] <= 3
+        if blocks:       # filtered map written straight as the stem's space-to-depth blocks
+            k, st = hg1.patch_size[0], hg1.stride
+            oh = (segmap.shape[2] + 2 * (k // 2) - k) // st + 1
+            ow = (segmap.shape[3] + 2 * (k // 2) - k) // st + 1
+            x = ops.gauss5x5_s2d(segmap.float(), dt, k // 2, oh + 1, ow + 1)
+        else:
+            x = self.gaussian_filter.conv_gauss(segmap)
         feats = [None] * 4
         for s in range(4):
             if str(s + 1) not in self.tuning_stage:
                 break
-            f, H, W = getattr(self, f"handcrafted_generator{s + 1}").embed_nhwc(x)
+            g = getattr(self, f"handcrafted_generator{s + 1}")
+            f, H, W = g.embed_blocks(x) if s == 0 and blocks else g.embed_nhwc(x)
             feats[s] = f
             x = f.view(f.shape[0], H, W, -1)
         return tuple(feats)

@@ -496,6 +496,16 @@ def nchw_to_s2d(x, dtype, s, pad, nbh, nbw):
     return out
 
 
+def gauss5x5_s2d(x, dtype, pad, nbh, nbw):
+    """GaussianFilter.conv_gauss of an NCHW f32 map (C <= 3) -> space-to-depth blocks [B, nbh, nbw, 48]."""
+    _chk(x, "x", torch.float32)
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    out = torch.empty(B, nbh, nbw, 48, device=x.device, dtype=dtype)
+    _lib.call("svk_gauss5x5_s2d", dtype_code(dtype), _p(x), _p(out), B, C, H, W, pad, nbh, nbw, _stream())
+    return out
+
+
 def conv2d_stem_s2d(x, w_s2d, k, stride, pad, bias=None, act=None):
     """A k <= 2*stride, stride-4 conv of an NCHW f32 map with 2/3 channels, as the space-to-depth packing + a
     2x2 unpadded conv over the blocks -> NHWC [B, OH, OW, Cout]; w_s2d from svk.pack.conv_w_s2d."""

@@ -859,13 +859,19 @@ class EVPTrainStep:
                 self._optimizer_launch(first=False)
             return self
         pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(self.graph, pool=pool):
+        # thread-local capture: the process group's watchdog thread polls the completion events of earlier
+        # collectives (hipEventQuery) at any time, which a global-mode capture treats as an illegal call
+        # from another thread and aborts on (seen on MI355X as "operation not permitted when stream is
+        # capturing" in the watchdog).  The captured work itself never calls into RCCL.
+        torch.cuda.synchronize(self.dev)
+        mode = dict(pool=pool, capture_error_mode="thread_local")
+        with torch.cuda.graph(self.graph, **mode):
             self._gout = self.fb_head(*self._static)
         self.graph_rest = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_rest, pool=pool):
+        with torch.cuda.graph(self.graph_rest, **mode):
             self.fb_rest()
         self.graph_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph_opt, pool=pool):
+        with torch.cuda.graph(self.graph_opt, **mode):
             self.grad.mul_(1.0 / self.world)
             self._optimizer_launch(first=False)
         return self

@@ -148,6 +148,12 @@ int svk_nchw_to_nhwc(int dtype_out, const float* X, void* Y, int B, int C, int H
 int svk_nchw_to_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int s, int pad, int NBH,
                     int NBW, void* stream);
 
+/* GaussianFilter.conv_gauss (reflect pad 2, binomial 5x5 / 256; mix_transformer_evp.py:495-514) written as
+ * the stem's space-to-depth blocks [B, NBH, NBW, 48] (svk_nchw_to_s2d's layout with 3 channels, channels
+ * >= C zero): the handcrafted prompt stem's input.  Values bitwise equal to svk_gauss5x5_reflect's. */
+int svk_gauss5x5_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int pad, int NBH, int NBW,
+                     void* stream);
+
 int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int Cpad,
                          void* stream);
 

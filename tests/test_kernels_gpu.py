@@ -670,3 +670,20 @@ def test_stem_conv_s2d(cuda, dt, B, C, H, W, Cout):
     ref = F.relu(F.conv2d(x.to(dt).double(), w.to(dt).double(), b.double(), stride=4, padding=3)).permute(0, 2, 3, 1)
     _close(got, ref, dt)
     _close(got, old.double().cpu(), dt)
+
+
+@pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,C,H,W", [(2, 3, 224, 224), (1, 3, 36, 20), (2, 2, 12, 28), (1, 1, 9, 13)])
+def test_gauss5x5_s2d(cuda, dt, B, C, H, W):
+    """GaussianFilter.conv_gauss written as the stem's space-to-depth blocks == svk_gauss5x5_reflect's NHWC map
+    rearranged into blocks (bitwise: the same arithmetic per pixel), zeros outside the image."""
+    from svk import ops
+    x = torch.rand(B, C, H, W, generator=torch.Generator().manual_seed(71)).to(cuda)
+    OH, OW = (H - 1) // 4 + 1, (W - 1) // 4 + 1
+    got = ops.gauss5x5_s2d(x, dt, 3, OH + 1, OW + 1)
+    ref8 = ops.gauss5x5_reflect(x, dt, cpad=8)[..., :3]                       # [B, H, W, 3]
+    pad = torch.zeros(B, 4 * (OH + 1), 4 * (OW + 1), 3, device=cuda, dtype=dt)
+    pad[:, 3:3 + H, 3:3 + W] = ref8
+    ref = pad.view(B, OH + 1, 4, OW + 1, 4, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, OH + 1, OW + 1, 48)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
