@@ -946,6 +946,68 @@ __global__ __launch_bounds__(256) void gauss5x5_s2d_kernel(const float* __restri
   for (int k = 0; k < 6; ++k) store_vec8(dst + 8 * k, o + 8 * k);
 }
 
+// The same filter, one 64-lane workgroup per block row: the 8 reflect-mapped input rows of every channel
+// are staged in LDS with float4 loads (W % 4 == 0), then each lane filters one block from LDS — the
+// per-lane 8-column windows of the direct kernel cost 192 scalar loads per block.  Same arithmetic.
+template <typename T>
+__global__ __launch_bounds__(64) void gauss5x5_s2d_lds_kernel(const float* __restrict__ X, T* __restrict__ Y, int C,
+                                                              int H, int W, int pad, int NBH, int NBW) {
+  extern __shared__ __attribute__((aligned(16))) float srow[];      // [C][8][W]
+  const int by = blockIdx.x % NBH;
+  const long b = blockIdx.x / NBH;
+  const int py0 = 4 * by - pad;
+  const int W4 = W >> 2;
+  for (int e = threadIdx.x; e < C * 8 * W4; e += 64) {
+    const int c = e / (8 * W4), r = (e / W4) % 8, x4 = e % W4;
+    const int yy = min(max(reflect(min(max(py0 - 2 + r, -2), H + 1), H), 0), H - 1);
+    reinterpret_cast<float4*>(srow)[(c * 8 + r) * W4 + x4] =
+        reinterpret_cast<const float4*>(X + (((long)b * C + c) * H + yy) * W)[x4];
+  }
+  __syncthreads();
+  const int bx = threadIdx.x;
+  if (bx >= NBW) return;
+  const int px0 = 4 * bx - pad;
+  const float k1[5] = {1.f / 16.f, 4.f / 16.f, 6.f / 16.f, 4.f / 16.f, 1.f / 16.f};
+  int cx[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) cx[j] = min(max(reflect(min(max(px0 - 2 + j, -2), W + 1), W), 0), W - 1);
+  T o[48];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const float* src = srow + min(c, C - 1) * 8 * W;
+    float h[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = src[r * W + cx[j]];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) a += w[k + j] * k1[j];
+        h[r][k] = a;
+      }
+    }
+#pragma unroll
+    for (int dy = 0; dy < 4; ++dy)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 0.f;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) a += h[dy + i][k] * k1[i];
+        const bool ok = c < C && py0 + dy >= 0 && py0 + dy < H && px0 + k >= 0 && px0 + k < W;
+        o[(dy * 4 + k) * 3 + c] = from_f<T>(ok ? a : 0.f);
+      }
+  }
+  T* dst = Y + ((long)blockIdx.x * NBW + bx) * 48;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) store_vec8(dst + 8 * k, o + 8 * k);
+}
+
+// LDS-staged Gaussian / float4 frame packing for the space-to-depth stems (env SVK_S2D_PACK_VEC, 1 = on)
+static const bool g_s2d_pack_vec = getenv("SVK_S2D_PACK_VEC") ? atoi(getenv("SVK_S2D_PACK_VEC")) != 0 : false;
+
 extern "C" int svk_gauss5x5_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int pad, int NBH,
                                 int NBW, void* stream) {
   if (B < 0 || C < 1 || C > 3 || H < 3 || W < 3 || NBH <= 0 || NBW <= 0 || pad < 0 || !X || !Y) {
@@ -956,11 +1018,56 @@ extern "C" int svk_gauss5x5_s2d(int dtype_out, const float* X, void* Y, int B, i
   }
   if (B == 0) return SVK_OK;
   const long nblk = (long)B * NBH * NBW;
+  const size_t lds = (size_t)C * 8 * W * sizeof(float);
   SVK_DISPATCH_H16(dtype_out, T, {
+    if (g_s2d_pack_vec && W % 4 == 0 && NBW <= 64 && ((uintptr_t)X & 15) == 0 && lds <= 65536 &&
+        (long)B * NBH < 0x7fffffffL) {
+      hipLaunchKernelGGL((gauss5x5_s2d_lds_kernel<T>), dim3((unsigned)(B * NBH)), dim3(64), lds, (hipStream_t)stream, X,
+                         (T*)Y, C, H, W, pad, NBH, NBW);
+      return check_launch("gauss5x5_s2d_lds");
+    }
     hipLaunchKernelGGL((gauss5x5_s2d_kernel<T>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, C, H, W, pad,
                        NBH, NBW, nblk);
     return check_launch("gauss5x5_s2d");
   });
+}
+
+// pad = S - 1 = 3 with W % 4 == 0: block columns 4*bx - 3 .. 4*bx straddle two aligned float4 chunks
+// (4*bx - 4 .. 4*bx - 1 and 4*bx .. 4*bx + 3), so each (row, channel) costs two 16-byte loads instead of
+// four scalar ones (chunk addresses clamped into the row, out-of-image values masked to zero).
+template <typename T, int C>
+__global__ __launch_bounds__(256) void nchw_to_s2d4_kernel(const float* __restrict__ X, T* __restrict__ Y, int H, int W,
+                                                           int NBH, int NBW, long nblk) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= nblk) return;
+  const int bx = (int)(q % NBW);
+  const long t = q / NBW;
+  const int by = (int)(t % NBH);
+  const long b = t / NBH;
+  const float* src = X + b * C * (long)H * W;
+  const int a0 = max(4 * bx - 4, 0), a1 = min(4 * bx, W - 4);
+  T o[16 * C];
+#pragma unroll
+  for (int dy = 0; dy < 4; ++dy) {
+    const int y = 4 * by - 3 + dy;
+    const bool oky = y >= 0 && y < H;
+    const int yc = min(max(y, 0), H - 1);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float* row = src + ((long)c * H + yc) * W;
+      const float4 u = *reinterpret_cast<const float4*>(row + a0);
+      const float4 v = *reinterpret_cast<const float4*>(row + a1);
+      const float val[4] = {u.y, u.z, u.w, v.x};
+#pragma unroll
+      for (int dx = 0; dx < 4; ++dx) {
+        const int x = 4 * bx - 3 + dx;
+        o[(dy * 4 + dx) * C + c] = from_f<T>(oky && x >= 0 && x < W ? val[dx] : 0.f);
+      }
+    }
+  }
+  T* dst = Y + q * 16 * C;
+#pragma unroll
+  for (int k = 0; k < 2 * C; ++k) store_vec8(dst + 8 * k, o + 8 * k);
 }
 
 extern "C" int svk_nchw_to_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int s, int pad,
@@ -974,6 +1081,15 @@ extern "C" int svk_nchw_to_s2d(int dtype_out, const float* X, void* Y, int B, in
   if (B == 0) return SVK_OK;
   const long nblk = (long)B * NBH * NBW;
   SVK_DISPATCH_H16(dtype_out, T, {
+    if (g_s2d_pack_vec && pad == 3 && W % 4 == 0 && W >= 4 && ((uintptr_t)X & 15) == 0) {
+      if (C == 3)
+        hipLaunchKernelGGL((nchw_to_s2d4_kernel<T, 3>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, H, W,
+                           NBH, NBW, nblk);
+      else
+        hipLaunchKernelGGL((nchw_to_s2d4_kernel<T, 2>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, H, W,
+                           NBH, NBW, nblk);
+      return check_launch("nchw_to_s2d4");
+    }
     if (C == 3)
       hipLaunchKernelGGL((nchw_to_s2d_kernel<T, 4, 3>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, H, W,
                          pad, NBH, NBW, nblk);
