@@ -149,6 +149,25 @@ def test_conv_weight_packing_order():
     np.testing.assert_allclose(got.permute(0, 3, 1, 2).numpy(), ref.numpy(), atol=1e-10)
 
 
+@pytest.mark.parametrize("C,H,W", [(3, 224, 224), (2, 20, 28), (3, 13, 9)])
+def test_stem_s2d_layout_on_cpu(C, H, W):
+    """The space-to-depth stem (svk_nchw_to_s2d's block layout, restated here in torch, + the 2x2 unpadded
+    conv with svk.pack.conv_w_s2d's weights) == the k = 7 / stride-4 / pad-3 conv, in float64."""
+    from svk.pack import conv_w_s2d
+    w = torch.randn(6, C, 7, 7, dtype=torch.float64)
+    x = torch.randn(2, C, H, W, dtype=torch.float64)
+    ref = torch.nn.functional.conv2d(x, w, stride=4, padding=3)
+    OH, OW = ref.shape[2:]
+    # block (by, bx) = rows / columns 4*b - 3 .. 4*b, channel (dy, dx, c), zeros outside the image
+    xp = torch.zeros(2, C, 4 * (OH + 1), 4 * (OW + 1), dtype=torch.float64)
+    xp[:, :, 3:3 + H, 3:3 + W] = x
+    blocks = xp.view(2, C, OH + 1, 4, OW + 1, 4).permute(0, 2, 4, 3, 5, 1).reshape(2, OH + 1, OW + 1, 16 * C)
+    cols = blocks.unfold(1, 2, 1).unfold(2, 2, 1)                          # [2, OH, OW, 16C, by, bx]
+    cols = cols.permute(0, 1, 2, 4, 5, 3).reshape(2, OH, OW, -1)          # K order (by, bx, dy, dx, c)
+    got = cols @ conv_w_s2d(w, torch.float64, 4).t()
+    np.testing.assert_allclose(got.permute(0, 3, 1, 2).numpy(), ref.numpy(), atol=1e-10)
+
+
 def test_useful_start_idx():
     from models.data_process import get_useful_start_idx, get_useful_start_idx_LFB, SeqSampler
     # reference semantics (data_process.py:307-315): per video, starts count..count+len-seq
