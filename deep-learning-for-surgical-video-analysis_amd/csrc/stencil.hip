@@ -1005,8 +1005,8 @@ __global__ __launch_bounds__(64) void gauss5x5_s2d_lds_kernel(const float* __res
   for (int k = 0; k < 6; ++k) store_vec8(dst + 8 * k, o + 8 * k);
 }
 
-// LDS-staged Gaussian / float4 frame packing for the space-to-depth stems (env SVK_S2D_PACK_VEC, 1 = on)
-static const bool g_s2d_pack_vec = getenv("SVK_S2D_PACK_VEC") ? atoi(getenv("SVK_S2D_PACK_VEC")) != 0 : false;
+// LDS-staged Gaussian / float4 frame packing for the space-to-depth stems (env SVK_S2D_PACK_VEC=0 = off)
+static const bool g_s2d_pack_vec = getenv("SVK_S2D_PACK_VEC") ? atoi(getenv("SVK_S2D_PACK_VEC")) != 0 : true;
 
 extern "C" int svk_gauss5x5_s2d(int dtype_out, const float* X, void* Y, int B, int C, int H, int W, int pad, int NBH,
                                 int NBW, void* stream) {
