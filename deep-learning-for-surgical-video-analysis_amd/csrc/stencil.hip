@@ -1045,7 +1045,9 @@ __global__ __launch_bounds__(256) void nchw_to_s2d4_kernel(const float* __restri
   const int by = (int)(t % NBH);
   const long b = t / NBH;
   const float* src = X + b * C * (long)H * W;
-  const int a0 = max(4 * bx - 4, 0), a1 = min(4 * bx, W - 4);
+  // both chunk addresses clamped into the row: a block column past the image (NBW > W / 4 + 1, e.g. a
+  // k = 6 stem) reads in-row bytes whose values are all masked (4 * bx >= W + 4 there, so x >= W + 1)
+  const int a0 = min(max(4 * bx - 4, 0), W - 4), a1 = min(4 * bx, W - 4);
   T o[16 * C];
 #pragma unroll
   for (int dy = 0; dy < 4; ++dy) {

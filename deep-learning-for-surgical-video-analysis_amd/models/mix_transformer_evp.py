@@ -346,7 +346,8 @@ class PromptGenerator(nn.Module):
         returns the 4 token maps [B, N_s, C_s/4]."""
         hg1 = self.handcrafted_generator1
         dt = compute_dtype(self)
-        blocks = hg1.s2d_ok(dt) and segmap.shape[1] == hg1.proj.weight.shape[1] and segmap.shape[1] <= 3
+        # gauss5x5_s2d always writes 3-channel (48-wide) blocks: only a 3-channel stem takes the blocks path
+        blocks = hg1.s2d_ok(dt) and segmap.shape[1] == hg1.proj.weight.shape[1] == 3
         if blocks:       # filtered map written straight as the stem's space-to-depth blocks
             k, st = hg1.patch_size[0], hg1.stride
             oh = (segmap.shape[2] + 2 * (k // 2) - k) // st + 1

@@ -432,6 +432,7 @@ class TemporalTrainStep:
         # activation workspace (MS-TCN S(2L+1)TF f32 + masks, Mamba ~36 KB per frame at 10 blocks, i.e.
         # ~0.2 GB for a 6000-frame video); least-recently-used lengths beyond max_graphs are dropped
         self._g = collections.OrderedDict()
+        self._eager = collections.OrderedDict()
         self.max_graphs = int(max_graphs)
 
     def set_lr(self, lr):
@@ -463,7 +464,14 @@ class TemporalTrainStep:
         self.tr.ensure_fresh()
         T = x.shape[0]
         if not self.graphs:
-            ws = self._g.setdefault(("eager", T), _WS(self.dev))
+            # eager workspaces are bounded by the same LRU as the captured graphs, in a map of
+            # their own so evictions of one kind never drop the other
+            ws = self._eager.get(T)
+            if ws is None:
+                ws = self._eager[T] = _WS(self.dev)
+                while len(self._eager) > self.max_graphs:
+                    self._eager.popitem(last=False)
+            self._eager.move_to_end(T)
             self._body(x, labels, ant, ws)
             self._bump()
             return self.loss

@@ -120,7 +120,11 @@ class EVPTrainStep:
     (gradient all-reduce, BN buffer broadcast from rank 0); None = single process."""
 
     def __init__(self, model, lr=5e-4, momentum=0.9, dampening=0.0, weight_decay=1e-5, nesterov=False,
-                 dtype=torch.bfloat16, drop=True, seed=0, process_group=None, world_size=1):
+                 dtype=torch.bfloat16, drop=True, seed=0, process_group=None, world_size=1, grad_comm="f32"):
+        if grad_comm not in ("f32", "bf16"):
+            raise SvkError(f"EVPTrainStep: grad_comm must be 'f32' or 'bf16', got {grad_comm!r}")
+        self.grad_comm = grad_comm
+        self._comm = {}
         self.model = model
         self.dt = dtype
         self.hp = dict(lr=lr, momentum=momentum, dampening=dampening, weight_decay=weight_decay, nesterov=nesterov)
@@ -774,15 +778,31 @@ class EVPTrainStep:
         h = self.head_end
         return [self.grad[:h], self.grad[h:]] if 0 < h < self.grad.numel() else [self.grad]
 
-    def _allreduce_async(self, bucket):
+    def _allreduce_async(self, i):
+        """Start the all-reduce of gradient bucket ``i``.  grad_comm "bf16" (SURVEY.md §5): a bf16 copy of the
+        bucket travels (half the bytes per link), summed in bf16 by RCCL and widened back into the f32 master
+        gradient by _finish_buckets."""
         import torch.distributed as dist
+        bucket = self._grad_buckets()[i]
+        if self.grad_comm == "bf16":
+            comm = self._comm.get(i)
+            if comm is None or comm.numel() != bucket.numel():
+                comm = self._comm[i] = torch.empty(bucket.numel(), device=bucket.device, dtype=torch.bfloat16)
+            comm.copy_(bucket)
+            bucket = comm
         return dist.all_reduce(bucket, group=self.group, async_op=True)
+
+    def _finish_buckets(self, works):
+        for w in works:
+            w.wait()
+        if self.grad_comm == "bf16":
+            for i, b in enumerate(self._grad_buckets()):
+                b.copy_(self._comm[i])
 
     def allreduce_grads(self):
         """DDP gradient averaging over the flat f32 gradient (bucket by bucket; sum then / world)."""
         if self._ddp():
-            for w in [self._allreduce_async(b) for b in self._grad_buckets()]:
-                w.wait()
+            self._finish_buckets([self._allreduce_async(i) for i in range(len(self._grad_buckets()))])
             self.grad.mul_(1.0 / self.world)
 
     def train_iteration(self, x, y, flow, labels, ant_targets, masks=None):
@@ -791,13 +811,12 @@ class EVPTrainStep:
         -> wait -> average -> SGD."""
         self.sync_buffers()
         out = self.fb_head(x, y, flow, labels, ant_targets, masks)
-        buckets = self._grad_buckets()
-        works = [self._allreduce_async(buckets[0])] if self._ddp() and len(buckets) > 1 else []
+        nb = len(self._grad_buckets())
+        works = [self._allreduce_async(0)] if self._ddp() and nb > 1 else []
         self.fb_rest()
         if self._ddp():
-            works.append(self._allreduce_async(buckets[-1]))
-            for w in works:
-                w.wait()
+            works.append(self._allreduce_async(nb - 1))
+            self._finish_buckets(works)
             self.grad.mul_(1.0 / self.world)
         self.optimizer_step()
         return out
@@ -882,12 +901,11 @@ class EVPTrainStep:
         else:
             self.sync_buffers()
             self.graph.replay()
-            buckets = self._grad_buckets()
-            works = [self._allreduce_async(buckets[0])] if len(buckets) > 1 else []
+            nb = len(self._grad_buckets())
+            works = [self._allreduce_async(0)] if nb > 1 else []
             self.graph_rest.replay()
-            works.append(self._allreduce_async(buckets[-1]))
-            for w in works:
-                w.wait()
+            works.append(self._allreduce_async(nb - 1))
+            self._finish_buckets(works)
             self.graph_opt.replay()
         self._after_step()
         return self._gout
@@ -915,8 +933,13 @@ class EVPAutograd(EVPTrainStep):
 
     BIND_GRADS = False
 
-    def __init__(self, model, dtype):
-        super().__init__(model, dtype=dtype, drop=True, seed=0)
+    def __init__(self, model, dtype, counter=None):
+        # the mask stream follows torch's seed (torch.manual_seed, as the reference's DropPath / Dropout2d
+        # draws do), and a rebuilt trainer continues the previous one's device step count instead of
+        # replaying the masks of step 0
+        super().__init__(model, dtype=dtype, drop=True, seed=torch.initial_seed() & 0x7FFFFFFF)
+        if counter is not None:
+            self.counter.copy_(counter)
         self.names = list(self.params)
         self._snap()
 
@@ -971,7 +994,7 @@ class _EVPFn(torch.autograd.Function):
 def evp_trainer(model, dtype):
     t = model.__dict__.get("_svk_evp_autograd")
     if t is None or t.dt != dtype or t.frozen_changed():
-        t = EVPAutograd(model, dtype)
+        t = EVPAutograd(model, dtype, counter=None if t is None else t.counter)
         model.__dict__["_svk_evp_autograd"] = t
     return t
 

@@ -69,7 +69,7 @@ def test_shard_range_properties():
             assert max(sizes) - min(sizes) <= 1
 
 
-def _ddp_worker(rank, world, port, out):
+def _ddp_worker(rank, world, port, out, grad_comm="f32"):
     """The train step's data-parallel exchange (svk.train.EVPTrainStep.allreduce_grads over its two
     gradient buckets / sync_buffers) on CPU tensors: gradient averaging over ranks, BN buffers from
     rank 0."""
@@ -92,6 +92,7 @@ def _ddp_worker(rank, world, port, out):
                                   flow_encoder=types.SimpleNamespace(**{f"bn{i}": bns[i] for i in range(1, 5)}))
     tr = EVPTrainStep.__new__(EVPTrainStep)     # the exchange methods only, no GPU state
     tr.group, tr.world, tr.grad, tr.model, tr.head_end = dist.group.WORLD, world, grad, model, 400
+    tr.grad_comm, tr._comm = grad_comm, {}
     assert [b.numel() for b in tr._grad_buckets()] == [400, 600]      # head bucket, then the rest
     tr.allreduce_grads()
     tr.sync_buffers()
@@ -99,14 +100,23 @@ def _ddp_worker(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_train_ddp_exchange_world2():
+@pytest.mark.parametrize("grad_comm", ["f32", "bf16"])
+def test_train_ddp_exchange_world2(grad_comm):
+    """f32: the exact average; bf16 (SURVEY.md §5's compressed all-reduce): each rank's bucket rounded to bf16,
+    summed, widened back — within bf16's relative rounding of the exact average, identical on every rank."""
     world = 2
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.spawn(_ddp_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_ddp_worker, args=(world, _free_port(), out, grad_comm), nprocs=world, join=True)
     avg = (out[0][0] + out[1][0]) / 2
+    tol = dict(rtol=0, atol=0) if grad_comm == "f32" else dict(rtol=2 ** -7, atol=2 ** -7 * float(avg.abs().max()))
+    torch.testing.assert_close(out[0][1], out[1][1], rtol=0, atol=0)
     for r in range(world):
-        torch.testing.assert_close(out[r][1], avg)
+        if grad_comm == "f32":
+            torch.testing.assert_close(out[r][1], avg)
+        else:
+            torch.testing.assert_close(out[r][1], avg, **tol)
+            assert not torch.equal(out[r][1], avg)          # the bf16 path really ran
         for i in range(5):
             torch.testing.assert_close(out[r][2][i], torch.full((8,), float(i)))      # rank 0's buffers
             torch.testing.assert_close(out[r][3][i], torch.ones(8))

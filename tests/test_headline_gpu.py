@@ -95,6 +95,39 @@ def test_benched_config_bf16_b256(cuda, b256):
     np.testing.assert_allclose(gl.numpy(), yl.numpy(), rtol=0, atol=2e-2)
 
 
+@pytest.fixture(scope="module")
+def b3_256():
+    """mit_b3_evp — the model the reference's scripts build (train_evp.py:362, generate_evp_LFB.py:412) —
+    at the benched B = 256, fp32 oracle features and logits."""
+    sd = P.make_state_dict(SH.mit_evp_shapes("mit_b3_evp"), 3)
+    x, y, fl = I.frames(B, 23), I.segmaps(B, 23), I.flow(B, 23)
+    with torch.no_grad():
+        feat = M.forward(x, y, sd, "mit_b3_evp", fl, return_features=True)
+        yl, ya = _head_logits(feat, sd)
+    return sd, (x, y, fl), feat, yl, ya
+
+
+def test_mit_b3_fp16_b256_vs_oracle(cuda, b3_256):
+    """mit_b3_evp (18 stage-3 blocks against b2's 6: the longest 16-bit accumulation chain the callers run)
+    in fp16 at B = 256: both logit heads within the north-star 1e-3 of the fp32 oracle, phase argmax
+    identical for all 256 frames, features within FP16_FEAT_ATOL."""
+    from models import mix_transformer_evp as mte
+    sd, (x, y, fl), feat, yl, ya = b3_256
+    m = mte.mit_b3_evp()
+    m.load_state_dict(sd)
+    m.svk_dtype = torch.float16
+    m = m.to(cuda).eval()
+    with torch.no_grad():
+        f = m(x.to(cuda), y.to(cuda), fl.to(cuda), return_features=True).float().cpu()
+        gl, ga = (t.float().cpu() for t in m(x.to(cuda), y.to(cuda), fl.to(cuda)))
+    agree = _report("mit_b3 fp16", f, gl, ga, feat, yl, ya)
+    assert torch.isfinite(f).all()
+    np.testing.assert_allclose(f.numpy(), feat.numpy(), rtol=0, atol=FP16_FEAT_ATOL)
+    np.testing.assert_allclose(gl.numpy(), yl.numpy(), rtol=0, atol=FP16_LOGIT_ATOL)
+    np.testing.assert_allclose(ga.numpy(), ya.numpy(), rtol=0, atol=FP16_LOGIT_ATOL)
+    assert agree == 1.0 and torch.equal(gl.argmax(1), yl.argmax(1))
+
+
 def test_fp16_features_vs_reference_golden(cuda, golden):
     """fp16 path against the vectors the reference itself produced (B = 2, with flow)."""
     from models import mix_transformer_evp as mte

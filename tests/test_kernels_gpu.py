@@ -673,6 +673,26 @@ def test_stem_conv_s2d(cuda, dt, B, C, H, W, Cout):
 
 
 @pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("C,H,W,extra", [(3, 224, 224, 0), (2, 224, 224, 0), (3, 36, 20, 1), (2, 12, 28, 3),
+                                         (3, 8, 8, 4)])
+def test_nchw_to_s2d_block_grid(cuda, dt, C, H, W, extra):
+    """svk_nchw_to_s2d (pad 3, the float4 path for W % 4 == 0) == the zero-padded map rearranged into 4x4 blocks,
+    bitwise, including block grids larger than the image needs (a k = 6 stem; ADVICE r03: the last block
+    column's chunk address is clamped into the row, its values masked)."""
+    from svk import ops
+    B = 2
+    nbh, nbw = (H - 1) // 4 + 2 + extra, (W - 1) // 4 + 2 + extra
+    x = torch.randn(B, C, H, W, generator=torch.Generator().manual_seed(81)).to(cuda)
+    got = ops.nchw_to_s2d(x, dt, 4, 3, nbh, nbw)
+    pad = torch.zeros(B, C, 4 * nbh, 4 * nbw, device=cuda)
+    hh, ww = min(H, 4 * nbh - 3), min(W, 4 * nbw - 3)
+    pad[:, :, 3:3 + hh, 3:3 + ww] = x[:, :, :hh, :ww]
+    ref = pad.view(B, C, nbh, 4, nbw, 4).permute(0, 2, 4, 3, 5, 1).reshape(B, nbh, nbw, 16 * C).to(dt)
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,C,H,W", [(2, 3, 224, 224), (1, 3, 36, 20), (2, 2, 12, 28), (1, 1, 9, 13)])
 def test_gauss5x5_s2d(cuda, dt, B, C, H, W):
     """GaussianFilter.conv_gauss written as the stem's space-to-depth blocks == svk_gauss5x5_reflect's NHWC map

@@ -397,8 +397,10 @@ def _build(variant, cuda, dtype, seed=0):
     return m, sd, EVPTrainStep(m, dtype=dtype)
 
 
-@pytest.mark.parametrize("variant", ["mit_b0_evp", "mit_b2_evp"])
+@pytest.mark.parametrize("variant", ["mit_b0_evp", "mit_b2_evp", "mit_b3_evp"])
 def test_train_step_grads_fp32_vs_oracle(cuda, variant):
+    """f32 gradients of every trainable tensor vs fp64 autograd through the oracle; mit_b3_evp is the model
+    the reference's own scripts train (train_evp.py:362, finetune_evp.py:273)."""
     B = 3
     m, sd, tr = _build(variant, cuda, torch.float32)
     x, y, fl, lab, at = _train_inputs(B, 1)
@@ -570,7 +572,7 @@ def test_train_graph_replay_matches_eager(cuda):
     _close(rg, ra, 1e-2)
 
 
-def _ddp_rank(rank, world, port, out):
+def _ddp_rank(rank, world, port, out, grad_comm="f32"):
     import os
     import sys
     import torch.distributed as dist
@@ -588,7 +590,8 @@ def _ddp_rank(rank, world, port, out):
     m = m.to(dev)
     if rank == 1:                      # diverge rank 1's BN buffers: the step must re-sync them from rank 0
         m.head.linear_fuse.bn.running_mean.add_(1.0)
-    tr = EVPTrainStep(m, dtype=torch.float32, drop=False, process_group=dist.group.WORLD, world_size=world)
+    tr = EVPTrainStep(m, dtype=torch.float32, drop=False, process_group=dist.group.WORLD, world_size=world,
+                      grad_comm=grad_comm)
     x, y, fl, lab, at = (t.to(dev) for t in _train_inputs(2, 20 + rank))
     rm_before = m.head.linear_fuse.bn.running_mean.clone()
     tr.forward_backward(x, y, fl, lab, at)
@@ -601,9 +604,11 @@ def _ddp_rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_train_ddp_two_ranks_gloo(cuda):
+@pytest.mark.parametrize("grad_comm", ["f32", "bf16"])
+def test_train_ddp_two_ranks_gloo(cuda, grad_comm):
     """DDP semantics of the train step with 2 ranks (gloo over the one GPU of the test box; the
-    bench's multi-GPU runs use RCCL): averaged gradients, identical parameters after the step."""
+    bench's multi-GPU runs use RCCL): averaged gradients, identical parameters after the step.  bf16: the
+    compressed all-reduce — averages within bf16 rounding, still identical on both ranks."""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -611,9 +616,15 @@ def test_train_ddp_two_ranks_gloo(cuda):
     port = s.getsockname()[1]
     s.close()
     out = mp.Manager().dict()
-    mp.spawn(_ddp_rank, args=(2, port, out), nprocs=2, join=True)
+    mp.spawn(_ddp_rank, args=(2, port, out, grad_comm), nprocs=2, join=True)
     (l0, a0, p0, _), (l1, a1, p1, _) = out[0], out[1]
-    torch.testing.assert_close(a0, (l0 + l1) / 2, rtol=1e-5, atol=1e-7)
+    if grad_comm == "f32":
+        torch.testing.assert_close(a0, (l0 + l1) / 2, rtol=1e-5, atol=1e-7)
+    else:
+        ref = (l0 + l1) / 2
+        rel = ((a0 - ref).norm() / ref.norm()).item()
+        print(f"bf16 all-reduce: relative L2 of the averaged gradient {rel:.3e}")
+        assert 0 < rel <= 4e-3
     torch.testing.assert_close(a1, a0)
     torch.testing.assert_close(p1, p0)
     assert not torch.equal(l0, l1)                 # the ranks really saw different frames
@@ -679,7 +690,7 @@ def test_train_ddp_two_ranks_capture_replay(cuda):
     assert torch.isfinite(l0).all() and not torch.equal(l0, l1)
 
 
-def _rccl_rank(rank, world, port, out):
+def _rccl_rank(rank, world, port, out, grad_comm="f32"):
     """World-size-1 DDP over RCCL (the "nccl" backend on ROCm): the bucketed async all-reduce and the
     coalesced BN broadcast run as real RCCL collectives on the box's GPU, eagerly and around the three
     captured graphs; the same steps without a process group are the reference."""
@@ -713,7 +724,8 @@ def _rccl_rank(rank, world, port, out):
         m.load_state_dict(P.make_state_dict({k: v.shape for k, v in m.state_dict().items()}, 0))
         m = m.to(dev)
         grp = dist.group.WORLD if mode == "rccl" else None
-        tr = EVPTrainStep(m, dtype=torch.float32, drop=False, process_group=grp, world_size=world)
+        tr = EVPTrainStep(m, dtype=torch.float32, drop=False, process_group=grp, world_size=world,
+                          grad_comm=grad_comm)
         x, y, fl, lab, at = (t.to(dev) for t in _train_inputs(2, 60))
         f0 = tr.flat.detach().clone()
         tr.step(x, y, fl, lab, at)                     # eager train_iteration
@@ -730,7 +742,8 @@ def _rccl_rank(rank, world, port, out):
     dist.destroy_process_group()
 
 
-def test_train_ddp_rccl_world1_capture_replay(cuda):
+@pytest.mark.parametrize("grad_comm", ["f32", "bf16"])
+def test_train_ddp_rccl_world1_capture_replay(cuda, grad_comm):
     """init_process_group("nccl") at world size 1 on the one GPU, then
     train_iteration, capture() and two replays through the bucketed async RCCL all-reduce and the BN
     broadcast; the parameters must follow the no-process-group step."""
@@ -741,15 +754,15 @@ def test_train_ddp_rccl_world1_capture_replay(cuda):
     port = s.getsockname()[1]
     s.close()
     out = mp.Manager().dict()
-    mp.spawn(_rccl_rank, args=(1, port, out), nprocs=1, join=True)
+    mp.spawn(_rccl_rank, args=(1, port, out, grad_comm), nprocs=1, join=True)
     assert out["backend"] == "nccl"
     # 3 steps x (2 gradient buckets + 1 coalesced BN broadcast)
     assert out["calls"]["all_reduce"] == 6 and out["calls"]["broadcast"] == 3, out["calls"]
     (ur, rr, nr), (us, rs, ns) = out["res"]["rccl"], out["res"]["single"]
     assert nr == ns == 3
     rel = ((ur - us).norm() / us.norm()).item()
-    print(f"RCCL world-1 vs single-process update: relative L2 {rel:.3e}")
-    assert us.norm() > 0 and rel <= 1e-4
+    print(f"RCCL world-1 ({grad_comm} gradient exchange) vs single-process update: relative L2 {rel:.3e}")
+    assert us.norm() > 0 and rel <= (1e-4 if grad_comm == "f32" else 1e-2)
     torch.testing.assert_close(rr, rs, rtol=1e-5, atol=1e-6)
 
 
@@ -794,7 +807,7 @@ def test_train_mode_autograd_grads_equal_native_step_fp32(cuda):
     loss.backward()
     torch.cuda.synchronize()
     m2 = _ref_frozen_model("mit_b0_evp", cuda)
-    tr = EVPTrainStep(m2, dtype=torch.float32, seed=0)
+    tr = EVPTrainStep(m2, dtype=torch.float32, seed=m.__dict__["_svk_evp_autograd"].seed)
     l2, _, _ = tr.forward_backward(x, y, fl, lab, at)
     torch.cuda.synchronize()
     assert abs(loss.item() - float(l2.sum())) <= 1e-5 * max(1.0, abs(loss.item()))
@@ -817,7 +830,8 @@ def test_train_mode_autograd_grads_equal_native_step_fp32(cuda):
                                rtol=1e-5, atol=1e-6)
 
 
-def test_train_evp_loop_verbatim_fp16_b8(cuda):
+@pytest.mark.parametrize("variant", ["mit_b2_evp", "mit_b3_evp"])
+def test_train_evp_loop_verbatim_fp16_b8(cuda, variant):
     """the train_evp.py:473-515 inner loop verbatim for two steps at B = 8 —
     model.train(), autocast(float16) forward, CE(sum) + SmoothL1(sum), scaler.scale(loss).backward(),
     scaler.step(optimizer) with torch's SGD over the script's parameter groups, scaler.update() — against
@@ -826,7 +840,7 @@ def test_train_evp_loop_verbatim_fp16_b8(cuda):
     update vector within 1.5x + 1e-2 of it; measured values printed), and within 5e-2 of the native f16
     step (the autograd side back-propagates the GradScaler-scaled loss in f16)."""
     from svk.train import EVPTrainStep
-    B, variant = 8, "mit_b2_evp"
+    B = 8           # mit_b3_evp: the model train_evp.py:362 itself builds
     x, y, fl, lab, at = (t.to(cuda) for t in _train_inputs(B, 71))
     model = _ref_frozen_model(variant, cuda)
     p0 = {n: p.detach().clone() for n, p in model.named_parameters() if p.requires_grad}
@@ -853,10 +867,11 @@ def test_train_evp_loop_verbatim_fp16_b8(cuda):
             applied.append(i)
     print(f"train_evp loop: applied steps {applied}, final scale {scaler.get_scale()}")
     assert applied, "both steps skipped"
+    seed = model.__dict__["_svk_evp_autograd"].seed   # the autograd node's mask stream (torch's seed)
 
     def native(dtype):
         m2 = _ref_frozen_model(variant, cuda)
-        tr = EVPTrainStep(m2, dtype=dtype, seed=0)
+        tr = EVPTrainStep(m2, dtype=dtype, seed=seed)
         for i in applied:
             tr.counter.fill_(i)                 # the draws of forward i
             tr.step(x, y, fl, lab, at)
