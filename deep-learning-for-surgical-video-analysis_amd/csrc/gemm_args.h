@@ -32,6 +32,8 @@ struct GemmArgs {
 // T = __bf16 or _Float16 (instantiated in gemm_pk.hip).
 template <typename T> int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
 template <typename T> int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
+// gemm_pp.hip: 256 x bn (256 / 320) ping-pong persistent GEMM, dense A, plain epilogue; returns 1 when not eligible.
+template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int bn);
 
 // wgrad_pk.hip: dW (+ db) += dY^T X (16-bit operands, LDS-DMA slabs + ds_read_b64_tr_b16 fragments),
 // batched over Z = (Z / nzi, Z % nzi) element offsets; returns 1 when not eligible (caller: wgrad_kernel).

@@ -1,0 +1,332 @@
+// Ping-pong 256-row GEMM for the MFMA-bound token GEMMs (f16 / bf16 in and out, f32 accumulate):
+//
+//   C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]
+//
+// Why a second GEMM next to gemm_pk: gemm_pk's 128 x 128 tile (4 waves of 64 x 64, two workgroups per CU)
+// reads 16 fragment vectors from LDS per 32 MFMAs and synchronises its four waves twice per 64-deep K-step;
+// on the long-K / wide-N shapes (the SegFormer head, stage-3 / stage-4 fc1 / fc2 / kv) it peaks near
+// 700 TF/s while hipBLASLt runs them 1.15-1.42x faster.  This kernel is the CDNA4 "ping-pong" shape:
+//
+//  * one 512-thread workgroup per CU, a 256 x BN x 64 tile (BN = 256: 4 x 64-column waves; BN = 320: 4 x 80,
+//    so the N = 320 / 640 / 1280 shapes have no padded columns), 8 waves = 2 groups of 4: group g owns rows
+//    128 g .. 128 g + 127, wave c of a group owns columns c * BN / 4 ..; a wave's 128 x BN/4 accumulators
+//    (128 / 160 registers) live in the AGPR half of the register file;
+//  * two K-tile buffers in LDS (128 / 144 KiB), filled by LDS-DMA (`global_load_lds_dwordx4`, the XOR
+//    swizzle applied on the source address so every ds_read_b128 fragment read is conflict-free);
+//  * the two groups run ONE barrier interval apart (group 1 passes one extra s_barrier first): in every
+//    interval one group issues its 16-20 MFMAs while the other reads its next fragments from LDS and issues
+//    its share of the next K-tile's DMA, so each SIMD's matrix pipe alternates between its two waves and the
+//    fragment reads, DMA issue and barrier waits of one wave hide under the other wave's MFMAs;
+//  * a K-tile is 4 phases per group: phase p = MFMA rows 32 p .. 32 p + 31 of the wave's 128 (2 x BN/64
+//    blocks x 2 k-steps = 16 / 20 MFMAs); the wave's B fragments (BN/64 blocks x 2 k-steps) are read once per
+//    K-tile and kept in registers, A fragments 4 per phase;
+//  * persistent: a fixed grid (one workgroup per CU) walks the (tile, K-tile) stream; the next K-tile — at a
+//    tile boundary the next tile's first — is DMA'd during the current one, so tile prologues are hidden;
+//  * transposed MFMA (W fragment x A fragment): each lane holds 4 consecutive output columns of a row, so the
+//    epilogue (bias, activation, residual in f32, one rounding) stores 8-byte row pieces from registers.
+//
+// Buffer hazards (t = K-tile of the stream, buffer t % 2; interval i of the workgroup's barrier sequence):
+//  group 0 reads tile t in intervals 8t, 8t+2, 8t+4, 8t+6, group 1 in 8t+1 .. 8t+7 (odd); a read issued in
+//  interval i is retired (lgkmcnt, before the MFMAs that consume it) inside interval i + 1.  The DMA of tile
+//  t+1 overwrites tile t-1's buffer, whose last read (group 1, interval 8t-1) retired in 8t: it is issued in
+//  intervals 8t+1 / 8t+3 (group 1) and 8t+2 / 8t+4 (group 0), and every wave retires its own DMA
+//  (`s_waitcnt vmcnt(0)`) before the barrier that precedes the first read of tile t+1 (interval 8t+8): group 0
+//  at the end of its compute interval 8t+7, group 1 at the end of its LOAD interval 8t+7 (its last compute
+//  interval of tile t, 8t+8, is already past that barrier).  Raw s_barrier (never __syncthreads, whose fence drains DMA).
+#include "svk_common.h"
+#include "gemm_args.h"
+#include <stdio.h>
+#include <type_traits>
+
+namespace svk {
+namespace pp {
+
+static __device__ __attribute__((aligned(16))) uint4 g_zero[4];   // zero block: K tails
+static __device__ __attribute__((aligned(16))) uint2 g_trash[64];  // sink of the epilogue's out-of-range stores
+
+typedef __attribute__((address_space(3))) void* las_ptr;
+
+template <int BN_>
+struct Cfg {
+  static constexpr int BM = 256, BN = BN_, BK = 64, NT = 512;
+  static constexpr int WN = BN / 4, TM = 8, TN = WN / 16;
+  static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
+  static constexpr int STAGE = A_BYTES + B_BYTES, LDS = 2 * STAGE;
+  static constexpr int A_LD = A_BYTES / (NT * 16), B_LD = B_BYTES / (NT * 16);   // DMA instructions per thread
+  static_assert(WN % 16 == 0 && A_BYTES % (NT * 16) == 0 && B_BYTES % (NT * 16) == 0, "tile shape");
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(BN == 256, "the DMA stream's 8 pieces per K-tile = 4 W pieces (BN / 64) + 4 A pieces");
+};
+
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ void barrier() {
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <typename T, class C, bool KTAIL, int ACT>
+__global__ __launch_bounds__(512, 2)
+void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
+  typedef v8_t<T> tx8;
+  constexpr int BN = C::BN, WN = C::WN, TM = C::TM, TN = C::TN;
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = wave >> 2, wc = wave & 3;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int G = gridDim.x;
+  const int first = xcd_remap(blockIdx.x, G);
+  if (first >= ntiles) return;                       // whole workgroup: no barrier is left waiting
+  const T* A = static_cast<const T*>(p.A);
+  const T* Wt = static_cast<const T*>(p.W);
+  const char* zero = reinterpret_cast<const char*>(g_zero);
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
+
+  // LDS-DMA stream.  A K-tile is 8 pieces of one `global_load_lds_dwordx4` per thread: B0..B3 (W rows 32 w + 8 i
+  // .. of wave w, i = 0..3: the whole 256-row W slab) and A0..A3 (piece A_p = the rows phase p reads: 32 p ..
+  // 32 p + 31 of each group's half; wave w loads 8 of them).  Every interval of every wave issues exactly ONE
+  // piece: slot s (0..7) of the K-tile computed from stream position u issues piece (s + 1) % 8 of position
+  // u + 1 (s < 7) or piece 0 of u + 2 (s = 7), i.e. the DMA runs 9 intervals ahead.  Each interval ends with
+  // `s_waitcnt vmcnt(3)`: a piece is retired 3 intervals after its issue (group 1 one interval later), so it
+  // is readable 5 intervals after group 0 issued it — the deadlines (B pieces and A0 of position u read from
+  // interval 8u, A_p from 8u + 2p) and the buffer reuse (a piece overwrites the same piece of position u - 2,
+  // whose reads retired by interval 8u - 14 + 2p) both hold with that distance.  Per-tile row offsets
+  // (32-bit, byte offsets from A / W) are kept for the DMA cursor's tile.
+  auto opaque = [](int v) { asm volatile("" : "+s"(v)); return v; };
+  const int cq = (lane & 7) ^ ((lane >> 3) & 7);          // this lane's swizzled 16-byte chunk (rows are 8-aligned)
+  const long ldab = p.lda * 2, ldwb = p.ldw * 2;
+  uint32_t offA[4], offB[4];
+  auto set_rows = [&](int tile) {
+    tile = opaque(tile);
+    const int m0 = (tile / ntn) * C::BM, n0 = (tile % ntn) * BN;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int ra = (wave >> 2) * 128 + 32 * q + (wave & 3) * 8 + (lane >> 3);
+      const int rb = wave * 32 + 8 * q + (lane >> 3);
+      offA[q] = (uint32_t)min(m0 + ra, p.M - 1) * (uint32_t)ldab + cq * 16;
+      offB[q] = (uint32_t)min(n0 + rb, p.N - 1) * (uint32_t)ldwb + cq * 16;
+    }
+  };
+  auto issue = [&](int piece, int kt, int buf) {
+    const int q = piece & 3;
+    const bool isA = piece >= 4;
+    const char* base = isA ? reinterpret_cast<const char*>(A) : reinterpret_cast<const char*>(Wt);
+    const char* src = base + (isA ? offA[q] : offB[q]) + (uint32_t)kt * 128u;
+    if constexpr (KTAIL) src = kt * C::BK + cq * 8 < p.K ? src : zero;
+    const uint32_t row0 = isA ? (wave >> 2) * 128 + 32 * q + (wave & 3) * 8 : C::BM + wave * 32 + 8 * q;
+    dma16(src, lds0 + buf * C::STAGE + row0 * 128);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  tx8 fb[TN][2], fa[2][2];
+
+  auto read_b = [&](int buf) {
+    const char* sb = smem + buf * C::STAGE + C::A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int cc = ((ks * 4 + fq) ^ (fr & 7)) * 16;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j][ks] = *reinterpret_cast<const tx8*>(sb + (wc * WN + j * 16 + fr) * 128 + cc);
+    }
+  };
+  auto read_a = [&](int buf, int ph) {
+    const char* sa = smem + buf * C::STAGE;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int cc = ((ks * 4 + fq) ^ (fr & 7)) * 16;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        fa[i][ks] = *reinterpret_cast<const tx8*>(sa + (g * 128 + (2 * ph + i) * 16 + fr) * 128 + cc);
+    }
+  };
+  auto mfma_phase = [&](int ph) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[2 * ph + i][j] = mfma16x16x32(fb[j][ks], fa[i][ks], acc[2 * ph + i][j]);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // epilogue of one tile: lane (fr, fq) of block (i, j) holds C[m0 + 128 g + 16 i + fr][n0 + wc WN + 16 j + 4 fq ..+3].
+  // Every lane issues exactly TM * TN stores (out-of-range pieces go to a scratch row): the wait counts after
+  // the epilogue assume that number.
+  const T* R = static_cast<const T*>(p.R);
+  T* Cout = static_cast<T*>(p.C);
+  constexpr int NST = TM * TN;
+  auto epilogue = [&](int tile) {
+    tile = opaque(tile);
+    const int m0 = (tile / ntn) * C::BM + g * 128, n0 = (tile % ntn) * BN + wc * WN;
+    f32x4 bj[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = min(n0 + j * 16 + fq * 4, p.N - 4);
+      bj[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {                    // two halves of the rows: fewer live residual registers
+      uint2 res[TM / 2][TN];
+#pragma unroll
+      for (int ii = 0; ii < TM / 2; ++ii)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int m = min(m0 + (h * 4 + ii) * 16 + fr, p.M - 1), n = min(n0 + j * 16 + fq * 4, p.N - 4);
+          res[ii][j] = R ? *reinterpret_cast<const uint2*>(R + (long)m * p.ldr + n) : uint2{0u, 0u};
+        }
+#pragma unroll
+      for (int ii = 0; ii < TM / 2; ++ii) {
+        const int i = h * 4 + ii;
+        const int m = m0 + i * 16 + fr;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + j * 16 + fq * 4;
+          float v[4] = {acc[i][j][0] + bj[j].x, acc[i][j][1] + bj[j].y, acc[i][j][2] + bj[j].z, acc[i][j][3] + bj[j].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], ACT);
+          const f32x2 r01 = unpack2<T>(res[ii][j].x), r23 = unpack2<T>(res[ii][j].y);
+          v[0] += r01.x;
+          v[1] += r01.y;
+          v[2] += r23.x;
+          v[3] += r23.y;
+          T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+          uint2* dst = m < p.M && n < p.N ? reinterpret_cast<uint2*>(Cout + (long)m * p.ldc + n) : g_trash + lane;
+          *dst = *reinterpret_cast<const uint2*>(o);
+          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+    }
+  };
+
+  // ---- prologue: stream position 0 (the first tile's first K-tile) whole, retired; then piece 0 of position 1
+  int dtile = first, dkt = 0, dbuf = 0;
+  bool dlive = true;
+  auto advance = [&]() {
+    dbuf ^= 1;
+    if (++dkt == nk) {
+      dkt = 0;
+      dtile += G;
+      dlive = dtile < ntiles;
+      if (dlive) set_rows(dtile);
+    }
+  };
+  set_rows(first);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) issue(k, 0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  advance();
+  if (dlive) issue(0, dkt, dbuf);
+  barrier();
+  if (g == 1) barrier();                              // the stagger: group 1 runs one interval behind
+
+  int buf = 0;
+  bool post = false;                                  // the previous K-tile ended with an epilogue
+  for (int tile = first; tile < ntiles; tile += G) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool last = kt == nk - 1;
+      // the 8 intervals of this K-tile, each a compile-time slot (a runtime slot index would put the
+      // accumulators in scratch)
+      auto slot = [&](auto S_) {
+        constexpr int s = decltype(S_)::value, ph = s >> 1;
+        if (s == 7) advance();
+        if (dlive) issue((s + 1) & 7, dkt, dbuf);
+        if constexpr ((s & 1) == 0) {                 // ---- load interval
+          if constexpr (ph == 0) read_b(buf);
+          read_a(buf, ph);
+        } else {                                      // ---- compute interval
+          mfma_phase(ph);
+          if (s == 7 && last) epilogue(tile);
+        }
+        // the epilogue's NST stores are younger than the 2 pieces issued before them: while they may still be
+        // in flight (this interval and the next two), the count leaves them out
+        if ((s == 7 && last) || (s < 2 && post)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + 3) : "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        barrier();
+      };
+      slot(std::integral_constant<int, 0>{});
+      slot(std::integral_constant<int, 1>{});
+      slot(std::integral_constant<int, 2>{});
+      slot(std::integral_constant<int, 3>{});
+      slot(std::integral_constant<int, 4>{});
+      slot(std::integral_constant<int, 5>{});
+      slot(std::integral_constant<int, 6>{});
+      slot(std::integral_constant<int, 7>{});
+      post = last;
+      buf ^= 1;
+    }
+  }
+  if (g == 0) barrier();                              // equal barrier counts: group 0 matches the stagger
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+static int slots_of(const void* fn) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 512, 0);
+  return std::max(1, cus) * std::max(1, per);
+}
+
+template <typename T, int BN, bool KTAIL, int ACT>
+static int launch(const GemmArgs& a, hipStream_t st) {
+  typedef Cfg<BN> C;
+  const int ntm = (a.M + C::BM - 1) / C::BM, ntn = (a.N + BN - 1) / BN;
+  const long ntiles = (long)ntm * ntn;
+  const int nk = (a.K + 63) / 64;
+  static const int slots = slots_of(reinterpret_cast<const void*>(&gemm_pp<T, C, KTAIL, ACT>));
+  const int grid = (int)std::min<long>(ntiles, slots);
+  hipLaunchKernelGGL((gemm_pp<T, C, KTAIL, ACT>), dim3(grid), dim3(512), 0, st, a, ntn, (int)ntiles, nk);
+  static char name[96];
+  if (!name[0])
+    snprintf(name, sizeof(name), "gemm_pp<%s, Cfg<%d>, %s, %d>", type_name<T>(), BN, KTAIL ? "true" : "false", ACT);
+  set_last_kernel(name);
+  return check_launch("gemm_pp");
+}
+
+template <typename T, int BN>
+static int launch_bn(const GemmArgs& a, hipStream_t st) {
+  const bool tail = a.K % 64 != 0;
+  switch (a.act) {
+    case SVK_ACT_GELU: return tail ? launch<T, BN, true, SVK_ACT_GELU>(a, st) : launch<T, BN, false, SVK_ACT_GELU>(a, st);
+    case SVK_ACT_RELU: return tail ? launch<T, BN, true, SVK_ACT_RELU>(a, st) : launch<T, BN, false, SVK_ACT_RELU>(a, st);
+    case 0: return tail ? launch<T, BN, true, 0>(a, st) : launch<T, BN, false, 0>(a, st);
+    default: return 1;
+  }
+}
+
+}  // namespace pp
+
+// Dense A only (asrc 0), plain epilogue (bias / GELU / ReLU / residual), K % 8 == 0, N % 4 == 0, 16-byte
+// aligned operand rows.  bn: 256 or 320.  Returns 1 when not eligible.
+template <typename T>
+int gemm_pp_try(const GemmArgs& a, hipStream_t st, int bn) {
+  auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
+  if (a.K % 8 || a.N % 4 || a.lda % 8 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4) || a.out_mode || a.U ||
+      a.rscale || a.ksplit > 1)
+    return 1;
+  if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
+  // 32-bit byte offsets of the DMA rows
+  if ((long)a.M * a.lda * 2 + 256 >= (1L << 32) || (long)a.N * a.ldw * 2 + 256 >= (1L << 32)) return 1;
+  if (bn == 256) return pp::launch_bn<T, 256>(a, st);
+  return 1;
+}
+
+template int gemm_pp_try<bf16>(const GemmArgs&, hipStream_t, int);
+template int gemm_pp_try<f16>(const GemmArgs&, hipStream_t, int);
+
+}  // namespace svk

@@ -32,12 +32,14 @@ constexpr int PP_ROWS = 4;     // sweep (B = 256, 480x854): 2 rows 893k, 4 rows 
 
 __global__ __launch_bounds__(256) void pp_resize_h(const uint8_t* __restrict__ in, uint8_t* __restrict__ tmp,
                                                    const int* __restrict__ xb, const int* __restrict__ xk, int ksx,
-                                                   int B, int H, int W, int CW, int cx0) {
+                                                   int B, int H, int W, int CW, int cx0, const int* __restrict__ prm,
+                                                   int pstride) {
   extern __shared__ uint4 pp_lds[];
   uint8_t* rows = reinterpret_cast<uint8_t*>(pp_lds);
   const int blocks_per_frame = (H + PP_ROWS - 1) / PP_ROWS;
   const int b = blockIdx.x / blocks_per_frame;
   const int y0 = (blockIdx.x - b * blocks_per_frame) * PP_ROWS;
+  if (prm) cx0 = prm[b * pstride];                             // training: the sample's RandomCrop column offset
   const int nr = min(PP_ROWS, H - y0);
   const long rowbytes = (long)W * 3;
   const long start = ((long)b * H + y0) * rowbytes;
@@ -176,6 +178,14 @@ __global__ __launch_bounds__(256) void pp_flow(const float* __restrict__ in, flo
   o[plane] = __fmul_rn(v, sv);
 }
 
+void pp_resize_h_launch(const uint8_t* in, uint8_t* tmp, const int* xb, const int* xk, int ksx, int B, int H, int W,
+                        int CW, int cx0, const int* prm, int pstride, hipStream_t s) {
+  const long lds = ((16 + (long)PP_ROWS * W * 3 + 15) / 16) * 16;
+  const int bpf = (H + PP_ROWS - 1) / PP_ROWS;
+  hipLaunchKernelGGL(pp_resize_h, dim3((unsigned)((long)B * bpf)), dim3(256), (size_t)lds, s, in, tmp, xb, xk, ksx, B, H,
+                     W, CW, cx0, prm, pstride);
+}
+
 }  // namespace svk
 
 using namespace svk;
@@ -199,9 +209,7 @@ extern "C" int svk_frame_preproc(const void* frames, void* tmp, float* out, cons
   }
   const long lds = ((16 + (long)PP_ROWS * W * 3 + 15) / 16) * 16;
   if (lds > 64 * 1024) { set_error("svk_frame_preproc: frame width %d too large (W*3*%d > 64 KiB)", W, PP_ROWS); return SVK_EUNSUPPORTED; }
-  const int bpf = (H + PP_ROWS - 1) / PP_ROWS;
-  hipLaunchKernelGGL(pp_resize_h, dim3((unsigned)((long)B * bpf)), dim3(256), (size_t)lds, s, (const uint8_t*)frames,
-                     (uint8_t*)tmp, xbounds, xcoef, ksx, B, H, W, CW, crop_x0);
+  pp_resize_h_launch((const uint8_t*)frames, (uint8_t*)tmp, xbounds, xcoef, ksx, B, H, W, CW, crop_x0, nullptr, 0, s);
   const bool vec = CW % 4 == 0 && ((uintptr_t)tmp & 3) == 0 && ((uintptr_t)out & 15) == 0;
   if (vec)
     hipLaunchKernelGGL((pp_resize_v_norm<4>), dim3((unsigned)((tv / 4 + 255) / 256)), dim3(256), 0, s,

@@ -105,29 +105,29 @@ class RandomCrop(object):
         self.padding = padding
         self.count = 0
 
+    def draw(self, w, h):
+        """The offset __call__ draws for a (padded) w x h input — (x1, y1), count advanced — or None when the
+        input already has the crop size (no draw, no count: data_process.py:71-72)."""
+        th, tw = self.size
+        if w == tw and h == th:
+            return None
+        random.seed(self.count // sequence_length)
+        x1 = random.randint(0, w - tw)
+        y1 = random.randint(0, h - th)
+        self.count += 1
+        return x1, y1
+
     def __call__(self, img):
         th, tw = self.size
         if isinstance(img, torch.Tensor):
             if self.padding > 0:
                 img = F.pad(img, (self.padding,) * 4, value=0)
-            h, w = img.shape[-2], img.shape[-1]
-            if w == tw and h == th:
-                return img
-            random.seed(self.count // sequence_length)
-            x1 = random.randint(0, w - tw)
-            y1 = random.randint(0, h - th)
-            self.count += 1
-            return img[..., y1:y1 + th, x1:x1 + tw]
+            xy = self.draw(img.shape[-1], img.shape[-2])
+            return img if xy is None else img[..., xy[1]:xy[1] + th, xy[0]:xy[0] + tw]
         if self.padding > 0:
             img = ImageOps.expand(img, border=self.padding, fill=0)
-        w, h = img.size
-        if w == tw and h == th:
-            return img
-        random.seed(self.count // sequence_length)
-        x1 = random.randint(0, w - tw)
-        y1 = random.randint(0, h - th)
-        self.count += 1
-        return img.crop((x1, y1, x1 + tw, y1 + th))
+        xy = self.draw(*img.size)
+        return img if xy is None else img.crop((xy[0], xy[1], xy[0] + tw, xy[1] + th))
 
 
 class RandomHorizontalFlip(object):
@@ -137,11 +137,15 @@ class RandomHorizontalFlip(object):
     def __init__(self):
         self.count = 0
 
-    def __call__(self, img):
+    def draw(self):
+        """True when this call flips (count advanced)."""
         random.seed(self.count // sequence_length)
         prob = random.random()
         self.count += 1
-        if prob >= 0.5:
+        return prob < 0.5
+
+    def __call__(self, img):
+        if not self.draw():
             return img
         if isinstance(img, torch.Tensor):
             img = img.flip(-1)
@@ -159,10 +163,14 @@ class RandomRotation(object):
         self.degrees = degrees
         self.count = 0
 
-    def __call__(self, img):
+    def draw(self):
+        """The integer angle of this call (count advanced)."""
         random.seed(self.count // sequence_length)
         self.count += 1
-        angle = random.randint(-self.degrees, self.degrees)
+        return random.randint(-self.degrees, self.degrees)
+
+    def __call__(self, img):
+        angle = self.draw()
         if isinstance(img, torch.Tensor):
             img = _rotate_tensor_nearest(img, angle)
             if img.shape[0] == 2:

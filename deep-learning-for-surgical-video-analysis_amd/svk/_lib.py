@@ -57,6 +57,9 @@ SIGNATURES = {
     "svk_frame_preproc": [P, P, P, P, P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
                           P],
     "svk_flow_preproc": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P],
+    "svk_train_augment": [P, P, P, P, P, P, P, c_int, P, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                          P, P, P],
+    "svk_train_augment_flow": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P],
     "svk_anticipation_gt": [P, c_long, c_int, c_int, ctypes.c_double, P, P],
     "svk_window_unfold": [c_int, P, c_long, P, P, c_int, c_int, c_int, P],
     "svk_add_bcast": [c_int, P, P, P, c_long, c_int, c_int, P],

@@ -321,6 +321,26 @@ int svk_flow_preproc(const float* flow, float* out, const int* xofs, const float
                      const float* yalpha, int B, int H, int W, int crop_y0, int crop_x0, int CH, int CW,
                      float scale_u, float scale_v, void* stream);
 
+/* Training augmentations (train_evp.py:146-163 via data_process.py:53-186; replaces the DataLoader workers'
+ * PIL transform of CholecFlowDataset.__getitem__, data_process.py:455-462): decoded uint8 frames / RGB segmaps
+ * [B, H, W, 3] -> Pillow bilinear Resize to RH x RW -> RandomCrop CH x CW at (params[b*16+0], params[b*16+1]) ->
+ * [ColorJitter] -> [flip] -> [rotate] -> ToTensor -> Normalize -> out [B, 3, CH, CW] f32, bit-exact to Pillow.
+ * params [B][16] int32: x1, y1, flip, rot, a0..a5 (Image.rotate's inverse matrix in 16.16 fixed point), jitter,
+ * brightness, contrast, saturation (f32 bits), hue shift (0..255), unused.  Workspace: tmp [B, H, CW, 3] uint8,
+ * crop [B, CH, CW, 3] uint8, sums [B] int64.  Resize tables as svk_frame_preproc (for H -> RH, W -> RW). */
+int svk_train_augment(const void* frames, void* tmp, void* crop, long long* sums, float* out, const int* xbounds,
+                      const int* xcoef, int ksx, const int* ybounds, const int* ycoef, int ksy, const int* params,
+                      int B, int H, int W, int RH, int RW, int CH, int CW, const float* mean, const float* std,
+                      void* stream);
+
+/* The geometric training augmentations on the RAFT flow (data_process.py:471-487): cv2 INTER_LINEAR resize +
+ * displacement scale (tables as svk_flow_preproc), RandomCrop at (x1, y1), [flip: u negated], [rotate: nearest
+ * affine grid sample + vector rotation] -> out [B, 2, CH, CW] f32.  params [B][16] int32: x1, y1, flip, rot, t00,
+ * t01, t02, t10, t11, t12 (the grid's rescaled inverse rotation, f32 bits), cos, sin (f32 bits). */
+int svk_train_augment_flow(const float* flow, float* out, const int* xofs, const float* xalpha, const int* yofs,
+                           const float* yalpha, const int* params, int B, int H, int W, int CH, int CW, float scale_u,
+                           float scale_v, void* stream);
+
 /* Phase-anticipation targets (generate_phase_anticipation.py:10-34, generate_anticipation_gt): phases
  * [P, T] int64 one-hot presence (row stride ldp), horizon in minutes -> out [T, P] f32; per phase a
  * backward recurrence count = present ? 0 : min(horizon, count + 1/1500) in double, out = f32(count) / f32(horizon). */

@@ -11,3 +11,5 @@ step blaslt timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format c
 cat $O/blaslt.log | grep -v amdgpu.ids
 step train timeout -k 10 600 python -u -m pytest tests/test_train_gpu.py tests/test_temporal_train_gpu.py -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_train.log 2>&1
 tail -3 $O/pytest_train.log
+step new timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_headline_gpu.py -q -rf -k "s2d or b3" --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_new.log 2>&1
+tail -3 $O/pytest_new.log
