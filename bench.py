@@ -401,6 +401,66 @@ def workload_preproc(args, dev, rank, dtype):
     return step, args.batch, config, check, (lambda: cpu_baseline_preproc(min(args.cpu_baseline_seconds, 10.0)))
 
 
+def cpu_baseline_augment(budget_s, H=480, W=854):
+    """One training sample as the reference's DataLoader worker makes it (decoded frame + segmap through Pillow:
+    Resize, RandomCrop, ColorJitter, flip, rotate, ToTensor, Normalize; the flow through cv2-style resize + the
+    tensor crop / flip / rotation) with the drop-in synced classes, one host thread."""
+    import random
+    from PIL import Image
+    from models import data_process as DP
+    from oracle import preproc as OP
+    rng = np.random.default_rng(0)
+    img, seg = (rng.integers(0, 256, size=(H, W, 3), dtype=np.uint8) for _ in range(2))
+    flow = rng.normal(size=(H, W, 2)).astype(np.float32)
+    crop, jit, flip, rot = DP.RandomCrop(224), DP.ColorJitter(0.1, 0.1, 0.1, 0.05), DP.RandomHorizontalFlip(), DP.RandomRotation(5)
+    m, s = torch.tensor(DP.MEAN)[:, None, None], torch.tensor(DP.STD)[:, None, None]
+
+    def pil(a):
+        im = Image.fromarray(a).resize((250, 250), Image.BILINEAR)
+        for t in (crop, jit, flip, rot):
+            im = t(im)
+        return torch.from_numpy(np.array(im)).permute(2, 0, 1).float().div(255).sub_(m).div_(s)
+
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < budget_s or n == 0:
+        pil(img)
+        pil(seg)
+        r = OP.cv2_resize_linear(flow, (250, 250))
+        t = torch.from_numpy(np.ascontiguousarray(r.transpose(2, 0, 1)))
+        rot(flip(crop(t)))
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 2), "unit": "frames/s", "cores": 1, "kind": "port",
+            "sample": f"{n} samples {H}x{W} (frame + segmap through Pillow, flow through the host tensor path; "
+                      f"train_evp.py use_flip=1 transform, one worker thread) in {dt:.1f} s"}
+
+
+def workload_augment(args, dev, rank, dtype):
+    """train_evp.py's training transform (use_flip=1) on a B-sample batch of decoded 480x854 frames, RGB segmaps
+    and RAFT flows resident in HBM (svk.augment.TrainAugment: synced parameter draws on the host, bit-exact
+    Pillow arithmetic on the GPU); one step = one batch."""
+    from svk.augment import TrainAugment
+    H, W = 480, 854
+    g = torch.Generator(device=dev)
+    g.manual_seed(4321 + rank)
+    frames = torch.randint(0, 256, (args.batch, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    segs = torch.randint(0, 256, (args.batch, H, W, 3), dtype=torch.uint8, device=dev, generator=g)
+    flows = torch.randn(args.batch, H, W, 2, device=dev, generator=g)
+    aug = TrainAugment(use_flip=1)
+
+    def step():
+        return aug(frames, segs, flows)[0]
+
+    def check(o):
+        assert o.shape == (args.batch, 3, 224, 224) and torch.isfinite(o).all()
+
+    config = {"workload": "train_evp.py training transform (use_flip=1): Resize(250) -> RandomCrop(224) -> ColorJitter -> "
+                          "flip -> RandomRotation(5) -> ToTensor -> Normalize on decoded 480x854 frames + RGB segmaps "
+                          "(Pillow-exact), crop / flip / rotation on the RAFT flow; synced host draws per sample",
+              "per_gpu_batch": args.batch}
+    return step, args.batch, config, check, (lambda: cpu_baseline_augment(min(args.cpu_baseline_seconds, 10.0)))
+
+
 def cpu_baseline_e2e(variant, budget_s, modules, inputs, chunk=32):
     """Config 5's chain restated on the oracle (torch CPU, fp32) on a bounded sample: ``chunk`` frames of
     the benched inputs through the SAME weights as the GPU modules.  The GPU chain runs once on the same
@@ -630,7 +690,7 @@ def workload_tecno_train(args, dev, rank, dtype):
     return step, sum(lens), config, check, (lambda: cpu_baseline_tecno_train(kind, args.cpu_baseline_seconds))
 
 
-WORKLOADS = {"extract": workload_extract, "lfb": workload_lfb, "mstcn": workload_mstcn, "mamba": workload_mamba, "preproc": workload_preproc, "e2e": workload_e2e, "train": workload_train,
+WORKLOADS = {"extract": workload_extract, "lfb": workload_lfb, "augment": workload_augment, "mstcn": workload_mstcn, "mamba": workload_mamba, "preproc": workload_preproc, "e2e": workload_e2e, "train": workload_train,
              "tecno_train": workload_tecno_train}
 
 
@@ -858,7 +918,7 @@ def run_leg(args, dev, rank, world, dtype):
                                "steps": n2}
             step.set_dtype(dtype)
     value = world * units * args.steps / elapsed
-    f32_only = args.workload in ("mstcn", "mamba", "preproc", "tecno_train")
+    f32_only = args.workload in ("mstcn", "mamba", "preproc", "tecno_train", "augment")
     dtype_name = "fp32" if f32_only else args.dtype
     roofline = roofline_of(records, prof_steps, elapsed, args.steps, args.workload, dtype_name, value, world,
                            args.dump_gemm if rank == 0 else None)

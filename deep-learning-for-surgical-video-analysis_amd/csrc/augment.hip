@@ -30,8 +30,13 @@ constexpr int AUG_PREC = 22;
 constexpr int AUG_NP = 16;   // int32 parameters per sample (see svk.h)
 
 __device__ __forceinline__ int aug_clip8(int ss) {
-  const int v = ss >> AUG_PREC;
-  return v < 0 ? 0 : (v > 255 ? 255 : v);
+  int v = ss >> AUG_PREC;
+  v = v < 0 ? 0 : (v > 255 ? 255 : v);
+  // keep hipcc 7.2 from fusing two (shift, clamp, pack) chains into v_ashr_pk_u8_i32: its lowering assumes
+  // the instruction zeroes bits 31:16 of the destination, the hardware keeps them (bytes 6 and 10 of each
+  // 12-byte group came out OR-ed with a neighbour); isa_check.py rejects the instruction in every object
+  asm volatile("" : "+v"(v));
+  return v;
 }
 
 // vertical Pillow pass over the horizontal result tmp [B, H, CW, 3] (CW = crop width, columns already at the

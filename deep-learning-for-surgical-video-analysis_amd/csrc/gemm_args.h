@@ -25,6 +25,9 @@ struct GemmArgs {
   int out_mode, uH, uW, us, uC;
   // split-K (gemm_pk_conv_splitk): raw f32 partial sums of ksplit K parts -> slab [ksplit][M][N]
   int ksplit; float* slab;
+  // stream-K workspace of the launching stream (gemm_pp; svk_set_stream_workspace): partial sums for up to
+  // sk_slots workgroups and one flag per (workgroup, wave), zero between launches
+  void* sk_part; int* sk_flags; int sk_slots;
 };
 
 // gemm_pk.hip: persistent LDS-DMA bf16 / f16 GEMM / implicit-GEMM conv (asrc 1) for the plain-epilogue
@@ -32,8 +35,9 @@ struct GemmArgs {
 // T = __bf16 or _Float16 (instantiated in gemm_pk.hip).
 template <typename T> int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
 template <typename T> int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
-// gemm_pp.hip: 256 x bn (256 / 320) ping-pong persistent GEMM, dense A, plain epilogue; returns 1 when not eligible.
-template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int bn);
+// gemm_pp.hip: 256 x 256 ping-pong persistent GEMM, dense A, plain epilogue; variant 0 / 1 = first / deep DMA
+// schedule, 2 = deep + stream-K; returns 1 when not eligible.
+template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant);
 
 // wgrad_pk.hip: dW (+ db) += dY^T X (16-bit operands, LDS-DMA slabs + ds_read_b64_tr_b16 fragments),
 // batched over Z = (Z / nzi, Z % nzi) element offsets; returns 1 when not eligible (caller: wgrad_kernel).

@@ -73,7 +73,15 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <typename T, class C, bool KTAIL, int ACT>
+// SK (stream-K): the grid's workgroups split the ntiles * nk K-tiles of the whole GEMM into equal contiguous
+// ranges, so no CU idles in a last partial wave of tiles.  A range starts and ends inside tiles: its first piece
+// (if it starts past a tile's K-tile 0) is written as f32 partial sums to part[w] and announced by one flag per
+// wave (plain 16-byte stores, vmcnt(0), agent release fence, relaxed agent flag store); its last piece, if it
+// ends before the tile's last K-tile, waits for the flags of the following workgroups that hold the rest of the
+// tile (relaxed poll, agent acquire), adds their partials in workgroup order and runs the epilogue.  Partials are
+// produced at the START of a range and consumed at its END, so the waits are short; a workgroup only waits for
+// higher-numbered ones, which never wait for it (no cycle).  The consumer resets each flag it consumed.
+template <typename T, class C, bool KTAIL, int ACT, int DEEP, bool SK>
 __global__ __launch_bounds__(512, 2)
 void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   typedef v8_t<T> tx8;
@@ -85,8 +93,12 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   const int g = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int G = gridDim.x;
-  const int first = xcd_remap(blockIdx.x, G);
-  if (first >= ntiles) return;                       // whole workgroup: no barrier is left waiting
+  const int first = xcd_remap(blockIdx.x, G);         // data-parallel: first tile; stream-K: range index
+  // (the host keeps ntiles * nk * G < 2^31; readfirstlane: the integer divisions run on the vector unit)
+  const int units = ntiles * nk;
+  const int ustart = SK ? __builtin_amdgcn_readfirstlane(first * units / G) : 0;
+  const int uend = SK ? __builtin_amdgcn_readfirstlane((first + 1) * units / G) : 0;
+  if (SK ? ustart >= uend : first >= ntiles) return;   // whole workgroup: no barrier is left waiting
   const T* A = static_cast<const T*>(p.A);
   const T* Wt = static_cast<const T*>(p.W);
   const char* zero = reinterpret_cast<const char*>(g_zero);
@@ -94,14 +106,18 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
 
   // LDS-DMA stream.  A K-tile is 8 pieces of one `global_load_lds_dwordx4` per thread: B0..B3 (W rows 32 w + 8 i
   // .. of wave w, i = 0..3: the whole 256-row W slab) and A0..A3 (piece A_p = the rows phase p reads: 32 p ..
-  // 32 p + 31 of each group's half; wave w loads 8 of them).  Every interval of every wave issues exactly ONE
-  // piece: slot s (0..7) of the K-tile computed from stream position u issues piece (s + 1) % 8 of position
-  // u + 1 (s < 7) or piece 0 of u + 2 (s = 7), i.e. the DMA runs 9 intervals ahead.  Each interval ends with
-  // `s_waitcnt vmcnt(3)`: a piece is retired 3 intervals after its issue (group 1 one interval later), so it
-  // is readable 5 intervals after group 0 issued it — the deadlines (B pieces and A0 of position u read from
-  // interval 8u, A_p from 8u + 2p) and the buffer reuse (a piece overwrites the same piece of position u - 2,
-  // whose reads retired by interval 8u - 14 + 2p) both hold with that distance.  Per-tile row offsets
-  // (32-bit, byte offsets from A / W) are kept for the DMA cursor's tile.
+  // 32 p + 31 of each group's half; wave w loads 8 of them, group g's waves exactly group g's rows).  Every
+  // interval of every wave issues exactly ONE piece, in stream order, so `s_waitcnt vmcnt(NW)` at the end of
+  // every interval retires each piece NW intervals after its issue (readable one interval later; group 1 issues
+  // one interval after group 0).  Issue time of piece k of stream position u: 8u - DD + k (group 0's interval
+  // numbering).  Deadlines: the B pieces are read by group 0 from 8u on — group 1's copy must retire by 8u - 1:
+  // DD - 3 >= NW + 2; A_p is read by its own group from 8u + 2p: DD - 4 - p >= NW + 1 - 2p.  Buffer reuse (a
+  // piece overwrites the same piece of position u - 2): B after 8u - 14 (group 1's reads of u - 2 retired),
+  // A_p after 8u - 15 + 2p: DD <= 13.  DEEP = 0: DD = 9, NW = 3 (round-4 first form); DEEP = 1: DD = 13,
+  // NW = 8 — each piece gets 8 intervals (~2-4k cycles) to land instead of 3.
+  constexpr int DD = DEEP ? 13 : 9, NW = DEEP ? 8 : 3;
+  constexpr int OFF = DD & 7;                               // slot s issues piece (s + OFF) % 8 ...
+  static_assert(DD - 3 >= NW + 2 && DD - 4 >= NW + 1 && DD <= 13, "DMA schedule");
   auto opaque = [](int v) { asm volatile("" : "+s"(v)); return v; };
   const int cq = (lane & 7) ^ ((lane >> 3) & 7);          // this lane's swizzled 16-byte chunk (rows are 8-aligned)
   const long ldab = p.lda * 2, ldwb = p.ldw * 2;
@@ -171,7 +187,7 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   T* Cout = static_cast<T*>(p.C);
   constexpr int NST = TM * TN;
   auto epilogue = [&](int tile) {
-    tile = opaque(tile);
+    asm volatile("" : "+v"(tile));                   // opaque (see set_rows); a VGPR operand works on every path
     const int m0 = (tile / ntn) * C::BM + g * 128, n0 = (tile % ntn) * BN + wc * WN;
     f32x4 bj[TN];
 #pragma unroll
@@ -213,64 +229,145 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
     }
   };
 
-  // ---- prologue: stream position 0 (the first tile's first K-tile) whole, retired; then piece 0 of position 1
-  int dtile = first, dkt = 0, dbuf = 0;
+  // ---- stream-K partial sums: part[((w * 8 + wave) * NST + i * TN + j) * 64 + lane] (f32x4, lane-major: every
+  // store / load instruction is one contiguous KiB), flags[w * 8 + wave]
+  f32x4* const part = reinterpret_cast<f32x4*>(p.sk_part);
+  int* const flags = p.sk_flags;
+  auto store_partial = [&]() {
+    int slot = (first * 8 + wave) * NST * 64 + lane;
+    asm volatile("" : "+v"(slot));                   // opaque: the store addresses must not be hoisted out of the loop
+    // inline asm, one base address per row block and immediate offsets for its TN column blocks (1 KiB apart):
+    // compiler-visible stores made hipcc materialise all 32 addresses (and copies of the accumulators) at once
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      f32x4* row = part + slot + i * TN * 64;
+      static_assert(TN <= 4, "immediate offsets up to 3 KiB");
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        asm volatile("global_store_dwordx4 %0, %1, off offset:%2" ::"v"(row), "v"(acc[i][j]), "n"(j * 1024) : "memory");
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) __hip_atomic_store(flags + first * 8 + wave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto fixup = [&](int tile) {
+    const int tend = (tile + 1) * nk;
+    for (int w2 = first + 1; w2 < G && __builtin_amdgcn_readfirstlane(w2 * units / G) < tend; ++w2) {
+      int* fl = flags + w2 * 8 + wave;
+      while (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int slot = (w2 * 8 + wave) * NST * 64 + lane;
+      asm volatile("" : "+v"(slot));
+      const f32x4* src = part + slot;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {               // one row block at a time: 16 registers of partials in flight
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] += src[(i * TN + j) * 64];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (lane == 0) __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+
+  // ---- prologue: stream position 0 whole and the first OFF pieces of position 1 (their nominal issue intervals
+  // are negative); position 0 retired before the first barrier
+  int dtile = SK ? __builtin_amdgcn_readfirstlane(ustart / nk) : first;
+  int dkt = SK ? __builtin_amdgcn_readfirstlane(ustart % nk) : 0, dbuf = 0;
+  int dunit = ustart;
   bool dlive = true;
   auto advance = [&]() {
     dbuf ^= 1;
+    if constexpr (SK) dlive = ++dunit < uend;
     if (++dkt == nk) {
       dkt = 0;
-      dtile += G;
-      dlive = dtile < ntiles;
+      dtile += SK ? 1 : G;
+      if constexpr (!SK) dlive = dtile < ntiles;
       if (dlive) set_rows(dtile);
     }
   };
-  set_rows(first);
+  set_rows(dtile);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) issue(k, 0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  for (int k = 0; k < 8; ++k) issue(k, dkt, 0);
   advance();
-  if (dlive) issue(0, dkt, dbuf);
+#pragma unroll
+  for (int k = 0; k < OFF; ++k)
+    if (dlive) issue(k, dkt, dbuf);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OFF) : "memory");
   barrier();
   if (g == 1) barrier();                              // the stagger: group 1 runs one interval behind
 
   int buf = 0;
-  bool post = false;                                  // the previous K-tile ended with an epilogue
-  for (int tile = first; tile < ntiles; tile += G) {
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool last = kt == nk - 1;
-      // the 8 intervals of this K-tile, each a compile-time slot (a runtime slot index would put the
-      // accumulators in scratch)
-      auto slot = [&](auto S_) {
-        constexpr int s = decltype(S_)::value, ph = s >> 1;
-        if (s == 7) advance();
-        if (dlive) issue((s + 1) & 7, dkt, dbuf);
-        if constexpr ((s & 1) == 0) {                 // ---- load interval
-          if constexpr (ph == 0) read_b(buf);
-          read_a(buf, ph);
-        } else {                                      // ---- compute interval
-          mfma_phase(ph);
-          if (s == 7 && last) epilogue(tile);
+  int post = 0;                                       // intervals left in which the epilogue's stores may still fly
+  int tile = dtile, kt = dkt;
+  int kfirst = kt;                                    // K-tile the current piece of the tile started at
+  int u = ustart;
+  while (SK ? u < uend : tile < ntiles) {
+    const bool tlast = kt == nk - 1, rlast = SK && u == uend - 1;
+    // the 8 intervals of this K-tile, each a compile-time slot (a runtime slot index would put the
+    // accumulators in scratch)
+    auto slot = [&](auto S_) {
+      constexpr int s = decltype(S_)::value, ph = s >> 1, piece = (s + OFF) & 7;
+      if (piece == 0) advance();                      // the cursor moves to the next stream position
+      if (dlive) issue(piece, dkt, dbuf);
+      if constexpr ((s & 1) == 0) {                   // ---- load interval
+        if constexpr (ph == 0) read_b(buf);
+        read_a(buf, ph);
+      } else {                                        // ---- compute interval
+        mfma_phase(ph);
+        if (s == 7 && (tlast || rlast)) {
+          if (SK && kfirst > 0) {                     // a piece that began mid-tile: partial sums out
+            store_partial();
+            post = 0;
+          } else if (!SK || tlast) {
+            epilogue(tile);
+            post = NW;
+          }
+          // else: the range ends with a tile's head piece — fixup + epilogue after the loop (out of the
+          // pipelined body, which keeps its register allocation)
         }
-        // the epilogue's NST stores are younger than the 2 pieces issued before them: while they may still be
-        // in flight (this interval and the next two), the count leaves them out
-        if ((s == 7 && last) || (s < 2 && post)) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + 3) : "memory");
-        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        barrier();
-      };
-      slot(std::integral_constant<int, 0>{});
-      slot(std::integral_constant<int, 1>{});
-      slot(std::integral_constant<int, 2>{});
-      slot(std::integral_constant<int, 3>{});
-      slot(std::integral_constant<int, 4>{});
-      slot(std::integral_constant<int, 5>{});
-      slot(std::integral_constant<int, 6>{});
-      slot(std::integral_constant<int, 7>{});
-      post = last;
-      buf ^= 1;
+      }
+      // the epilogue's NST stores are younger than the NW pieces issued before them: for NW intervals the
+      // count leaves them out as well
+      if (post > 0) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + NW) : "memory");
+        --post;
+      } else {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NW) : "memory");
+      }
+      barrier();
+    };
+    slot(std::integral_constant<int, 0>{});
+    slot(std::integral_constant<int, 1>{});
+    slot(std::integral_constant<int, 2>{});
+    slot(std::integral_constant<int, 3>{});
+    slot(std::integral_constant<int, 4>{});
+    slot(std::integral_constant<int, 5>{});
+    slot(std::integral_constant<int, 6>{});
+    slot(std::integral_constant<int, 7>{});
+    buf ^= 1;
+    ++u;
+    if (tlast) {
+      kt = 0;
+      kfirst = 0;
+      tile += SK ? 1 : G;
+    } else {
+      ++kt;
     }
   }
   if (g == 0) barrier();                              // equal barrier counts: group 0 matches the stagger
+  if constexpr (SK) {
+    const int te = __builtin_amdgcn_readfirstlane((uend - 1) / nk), ke = __builtin_amdgcn_readfirstlane((uend - 1) % nk);
+    const int ts = __builtin_amdgcn_readfirstlane(ustart / nk), ks = __builtin_amdgcn_readfirstlane(ustart % nk);
+    if (ke < nk - 1 && !(ts == te && ks > 0)) {        // the last piece is a tile's head
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      fixup(te);
+      epilogue(te);
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -282,29 +379,33 @@ static int slots_of(const void* fn) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <typename T, int BN, bool KTAIL, int ACT>
+template <typename T, int BN, bool KTAIL, int ACT, int DEEP, bool SK>
 static int launch(const GemmArgs& a, hipStream_t st) {
   typedef Cfg<BN> C;
   const int ntm = (a.M + C::BM - 1) / C::BM, ntn = (a.N + BN - 1) / BN;
   const long ntiles = (long)ntm * ntn;
   const int nk = (a.K + 63) / 64;
-  static const int slots = slots_of(reinterpret_cast<const void*>(&gemm_pp<T, C, KTAIL, ACT>));
-  const int grid = (int)std::min<long>(ntiles, slots);
-  hipLaunchKernelGGL((gemm_pp<T, C, KTAIL, ACT>), dim3(grid), dim3(512), 0, st, a, ntn, (int)ntiles, nk);
+  static const int slots = slots_of(reinterpret_cast<const void*>(&gemm_pp<T, C, KTAIL, ACT, DEEP, SK>));
+  const int grid = (int)std::min<long>(SK ? ntiles * nk : ntiles, slots);
+  if (SK && (!a.sk_part || !a.sk_flags || a.sk_slots < grid || ntiles * (long)nk * grid >= (1L << 31))) return 1;
+  hipLaunchKernelGGL((gemm_pp<T, C, KTAIL, ACT, DEEP, SK>), dim3(grid), dim3(512), 0, st, a, ntn, (int)ntiles, nk);
   static char name[96];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pp<%s, Cfg<%d>, %s, %d>", type_name<T>(), BN, KTAIL ? "true" : "false", ACT);
+    snprintf(name, sizeof(name), "gemm_pp<%s, Cfg<%d>, %s, %d, %d, %s>", type_name<T>(), BN, KTAIL ? "true" : "false", ACT,
+             DEEP, SK ? "true" : "false");
   set_last_kernel(name);
   return check_launch("gemm_pp");
 }
 
-template <typename T, int BN>
+template <typename T, int BN, int DEEP, bool SK>
 static int launch_bn(const GemmArgs& a, hipStream_t st) {
   const bool tail = a.K % 64 != 0;
   switch (a.act) {
-    case SVK_ACT_GELU: return tail ? launch<T, BN, true, SVK_ACT_GELU>(a, st) : launch<T, BN, false, SVK_ACT_GELU>(a, st);
-    case SVK_ACT_RELU: return tail ? launch<T, BN, true, SVK_ACT_RELU>(a, st) : launch<T, BN, false, SVK_ACT_RELU>(a, st);
-    case 0: return tail ? launch<T, BN, true, 0>(a, st) : launch<T, BN, false, 0>(a, st);
+    case SVK_ACT_GELU:
+      return tail ? launch<T, BN, true, SVK_ACT_GELU, DEEP, SK>(a, st) : launch<T, BN, false, SVK_ACT_GELU, DEEP, SK>(a, st);
+    case SVK_ACT_RELU:
+      return tail ? launch<T, BN, true, SVK_ACT_RELU, DEEP, SK>(a, st) : launch<T, BN, false, SVK_ACT_RELU, DEEP, SK>(a, st);
+    case 0: return tail ? launch<T, BN, true, 0, DEEP, SK>(a, st) : launch<T, BN, false, 0, DEEP, SK>(a, st);
     default: return 1;
   }
 }
@@ -312,9 +413,9 @@ static int launch_bn(const GemmArgs& a, hipStream_t st) {
 }  // namespace pp
 
 // Dense A only (asrc 0), plain epilogue (bias / GELU / ReLU / residual), K % 8 == 0, N % 4 == 0, 16-byte
-// aligned operand rows.  bn: 256 or 320.  Returns 1 when not eligible.
+// aligned operand rows.  Returns 1 when not eligible.
 template <typename T>
-int gemm_pp_try(const GemmArgs& a, hipStream_t st, int bn) {
+int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant) {
   auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
   if (a.K % 8 || a.N % 4 || a.lda % 8 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4) || a.out_mode || a.U ||
       a.rscale || a.ksplit > 1)
@@ -322,7 +423,10 @@ int gemm_pp_try(const GemmArgs& a, hipStream_t st, int bn) {
   if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
   // 32-bit byte offsets of the DMA rows
   if ((long)a.M * a.lda * 2 + 256 >= (1L << 32) || (long)a.N * a.ldw * 2 + 256 >= (1L << 32)) return 1;
-  if (bn == 256) return pp::launch_bn<T, 256>(a, st);
+  // variant: 0 = first DMA schedule, 1 = deep DMA schedule, 2 = deep + stream-K (needs the stream's workspace)
+  if (variant == 0) return pp::launch_bn<T, 256, 0, false>(a, st);
+  if (variant == 1) return pp::launch_bn<T, 256, 1, false>(a, st);
+  if (variant == 2) return pp::launch_bn<T, 256, 1, true>(a, st);
   return 1;
 }
 

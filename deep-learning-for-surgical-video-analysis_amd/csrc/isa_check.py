@@ -6,7 +6,10 @@
    and hipcc 7.2 inserts no wait (reproduced by tools/hazard/pk_hazard.hip: 1.5 % of lanes 48-63 wrong
    under MFMA load, none without op_sel or without the load; it was the round-2 gemm_pk "stale epilogue
    element").  The library is built without packed-FP32 ops; this check proves no such instruction
-   (v_pk_add/mul/fma_f32, or v_pk_mov_b32 with op_sel) reached the code objects.
+   (v_pk_add/mul/fma_f32, or v_pk_mov_b32 with op_sel) reached the code objects.  Also rejected:
+   v_ashr_pk_u8_i32 / v_ashr_pk_i8_i32, which hipcc 7.2 emits for two shift-clamp-pack chains assuming the
+   upper 16 destination bits are zeroed; on the GPU they keep the register's old contents (augment.hip's
+   vertical pass produced OR-ed bytes until it blocked the fusion).
 2. Epilogue operand loads of gemm_pk.  They are issued from inline asm so hipcc's waitcnt pass does not
    drain the cross-tile LDS-DMA prefetch; their completion is covered by the counted vmcnt of the tile's
    last K-step.  hipcc treats the destination VGPRs as written when the asm statement ends, so any
@@ -80,6 +83,8 @@ def check_packed(funcs):
         for addr, op, ops, _ in ins:
             if re.match(r"v_pk_(add|mul|fma)_f32", op) or (op == "v_pk_mov_b32" and "op_sel" in ops):
                 bad.append(f"{f}+0x{addr:x}: {op} {ops}")
+            if re.match(r"v_ashr_pk_[iu]8_i32", op):
+                bad.append(f"{f}+0x{addr:x}: {op} {ops} (16-bit result, upper half kept by the hardware)")
     return bad
 
 

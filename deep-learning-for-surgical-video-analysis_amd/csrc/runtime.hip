@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <mutex>
 
 #include "svk_common.h"
 
@@ -39,7 +40,39 @@ static int init_knob(int i) {
 }
 int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3), init_knob(4), init_knob(5)};
 
+// Caller-owned per-stream workspaces (svk_set_stream_workspace): the stream-K GEMM's partial sums and flags.
+struct StreamWs { hipStream_t st; void* part; long bytes; int* flags; int nflags; };
+static StreamWs g_ws[16];
+static int g_nws = 0;
+static std::mutex g_ws_mu;
+
+bool stream_workspace(hipStream_t st, void** part, long* bytes, int** flags, int* nflags) {
+  std::lock_guard<std::mutex> lk(g_ws_mu);
+  for (int i = 0; i < g_nws; ++i)
+    if (g_ws[i].st == st) {
+      *part = g_ws[i].part; *bytes = g_ws[i].bytes; *flags = g_ws[i].flags; *nflags = g_ws[i].nflags;
+      return true;
+    }
+  return false;
+}
+
 }  // namespace svk
+
+extern "C" int svk_set_stream_workspace(void* stream, void* part, long part_bytes, int* flags, int nflags) {
+  if ((part && part_bytes <= 0) || (flags && nflags <= 0) || ((uintptr_t)part & 15)) {
+    svk::set_error("svk_set_stream_workspace: bad args"); return SVK_EINVAL;
+  }
+  std::lock_guard<std::mutex> lk(svk::g_ws_mu);
+  hipStream_t st = (hipStream_t)stream;
+  for (int i = 0; i < svk::g_nws; ++i)
+    if (svk::g_ws[i].st == st) {
+      svk::g_ws[i] = svk::StreamWs{st, part, part_bytes, flags, nflags};
+      return SVK_OK;
+    }
+  if (svk::g_nws == 16) { svk::set_error("svk_set_stream_workspace: too many streams"); return SVK_EUNSUPPORTED; }
+  svk::g_ws[svk::g_nws++] = svk::StreamWs{st, part, part_bytes, flags, nflags};
+  return SVK_OK;
+}
 
 extern "C" int svk_tune(const char* knob, int value) {
   for (int i = 0; i < svk::TUNE_NKNOBS; ++i)

@@ -24,6 +24,8 @@ int check_launch(const char* what);
 // Tuning knobs set through svk_tune (runtime.hip); -1 = automatic.
 enum { TUNE_PK_CFG = 0, TUNE_PK_ELDS = 1, TUNE_DW_LDS = 2, TUNE_DW_ROWS = 3, TUNE_FFN_DIAG = 4, TUNE_PK_DIAG = 5, TUNE_NKNOBS = 6 };
 extern int g_tune[TUNE_NKNOBS];
+// Caller-owned workspace registered for a stream (svk_set_stream_workspace); false when none.
+bool stream_workspace(hipStream_t st, void** part, long* bytes, int** flags, int* nflags);
 // Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
 void set_last_kernel(const char* name);
 // norm.hip: Y = LN(sum of ks f32 split-K slabs [ks][M][C] + bias), bf16 out (svk_conv2d_ln_nhwc)

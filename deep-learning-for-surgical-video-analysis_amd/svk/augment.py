@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .ops import _chk, _p, _stream
+from .ops import _chk, _p, _prof_begin, _prof_end, _stream
 from .preproc import CHOLEC80_MEAN, CHOLEC80_STD, _coeffs, _CV_CACHE, cv2_linear_table
 
 NP = 16          # int32 parameters per sample (include/svk.h)
@@ -136,8 +136,11 @@ class TrainAugment:
         if out is None:
             out = torch.empty(B, 3, C, C, device=frames.device, dtype=torch.float32)
         m, sd = (ctypes.c_float * 3)(*self.mean), (ctypes.c_float * 3)(*self.std)
+        t0 = _prof_begin()
         _lib.call("svk_train_augment", _p(frames), _p(tmp), _p(crop), _p(sums), _p(out), _p(xb), _p(xk), ksx, _p(yb),
                   _p(yk), ksy, _p(prm), B, H, W, OH, OW, C, C, ctypes.addressof(m), ctypes.addressof(sd), _stream())
+        # algorithmic bytes: the decoded frames in, the f32 tensor out (the uint8 crop round trips are extra)
+        _prof_end(t0, "train_augment", 0, B * (H * W * 3 + 3 * C * C * 4), (B, H, W))
         return out
 
     def flows(self, flow, params, out=None):
@@ -158,8 +161,10 @@ class TrainAugment:
         if out is None:
             out = torch.empty(B, 2, C, C, device=flow.device, dtype=torch.float32)
         su, sv = float(np.float32(OW / W)), float(np.float32(OH / H))
+        t0 = _prof_begin()
         _lib.call("svk_train_augment_flow", _p(flow), _p(out), _p(xo), _p(xa), _p(yo), _p(ya), _p(prm), B, H, W, C, C,
                   su, sv, _stream())
+        _prof_end(t0, "train_augment_flow", 0, B * (H * W * 8 + 2 * C * C * 4), (B, H, W))
         return out
 
     def __call__(self, frames, segmaps=None, flow=None):

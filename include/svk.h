@@ -44,6 +44,11 @@ const char* svk_last_kernel(void);
  * Initial values from SVK_PK_CFG / SVK_PK_ELDS / SVK_DW_LDS / SVK_DW_LR. */
 int svk_tune(const char* knob, int value);
 
+/* Register caller-owned scratch for launches on `stream` (the library allocates nothing): the stream-K GEMM's
+ * f32 partial sums (part, part_bytes; 256 KiB per workgroup) and its flags (nflags int32, zero on registration,
+ * left zero by every launch).  One registration per stream; a later call replaces it. */
+int svk_set_stream_workspace(void* stream, void* part, long part_bytes, int* flags, int nflags);
+
 /* C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]
  * Replaces nn.Linear (+ activation, + residual add) at: Attention q/kv/proj
  * (mix_transformer_evp.py:81-84, 112-128), Mlp fc1/fc2 (:37-40, 61-65), Block residuals

@@ -1,0 +1,80 @@
+"""Kernel census of the graph-replayed extraction step (launches per replayed step, glue
+kernels inside the graph).  Two modes:
+  run:     python tools/graph_step_census.py run [--batch 256] [--replays 6]
+           builds MiT-b2 + flow at fp16, captures the step (svk.graphs.GraphedForward), synchronises, then
+           replays it --replays times and nothing else (run it under rocprofv3 --kernel-trace).
+  analyse: python tools/graph_step_census.py analyse KERNEL_TRACE_CSV [--replays 6]
+           takes the dispatches after the last host synchronisation gap, splits them into replays at the
+           step's last kernel (mean_rows), prints launches per step, the kernels that are not svk's, and
+           the sum of in-step gaps."""
+import argparse
+import collections
+import csv
+import os
+import sys
+
+
+def run(args):
+    import torch
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(repo, "deep-learning-for-surgical-video-analysis_amd"), repo]
+    from bench import synthetic_batch
+    from models import mix_transformer_evp as mte
+    from svk.graphs import GraphedForward
+    dev = torch.device("cuda:0")
+    torch.manual_seed(0)
+    m = mte.mit_b2_evp()
+    m.svk_dtype = torch.float16
+    m = m.to(dev).eval()
+    for p in m.parameters():
+        p.requires_grad_(False)
+    x, y, fl = synthetic_batch(args.batch, dev, 1234)
+    with torch.no_grad():
+        g = GraphedForward(m, x, y, fl, return_features=True)
+        for _ in range(3):
+            g()
+        torch.cuda.synchronize()
+        import time
+        time.sleep(0.05)                       # a host gap the analyser uses as the boundary
+        for _ in range(args.replays):
+            g()
+        torch.cuda.synchronize()
+    print("replays done", flush=True)
+
+
+def analyse(args):
+    rows = list(csv.DictReader(open(args.trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # last gap > 20 ms = the sleep before the measured replays
+    cut = 0
+    for i in range(1, len(rows)):
+        if int(rows[i]["Start_Timestamp"]) - int(rows[i - 1]["End_Timestamp"]) > 20_000_000:
+            cut = i
+    tail = rows[cut:]
+    steps, cur = [], []
+    for r in tail:
+        cur.append(r)
+        if "mean_rows" in r["Kernel_Name"]:
+            steps.append(cur)
+            cur = []
+    print(f"{len(steps)} replayed steps after the host gap ({len(tail)} dispatches)")
+    for k, st in enumerate(steps):
+        s0, e1 = int(st[0]["Start_Timestamp"]), max(int(r["End_Timestamp"]) for r in st)
+        busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in st)
+        foreign = collections.Counter(r["Kernel_Name"][:90] for r in st if "svk" not in r["Kernel_Name"])
+        print(f"step {k}: {len(st)} launches, span {(e1 - s0) / 1e6:.3f} ms, sum of kernel times {busy / 1e6:.3f} ms, "
+              f"non-svk: {dict(foreign) if foreign else 'none'}")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["run", "analyse"])
+    ap.add_argument("trace", nargs="?")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--replays", type=int, default=6)
+    args = ap.parse_args()
+    (run if args.mode == "run" else analyse)(args)
+
+
+if __name__ == "__main__":
+    main()
