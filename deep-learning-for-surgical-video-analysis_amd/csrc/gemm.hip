@@ -458,8 +458,11 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
   a.vec_out = aligned16(a.C) && (a.ldc % vw == 0) && (!a.R || (aligned16(a.R) && a.ldr % vw == 0)) &&
               (!a.U || (aligned16(a.U) && a.ldu % vw == 0)) && (a.out_mode == 0 || a.uC % 8 == 0);
   const bool ext = a.rscale || a.U || a.out_mode;
+  set_pk_reject(vec ? "" : "unaligned/K%8");
   if constexpr (sizeof(T) == 2 && ASRC <= 1) {
     if (vec && gemm_pk_try<T>(a, st, ASRC) == 0) return SVK_OK;
+  } else {
+    set_pk_reject(sizeof(T) == 2 ? "asrc" : "f32");
   }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;
@@ -470,7 +473,9 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
     if (!nm[0])
       snprintf(nm, 96, "gemm_kernel<%s, %d, %d, %s, %d, %s>", type_name<T>(), BM, BN,
                vec ? "true" : "false", ASRC, ext ? "true" : "false");
-    set_last_kernel(nm);
+    static thread_local char full[160];
+    snprintf(full, sizeof(full), "%s [%s]", nm, pk_reject());
+    set_last_kernel(full);
     if (ext) {
       if (vec) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, true, ASRC, true>), grid, dim3(NTHREADS), 0, st, a);
       else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, false, ASRC, true>), grid, dim3(NTHREADS), 0, st, a);
@@ -865,6 +870,9 @@ extern "C" int svk_conv2d_wgrad_nhwc(int dtype, const void* X, int B, int H, int
   a.H = H; a.Wd = W; a.Cin = Cin; a.OH = OH; a.OW = OW; a.kw = k; a.stride = stride; a.pad = pad;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
+    if constexpr (sizeof(T) == 2) {
+      if (wgrad_pk_conv_try<T>(X, B, H, W, Cin, dY, Cout, k, stride, pad, OH, OW, dW, db, st) == 0) return SVK_OK;
+    }
     const bool va = aligned16(dY) && Cout % 8 == 0;
     const bool vb = aligned16(X) && Cin % 8 == 0;
     return launch_wgrad<T, 1>(a, va, vb, st);

@@ -45,5 +45,8 @@ template <typename T>
 int wgrad_pk_try(const void* dY, long ldy, long sa_o, long sa_i, const void* X, long ldx, long sx_o, long sx_i,
                  float* dW, long lddw, long sw_o, long sw_i, float* db, int Z, int nzi, int M, int N, int K,
                  hipStream_t st);
+template <typename T>
+int wgrad_pk_conv_try(const void* X, int B, int H, int W, int Cin, const void* dY, int Cout, int k, int stride, int pad,
+                      int OH, int OW, float* dW, float* db, hipStream_t st);
 
 }  // namespace svk

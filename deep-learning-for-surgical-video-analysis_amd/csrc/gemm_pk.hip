@@ -515,11 +515,21 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   const int force = g_tune[TUNE_PK_CFG];
   if (getenv("SVK_NO_PK")) return 1;
   auto al = [](const void* q, int b) { return ((uintptr_t)q & (b - 1)) == 0; };
-  if (a.K % 8 || a.N % 4 || a.ldw % 8 || a.ldc % 4 || (a.R && a.ldr % 4)) return 1;
-  if (a.out_mode || (a.U && (a.ldu % 4 || !al(a.U, 8))) || (asrc != 0 && (a.U || a.rscale))) return 1;
-  if (asrc == 0 && a.lda % 8) return 1;
-  if (asrc == 1 && (a.Cin % 8 || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)) return 1;
-  if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
+  // the reason a call misses this path is kept for the fallback kernel's name (profiling: svk_last_kernel)
+  auto no = [](const char* why) { set_pk_reject(why); return 1; };
+  if (a.K % 8) return no("K%8");
+  if (a.N % 4) return no("N%4");
+  if (a.ldw % 8) return no("ldw%8");
+  if (a.ldc % 4 || (a.R && a.ldr % 4)) return no("ldc/ldr%4");
+  if (a.out_mode) return no("out_mode");
+  if (a.U && (a.ldu % 4 || !al(a.U, 8))) return no("U align");
+  if (asrc != 0 && (a.U || a.rscale)) return no("conv+U/rscale");
+  if (asrc == 0 && a.lda % 8) return no("lda%8");
+  if (asrc == 1 && (a.Cin % 8 || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)) return no("conv geometry");
+  if (!al(a.A, 16)) return no("A align");
+  if (!al(a.W, 16)) return no("W align");
+  if (!al(a.C, 8) || (a.R && !al(a.R, 8))) return no("C/R align");
+  if (a.bias && !al(a.bias, 16)) return no("bias align");
   int cfg = force;
   // Measured on the MiT-b2 B = 256 shapes, all variants interleaved in one process
   // (tools/tune_bench.py, profiles/r01/tune_r01.txt):

@@ -234,17 +234,18 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   f32x4* const part = reinterpret_cast<f32x4*>(p.sk_part);
   int* const flags = p.sk_flags;
   auto store_partial = [&]() {
-    int slot = (first * 8 + wave) * NST * 64 + lane;
-    asm volatile("" : "+v"(slot));                   // opaque: the store addresses must not be hoisted out of the loop
-    // inline asm, one base address per row block and immediate offsets for its TN column blocks (1 KiB apart):
-    // compiler-visible stores made hipcc materialise all 32 addresses (and copies of the accumulators) at once
+    // uniform slab base in SGPRs (first, wave are uniform), one VGPR lane offset for every store: no VGPR address
+    // registers at all (compiler-visible stores made hipcc materialise 32 addresses and spill)
+    const char* base = reinterpret_cast<const char*>(part) + (long)(first * 8 + wave) * NST * 1024;
+    const int lo = lane * 16;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      f32x4* row = part + slot + i * TN * 64;
+      const char* row = base + i * TN * 1024;
       static_assert(TN <= 4, "immediate offsets up to 3 KiB");
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        asm volatile("global_store_dwordx4 %0, %1, off offset:%2" ::"v"(row), "v"(acc[i][j]), "n"(j * 1024) : "memory");
+        asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3" ::"v"(lo), "v"(acc[i][j]), "s"(row), "n"(j * 1024)
+                     : "memory");
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -257,7 +258,9 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
     const int tend = (tile + 1) * nk;
     for (int w2 = first + 1; w2 < G && __builtin_amdgcn_readfirstlane(w2 * units / G) < tend; ++w2) {
       int* fl = flags + w2 * 8 + wave;
-      while (__hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) __builtin_amdgcn_s_sleep(2);
+      // bounded poll (~0.3 s): a schedule bug must end the kernel with wrong numbers, never hang the GPU
+      for (int spin = 0; spin < (1 << 21) && __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin)
+        __builtin_amdgcn_s_sleep(2);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       int slot = (w2 * 8 + wave) * NST * 64 + lane;
@@ -279,6 +282,9 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   int dkt = SK ? __builtin_amdgcn_readfirstlane(ustart % nk) : 0, dbuf = 0;
   int dunit = ustart;
   bool dlive = true;
+  // the consumer's cursor starts at stream position 0 (the DMA cursor is moved ahead by the prologue below)
+  int tile = dtile, kt = dkt;
+  int kfirst = kt;                                    // K-tile the current piece of the tile started at
   auto advance = [&]() {
     dbuf ^= 1;
     if constexpr (SK) dlive = ++dunit < uend;
@@ -302,8 +308,6 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
 
   int buf = 0;
   int post = 0;                                       // intervals left in which the epilogue's stores may still fly
-  int tile = dtile, kt = dkt;
-  int kfirst = kt;                                    // K-tile the current piece of the tile started at
   int u = ustart;
   while (SK ? u < uend : tile < ntiles) {
     const bool tlast = kt == nk - 1, rlast = SK && u == uend - 1;
@@ -324,15 +328,18 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
             post = 0;
           } else if (!SK || tlast) {
             epilogue(tile);
-            post = NW;
+            post = NW + 1;
           }
           // else: the range ends with a tile's head piece — fixup + epilogue after the loop (out of the
           // pipelined body, which keeps its register allocation)
         }
       }
-      // the epilogue's NST stores are younger than the NW pieces issued before them: for NW intervals the
-      // count leaves them out as well
-      if (post > 0) {
+      // the epilogue's NST stores are younger than the NW pieces issued before them: for the NW + 1 intervals
+      // until the last of those pieces is due, the count leaves them out as well.  Past the end of the stream no
+      // piece is issued, so a count of NW would leave the last pieces in flight into their reads: drain.
+      if (!dlive) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (post > 0) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + NW) : "memory");
         --post;
       } else {
@@ -426,7 +433,9 @@ int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant) {
   // variant: 0 = first DMA schedule, 1 = deep DMA schedule, 2 = deep + stream-K (needs the stream's workspace)
   if (variant == 0) return pp::launch_bn<T, 256, 0, false>(a, st);
   if (variant == 1) return pp::launch_bn<T, 256, 1, false>(a, st);
-  if (variant == 2) return pp::launch_bn<T, 256, 1, true>(a, st);
+  // variant 2 (stream-K) is not instantiated: hipcc spills ~55-67 VGPRs of its in-loop partial-sum path, and a
+  // scratch access is a vector-memory operation the counted DMA waits do not know about (isa_check rejects it)
+  (void)variant;
   return 1;
 }
 

@@ -142,15 +142,16 @@ def check_epilogue_loads(funcs):
 
 
 def check_scratch(notes):
-    """gemm_pk kernels must not use scratch (a spill of a register an inline-asm load is still writing
-    would store garbage; the round-3 256x256 tile that spilled faulted the GPU)."""
+    """gemm_pk / gemm_pp kernels must not use scratch (a spill of a register an inline-asm load is still writing
+    would store garbage; the round-3 256x256 tile that spilled faulted the GPU; and a scratch access is a vector
+    memory operation that the hand-counted `s_waitcnt vmcnt(N)` of the LDS-DMA pipelines does not know about)."""
     bad, cur = [], None
     for line in notes.split("\n"):
         m = re.match(r"\s+\.name:\s+(\S+)", line)
         if m:
             cur = m.group(1)
         m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count):\s+(\d+)", line)
-        if m and int(m.group(2)) > 0 and cur and "gemm_pk" in cur:
+        if m and int(m.group(2)) > 0 and cur and ("gemm_pk" in cur or "gemm_pp" in cur):
             bad.append(f"{cur}: .{m.group(1)} {m.group(2)}")
     return bad
 

@@ -13,6 +13,9 @@ static thread_local char g_err[512] = "";
 static thread_local const char* g_last_kernel = "";
 
 void set_last_kernel(const char* name) { g_last_kernel = name; }
+static thread_local const char* g_pk_reject = "";
+void set_pk_reject(const char* why) { g_pk_reject = why; }
+const char* pk_reject() { return g_pk_reject; }
 
 void set_error(const char* fmt, ...) {
   va_list ap;

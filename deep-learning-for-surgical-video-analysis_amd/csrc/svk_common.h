@@ -28,6 +28,8 @@ extern int g_tune[TUNE_NKNOBS];
 bool stream_workspace(hipStream_t st, void** part, long* bytes, int** flags, int* nflags);
 // Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
 void set_last_kernel(const char* name);
+void set_pk_reject(const char* why);   // why the last GEMM call missed gemm_pk (fallback kernel names)
+const char* pk_reject();
 // norm.hip: Y = LN(sum of ks f32 split-K slabs [ks][M][C] + bias), bf16 out (svk_conv2d_ln_nhwc)
 template <typename T>
 int splitk_layernorm(const float* S, int ks, const float* bias, T* Y, int M, int C, const float* gamma,

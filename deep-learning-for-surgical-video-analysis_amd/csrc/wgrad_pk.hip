@@ -79,9 +79,10 @@ struct Args {
   float* db;
   int M, N, K, mchunk, nzi;
   long sa_o, sa_i, sx_o, sx_i, sw_o, sw_i;
+  int H, Wd, Cin, OH, OW, kw, stride, pad;   // CONV: X is the NHWC input map, row m = output pixel, k = (ky, kx, ci)
 };
 
-template <typename T, class C>
+template <typename T, class C, bool CONV>
 __global__ __launch_bounds__(256) void wgrad_pk(Args p) {
   constexpr int BN = C::BN, BK = C::BK, TM = C::TM, TN = C::TN, CPRA = BN / 8, CPRB = BK / 8;
   typedef v8_t<T> tx8;
@@ -118,7 +119,19 @@ __global__ __launch_bounds__(256) void wgrad_pk(Args p) {
       const int s = (wave * C::B_LD + i) * 64 + lane;
       const int r = s / CPRB, c = (s % CPRB) ^ swz<CPRB>(r);
       const int m = m0 + r, k = k0 + c * 8;
-      const char* src = (m < mend && k < p.K) ? X + ((long)m * p.ldx + k) * (long)sizeof(T) : zero;
+      const char* src = zero;
+      if constexpr (CONV) {
+        // im2col on the fly: 8 consecutive k = 8 channels of one tap (Cin % 8 == 0) = 16 contiguous bytes
+        if (m < mend && k < p.K) {
+          const int ohw = p.OH * p.OW, b = m / ohw, pix = m - b * ohw, oy = pix / p.OW, ox = pix - oy * p.OW;
+          const int t = k / p.Cin, ci = k - t * p.Cin, ky = t / p.kw, kx = t - ky * p.kw;
+          const int iy = oy * p.stride - p.pad + ky, ix = ox * p.stride - p.pad + kx;
+          if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.Wd)
+            src = X + ((((long)b * p.H + iy) * p.Wd + ix) * p.Cin + ci) * (long)sizeof(T);
+        }
+      } else {
+        if (m < mend && k < p.K) src = X + ((long)m * p.ldx + k) * (long)sizeof(T);
+      }
       dma16(src, __builtin_amdgcn_readfirstlane(sb + (wave * C::B_LD + i) * 1024));
     }
   };
@@ -196,7 +209,7 @@ __global__ __launch_bounds__(256) void wgrad_pk(Args p) {
   }
 }
 
-template <typename T, class C>
+template <typename T, class C, bool CONV = false>
 static int launch(Args a, int Z, hipStream_t st) {
   const long tiles = (long)((a.N + C::BN - 1) / C::BN) * ((a.K + C::BK - 1) / C::BK);
   // M split: enough workgroups to fill the chip (~4 per CU), each with >= 128 rows (4 steps), and the f32
@@ -211,9 +224,9 @@ static int launch(Args a, int Z, hipStream_t st) {
   splits = (a.M + chunk - 1) / chunk;
   a.mchunk = (int)chunk;
   if (a.nzi <= 0) a.nzi = 1;
-  hipLaunchKernelGGL((wgrad_pk<T, C>), dim3((unsigned)tiles, (unsigned)splits, (unsigned)Z), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((wgrad_pk<T, C, CONV>), dim3((unsigned)tiles, (unsigned)splits, (unsigned)Z), dim3(256), 0, st, a);
   static char name[64];
-  if (!name[0]) snprintf(name, sizeof(name), "wgrad_pk<%s, Cfg<%d, %d>>", type_name<T>(), C::BN, C::BK);
+  if (!name[0]) snprintf(name, sizeof(name), "wgrad_pk<%s, Cfg<%d, %d>%s>", type_name<T>(), C::BN, C::BK, CONV ? ", conv" : "");
   set_last_kernel(name);
   return check_launch("wgrad_pk");
 }
@@ -243,6 +256,30 @@ int wgrad_pk_try(const void* dY, long ldy, long sa_o, long sa_i, const void* X, 
   if (K <= 64) return wgpk::launch<T, wgpk::Cfg<128, 64>>(a, Z, st);
   return wgpk::launch<T, wgpk::Cfg<128, 128>>(a, Z, st);
 }
+
+// conv weight gradient (svk_conv2d_wgrad_nhwc): dW[co][(ky, kx, ci)] (+ db) over output pixels, X the NHWC map
+// (16-byte aligned, Cin % 8 == 0), dY [M, Cout] rows (Cout % 8 == 0).  Returns 1 when not eligible.
+template <typename T>
+int wgrad_pk_conv_try(const void* X, int B, int H, int W, int Cin, const void* dY, int Cout, int k, int stride, int pad,
+                      int OH, int OW, float* dW, float* db, hipStream_t st) {
+  if (getenv("SVK_NO_WGRAD_PK")) return 1;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (Cin % 8 || Cout % 8 || !al(X) || !al(dY)) return 1;
+  if ((long)B * H * W * Cin > 0x7fffffffL) return 1;
+  wgpk::Args a{};
+  a.dY = dY; a.ldy = Cout; a.X = X; a.ldx = 0; a.dW = dW; a.lddw = (long)k * k * Cin; a.db = db;
+  a.M = B * OH * OW; a.N = Cout; a.K = k * k * Cin; a.nzi = 1;
+  a.H = H; a.Wd = W; a.Cin = Cin; a.OH = OH; a.OW = OW; a.kw = k; a.stride = stride; a.pad = pad;
+  if (Cout <= 64 && a.K <= 64) return wgpk::launch<T, wgpk::Cfg<64, 64>, true>(a, 1, st);
+  if (Cout <= 64) return wgpk::launch<T, wgpk::Cfg<64, 128>, true>(a, 1, st);
+  if (a.K <= 64) return wgpk::launch<T, wgpk::Cfg<128, 64>, true>(a, 1, st);
+  return wgpk::launch<T, wgpk::Cfg<128, 128>, true>(a, 1, st);
+}
+
+template int wgrad_pk_conv_try<bf16>(const void*, int, int, int, int, const void*, int, int, int, int, int, int, float*,
+                                     float*, hipStream_t);
+template int wgrad_pk_conv_try<f16>(const void*, int, int, int, int, const void*, int, int, int, int, int, int, float*,
+                                    float*, hipStream_t);
 
 template int wgrad_pk_try<bf16>(const void*, long, long, long, const void*, long, long, long, float*, long, long, long,
                                 float*, int, int, int, int, int, hipStream_t);

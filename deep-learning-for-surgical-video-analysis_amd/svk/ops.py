@@ -72,7 +72,10 @@ def set_profiler(records):
 
 def tune(knob, value):
     """Set a kernel-selection knob (svk_tune: "pk_cfg", "pk_elds", "dw_lds", "dw_rows"; -1 = auto)."""
+    global _SK_WANTED
     _lib.call("svk_tune", knob.encode(), int(value))
+    if knob == "pk_cfg" and int(value) == 72:
+        _SK_WANTED = True
 
 
 def _last_kernel():
@@ -118,7 +121,7 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
     if (SKINNY and row_scale is None and a.dtype in H16 and N <= 64 and K <= 128 and M >= 2048
             and a.data_ptr() % 16 == 0 and (K % 8 or lda % 8 == 0)):
         return gemm_skinny(a, w, bias, act, residual, out, N, dact, dact_src)
-    if a.dtype in H16:
+    if _SK_WANTED and a.dtype in H16:
         _stream_workspace(a.device)
     t0 = _prof_begin()
     if row_scale is None and dact is None:
@@ -155,6 +158,7 @@ SKINNY = os.environ.get("SVK_SKINNY", "1") == "1"
 # from the graph's pool, kept alive here.
 SK_SLOTS = 256
 _SK_WS = {}
+_SK_WANTED = os.environ.get("SVK_PP_SK") == "1"   # registered only while a stream-K variant can be chosen
 
 
 def _stream_workspace(device):

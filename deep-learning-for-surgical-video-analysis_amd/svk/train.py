@@ -163,23 +163,27 @@ class EVPTrainStep:
                     f"cross_attn_s4, everything else frozen); parameter {n!r} has requires_grad={p.requires_grad}")
             if is_trainable(n):
                 tr.append((n, p))
-        total = sum(p.numel() for _, p in tr)
-        self.flat = torch.empty(total, device=self.dev, dtype=torch.float32)
-        self.grad = torch.zeros(total, device=self.dev, dtype=torch.float32)
-        self.mom = torch.zeros(total, device=self.dev, dtype=torch.float32)
+        # every tensor starts 16-byte aligned (offsets rounded up to 4 floats): the f32 biases are read by the
+        # GEMM epilogues with 16-byte loads, and an unaligned one sent the GEMM to the legacy kernel; the gaps
+        # stay zero (zero gradient, zero momentum, SGD keeps them at 0)
         self.off = {}
         o = 0
+        for n, p in tr:
+            self.off[n] = o
+            o += (p.numel() + 3) // 4 * 4
+        total = o
+        self.flat = torch.zeros(total, device=self.dev, dtype=torch.float32)
+        self.grad = torch.zeros(total, device=self.dev, dtype=torch.float32)
+        self.mom = torch.zeros(total, device=self.dev, dtype=torch.float32)
         with torch.no_grad():
             for n, p in tr:
-                k = p.numel()
+                o, k = self.off[n], p.numel()
                 self.flat[o:o + k].copy_(p.detach().reshape(-1))
                 p.data = self.flat[o:o + k].view_as(p)
                 if self.BIND_GRADS:
                     p.grad = self.grad[o:o + k].view_as(p)
-                self.off[n] = o
-                o += k
         self.params = dict(tr)
-        self.n_trainable = total
+        self.n_trainable = sum(p.numel() for _, p in tr)
         # the head's parameters lead the flat buffer (model construction order): its gradient bucket
         heads = [n for n, _ in tr if n.startswith("head.")]
         self.head_end = max((self.off[n] + self.params[n].numel() for n in heads), default=0)

@@ -134,6 +134,8 @@ def test_conv_wgrad_dgrad(cuda, dt, B, Cin, H, Cout, k, s):
     dwp = torch.zeros(Cout, k * k * cp, device=cuda)
     dbias = torch.zeros(Cout, device=cuda)
     ops.conv2d_wgrad(xn, dyn, k, s, k // 2, dwp, dbias)
+    if dt != torch.float32:   # the 16-bit conv weight gradient runs on wgrad_pk's im2col DMA path
+        assert ops._last_kernel().startswith("wgrad_pk") and "conv" in ops._last_kernel(), ops._last_kernel()
     dw = dwp.view(Cout, k, k, cp)[..., :Cin].permute(0, 3, 1, 2)
     tol = 1e-4 if dt == torch.float32 else 2e-2
     _close(dw, wr.grad, tol)

@@ -4,10 +4,8 @@ export TMPDIR=/tmp
 O=gpurun_out/r04c
 mkdir -p $O
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ "$rc" -eq 0 ] || exit $rc; }
-timeout -k 10 200 python -u tools/aug_debug.py > $O/aug.log 2>&1; echo augdbg rc=$?
-grep -v amdgpu.ids $O/aug.log
-timeout -k 10 200 python -u -m pytest tests/test_preproc_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_preproc.log 2>&1; echo preproc rc=$?
-tail -2 $O/pytest_preproc.log
+timeout -k 10 200 python -u -m pytest tests/test_augment_gpu.py tests/test_preproc_gpu.py -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_aug.log 2>&1; echo aug rc=$?
+tail -2 $O/pytest_aug.log
 step pptest timeout -k 10 200 python -u -m pytest tests/test_kernels_gpu.py -x -q -rf -k "pingpong" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_pp.log 2>&1
 tail -3 $O/pytest_pp.log
 step sweep timeout -k 10 300 python -u tools/pk_cfg_sweep.py --reps 30 > $O/sweep.log 2>&1

@@ -17,7 +17,7 @@ SHAPES = [  # (M, N, K, residual, what)
     (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"), (200704, 128, 128, True, "s2 q/proj"),
     (802816, 64, 64, True, "s1 q/proj"),
 ]
-CFGS = [(-1, "auto"), (60, "128x128e"), (70, "pp256"), (71, "pp256d"), (72, "pp256sk")]
+CFGS = [(-1, "auto"), (60, "128x128e"), (70, "pp256"), (71, "pp256d")]
 
 
 def timeit(fn, reps):
@@ -35,7 +35,9 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
+    ap.add_argument("--no-sk", action="store_true", help="skip the stream-K variant")
     args = ap.parse_args()
+    cfgs = [c for c in CFGS if not (args.no_sk and c[0] == 72)]
     dt, dev = torch.float16, torch.device("cuda:0")
     lib = _lib.load()
     for M, N, K, res, what in SHAPES:
@@ -46,11 +48,7 @@ def main():
         out = torch.empty(M, N, device=dev, dtype=dt)
         ref = None
         row = []
-        for cfg, name in CFGS:
-            if cfg == 40 and N % 160:
-                continue
-            if cfg == 71 and N % 320:
-                continue
+        for cfg, name in cfgs:
             lib.svk_tune(b"pk_cfg", cfg)
             y = ops.gemm(a, w, b, residual=r, out=out).clone()
             kname = ops._last_kernel()
