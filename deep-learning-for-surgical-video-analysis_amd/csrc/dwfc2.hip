@@ -1,0 +1,284 @@
+// The back half of the stage-3 / stage-4 MixFFN in one kernel (mix_transformer_evp.py:60-67 with DWConv :19-30,
+// Block residual :169), 16-bit:
+//
+//   Y[m, n] = sum_k GELU(dwconv3x3(H)[m, k]) * W2[n, k] + b2[n] + R[m, n]
+//
+// H is fc1's output [B, WI, WI, K] (hidden K = 4C), W2 [N = C, K], R the Block input.  Unfused this is
+// dwconv3x3 (+ GELU) writing the hidden map G (B*WI*WI x K 16-bit values) and fc2 reading it back; here G never
+// leaves the chip: every K-step of 64 hidden channels the workgroup builds its 64-token G tile in LDS from a
+// halo'd H tile (the tile's tokens +- one image row + 1, flattened indices, neighbours masked at the image
+// edges), then runs the fc2 MFMAs on it.
+//
+//  * workgroup = 4 waves, 64 tokens x all N output channels (so each G value is made once); wave w owns
+//    columns 80 w .. (N = 320: 5 n-blocks of 16), 4 x 5 accumulator blocks (80 f32);
+//  * G production: thread (token t, 8-channel group cg) for tokens t and t + 32: acc = bias, 9 taps in the
+//    dwconv3x3_strip order (fma over f32 taps), GELU (the same gelu_rl), rounded to 16 bits -> LDS, rows
+//    XOR-swizzled (16-byte chunk c of row r at c ^ (r & 7)) so the MFMA fragment reads are conflict-free;
+//  * software pipeline, one barrier per K-step: iteration k issues the fc2 MFMAs of K-step k (G(k), W2
+//    fragments in registers), produces G(k + 1) from the H tile already in LDS, writes the H / tap tiles of
+//    k + 2 (register-staged, loaded one iteration earlier) and loads those of k + 3 and the W2 fragments of
+//    k + 1 — the MFMA and VALU streams are independent, the scheduler interleaves them;
+//  * transposed MFMA (W2 fragment x G fragment): a lane ends with 4 consecutive output channels of a token,
+//    the epilogue adds b2 and the residual in f32 and stores 8-byte row pieces.
+// Numerics: the dwconv + GELU exactly as dwconv3x3_strip (f32 taps and accumulation, G rounded to 16 bits),
+// fc2 as the GEMM (f32 accumulation, bias then residual, one rounding).
+#include "svk_common.h"
+
+namespace svk {
+namespace dwfc {
+
+__device__ __forceinline__ float gelu_rl(float x) {   // = stencil.hip's gelu_rl (erf form, |err| <= 1.5e-7)
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752f, ax, 1.0f));
+  float q = fmaf(-0.5f * 1.061405429f, t, -0.5f * -1.453152027f);
+  q = fmaf(q, t, -0.5f * 1.421413741f);
+  q = fmaf(q, t, -0.5f * -0.284496736f);
+  q = fmaf(q, t, -0.5f * 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170f);
+  return fmaf(ax * t * q, e, fmaxf(x, 0.f));
+}
+
+static __device__ __attribute__((aligned(16))) uint4 g_zero[4];   // DMA source of halo rows outside the map
+typedef __attribute__((address_space(3))) void* las_ptr;
+
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+template <int N_, int WI_>
+struct Cfg {
+  static constexpr int N = N_, WI = WI_, BM = 64, BK = 64, NT = 256;
+  static constexpr int WNB = N / 64;                  // 16-column n-blocks per wave (4 waves split N)
+  static constexpr int HR = BM + 2 * WI + 2;          // halo rows: tokens m0 - WI - 1 .. m0 + BM + WI
+  static constexpr int HBYTES = HR * BK * 2;
+  static constexpr int HCH = HR * 8;                  // 16-byte chunks of a halo tile
+  static constexpr int HBLK = (HCH + 63) / 64;       // 1 KiB DMA blocks of a halo tile
+  static constexpr int TBYTES = 10 * BK * 4;          // taps [9][64] + dwconv bias [64], f32
+  static constexpr int TCH = TBYTES / 16;
+  static constexpr int TBLK = (TCH + 63) / 64;
+  static constexpr int GBYTES = BM * BK * 2;
+  static constexpr int HSTRIDE = HBLK * 1024, TSTRIDE = TBLK * 1024;   // buffers in whole DMA blocks
+  static constexpr int H_OFF = 0, T_OFF = 2 * HSTRIDE, G_OFF = T_OFF + 2 * TSTRIDE;
+  static constexpr int LDS = G_OFF + 2 * GBYTES;
+  static_assert(N % 64 == 0 && LDS <= 64 * 1024, "shape");
+};
+
+template <typename T, class C>
+__global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const float* __restrict__ taps,
+                                               const float* __restrict__ dbias, const T* __restrict__ W2,
+                                               const float* __restrict__ b2, const T* __restrict__ R,
+                                               T* __restrict__ Y, int M, int K) {
+  typedef v8_t<T> tx8;
+  constexpr int BM = C::BM, WI = C::WI, WNB = C::WNB;
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM;
+  const int nk = K / C::BK;
+
+  // ---- G production mapping: tokens tok and tok + 32, channels 8 cg .. 8 cg + 7 of the K-step
+  const int cg = tid & 7, tok = tid >> 3;
+  uint32_t vmask[2];                                   // bit t: tap t's neighbour is inside the image
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int m = m0 + tok + 32 * i;
+    const int pix = m % (WI * WI), y = pix / WI, x = pix - y * WI;
+    uint32_t v = 0;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int yy = y + t / 3 - 1, xx = x + t % 3 - 1;
+      if (m < M && yy >= 0 && yy < WI && xx >= 0 && xx < WI) v |= 1u << t;
+    }
+    vmask[i] = v;
+  }
+
+  // ---- halo / tap tiles of K-step kt -> buffer buf by LDS-DMA (lane-linear 1 KiB blocks; halo rows outside
+  // [0, M) and the blocks' tail chunks read the zero block: they only feed masked taps)
+  const char* zero = reinterpret_cast<const char*>(g_zero);
+  auto dma_tiles = [&](int kt, int buf) {
+    for (int blk = wave; blk < C::HBLK + C::TBLK; blk += 4) {      // wave-uniform
+      const int c = (blk < C::HBLK ? blk : blk - C::HBLK) * 64 + lane;
+      const char* src = zero;
+      uint32_t dst;
+      if (blk < C::HBLK) {
+        const int r = c >> 3, q = c & 7, gm = m0 - WI - 1 + r;
+        if (c < C::HCH && gm >= 0 && gm < M) src = reinterpret_cast<const char*>(Hm + (long)gm * K + kt * 64 + q * 8);
+        dst = lds0 + C::H_OFF + buf * C::HSTRIDE + blk * 1024;
+      } else {
+        const int t = c >> 4, j = c & 15;                           // tap row t (9: bias), 4 floats
+        if (c < C::TCH) src = reinterpret_cast<const char*>(t < 9 ? taps + (long)t * K + kt * 64 + j * 4 : dbias + kt * 64 + j * 4);
+        dst = lds0 + C::T_OFF + buf * C::TSTRIDE + (blk - C::HBLK) * 1024;
+      }
+      dma16(src, __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+
+  // ---- G(k) from the halo / tap tiles in buffer hb into G buffer gb
+  auto produce = [&](int hb, int gb) {
+    const char* hs = smem + C::H_OFF + hb * C::HSTRIDE;
+    const float* ts = reinterpret_cast<const float*>(smem + C::T_OFF + hb * C::TSTRIDE) + cg * 8;
+    // one token at a time, one tap at a time (sched barriers): hipcc otherwise hoists all 18 halo and 18 tap
+    // reads of the step ahead of the FMAs and spills
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float acc[8];
+      {
+        const float4 b0 = *reinterpret_cast<const float4*>(ts + 9 * 64), b1 = *reinterpret_cast<const float4*>(ts + 9 * 64 + 4);
+        acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
+        acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const float4 w0 = *reinterpret_cast<const float4*>(ts + t * 64), w1 = *reinterpret_cast<const float4*>(ts + t * 64 + 4);
+        const float wt[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const int dr = WI + 1 + (t / 3 - 1) * WI + (t % 3 - 1);
+        uint4 h = *reinterpret_cast<const uint4*>(hs + (tok + 32 * i + dr) * 128 + cg * 16);
+        if (!((vmask[i] >> t) & 1u)) h = uint4{0u, 0u, 0u, 0u};
+        const uint32_t hw[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f32x2 p = unpack2<T>(hw[j]);
+          acc[2 * j] = fmaf(p.x, wt[2 * j], acc[2 * j]);
+          acc[2 * j + 1] = fmaf(p.y, wt[2 * j + 1], acc[2 * j + 1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      T o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) o[c] = (T)gelu_rl(acc[c]);
+      const int row = tok + 32 * i;
+      *reinterpret_cast<uint4*>(smem + C::G_OFF + gb * C::GBYTES + row * 128 + ((cg ^ (row & 7)) << 4)) =
+          *reinterpret_cast<const uint4*>(o);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- fc2: wave's W2 fragments (n-block nb, k-step ks) and the MFMAs over the G tile in buffer gb
+  const int n0w = wave * (C::N / 4);
+  // W2 fragments one k-step (32 channels) at a time: the ks = 0 set is loaded during the previous step's G
+  // production, the ks = 1 set while the ks = 0 MFMAs run (20 registers live instead of 40)
+  tx8 w2f[WNB];
+  auto load_w2 = [&](int kt, int ks) {
+#pragma unroll
+    for (int nb = 0; nb < WNB; ++nb)
+      w2f[nb] = *reinterpret_cast<const tx8*>(W2 + (long)(n0w + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
+  };
+  f32x4 acc[4][WNB];
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](int gb, int kt) {
+    const char* gs = smem + C::G_OFF + gb * C::GBYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      if (ks == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        load_w2(kt, 1);
+      }
+#pragma unroll
+      for (int mb = 0; mb < 4; ++mb) {
+        const int row = mb * 16 + fr;
+        const tx8 g = *reinterpret_cast<const tx8*>(gs + row * 128 + (((ks * 4 + fq) ^ (row & 7)) << 4));
+#pragma unroll
+        for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = mfma16x16x32(w2f[nb], g, acc[mb][nb]);
+      }
+    }
+  };
+
+  // ---- prologue: tiles 0 and 1 in LDS, G(0), the first W2 fragments
+  dma_tiles(0, 0);
+  if (nk > 1) dma_tiles(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  produce(0, 0);
+  load_w2(0, 0);
+  __syncthreads();
+  // iteration k: fc2 MFMAs of K-step k (G buffer k & 1), DMA of tile k + 2 into buffer k & 1 (last read producing
+  // G(k), before the previous barrier), G(k + 1) from buffer (k + 1) & 1 (DMA'd and waited for one iteration ago)
+  for (int k = 0; k < nk; ++k) {
+    mma(k & 1, k);
+    // the MFMAs have read the W2 fragments: their registers take the next K-step's (one set live, not two)
+    __builtin_amdgcn_sched_barrier(0);
+    if (k + 2 < nk) dma_tiles(k + 2, k & 1);
+    if (k + 1 < nk) {
+      load_w2(k + 1, 0);
+      produce((k + 1) & 1, (k + 1) & 1);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this wave's DMA of tile k + 2 landed
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane (fr, fq) of block (mb, nb) holds Y[m0 + 16 mb + fr][n0w + 16 nb + 4 fq .. + 3]
+#pragma unroll
+  for (int mb = 0; mb < 4; ++mb) {
+    const int m = m0 + mb * 16 + fr;
+    if (m >= M) continue;
+#pragma unroll
+    for (int nb = 0; nb < WNB; ++nb) {
+      const int n = n0w + nb * 16 + fq * 4;
+      const float4 bb = *reinterpret_cast<const float4*>(b2 + n);
+      float v[4] = {acc[mb][nb][0] + bb.x, acc[mb][nb][1] + bb.y, acc[mb][nb][2] + bb.z, acc[mb][nb][3] + bb.w};
+      if (R) {
+        const uint2 r = *reinterpret_cast<const uint2*>(R + (long)m * C::N + n);
+        const f32x2 r01 = unpack2<T>(r.x), r23 = unpack2<T>(r.y);
+        v[0] += r01.x; v[1] += r01.y; v[2] += r23.x; v[3] += r23.y;
+      }
+      const T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+      *reinterpret_cast<uint2*>(Y + (long)m * C::N + n) = *reinterpret_cast<const uint2*>(o);
+    }
+  }
+}
+
+template <typename T, class C>
+static int launch(const void* H, const float* taps, const float* db, const void* W2, const float* b2, const void* R,
+                  void* Y, int M, int K, hipStream_t st) {
+  const int grid = (M + C::BM - 1) / C::BM;
+  hipLaunchKernelGGL((dw_fc2<T, C>), dim3(grid), dim3(C::NT), 0, st, (const T*)H, taps, db, (const T*)W2, b2,
+                     (const T*)R, (T*)Y, M, K);
+  static char name[64];
+  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2<%s, Cfg<%d, %d>>", type_name<T>(), C::N, C::WI);
+  set_last_kernel(name);
+  return check_launch("dw_fc2");
+}
+
+}  // namespace dwfc
+}  // namespace svk
+
+using namespace svk;
+
+extern "C" int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K) {
+  return (dtype == SVK_F16 || dtype == SVK_BF16) && W == 14 && N == 320 && K % 64 == 0 && K >= 64;
+}
+
+extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2,
+                                 const float* b2, const void* R, void* Y, int B, int Himg, int Wimg, int K, int N,
+                                 void* stream) {
+  if (B < 0 || Himg <= 0 || Wimg <= 0 || K <= 0 || N <= 0 || !H || !taps || !dbias || !W2 || !b2 || !Y) {
+    set_error("svk_mixffn_dw_fc2: bad args"); return SVK_EINVAL;
+  }
+  if (Himg != Wimg || !svk_mixffn_dw_fc2_supported(dtype, Wimg, N, K)) {
+    set_error("svk_mixffn_dw_fc2: (dtype=%d, %dx%d, N=%d, K=%d) not instantiated", dtype, Himg, Wimg, N, K);
+    return SVK_EUNSUPPORTED;
+  }
+  if ((((uintptr_t)H) | ((uintptr_t)W2) | ((uintptr_t)taps) | ((uintptr_t)dbias) | ((uintptr_t)b2)) & 15 ||
+      (((uintptr_t)Y) | ((uintptr_t)R)) & 7) {
+    set_error("svk_mixffn_dw_fc2: misaligned operand"); return SVK_EINVAL;
+  }
+  const long M = (long)B * Himg * Wimg;
+  if (M == 0) return SVK_OK;
+  if (M * K > 0x7fffffffL) { set_error("svk_mixffn_dw_fc2: too many tokens"); return SVK_EUNSUPPORTED; }
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_H16(dtype, T, {
+    return dwfc::launch<T, dwfc::Cfg<320, 14>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
+  });
+}

@@ -115,8 +115,17 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   // piece overwrites the same piece of position u - 2): B after 8u - 14 (group 1's reads of u - 2 retired),
   // A_p after 8u - 15 + 2p: DD <= 13.  DEEP = 0: DD = 9, NW = 3 (round-4 first form); DEEP = 1: DD = 13,
   // NW = 8 — each piece gets 8 intervals (~2-4k cycles) to land instead of 3.
-  constexpr int DD = DEEP ? 13 : 9, NW = DEEP ? 8 : 3;
-  constexpr int OFF = DD & 7;                               // slot s issues piece (s + OFF) % 8 ...
+  //
+  // DEEP = 2 ("paired" schedule, the 8-phase template's placement): the compute intervals issue nothing but their
+  // MFMAs; load interval 2p of position u issues TWO pieces of position u + 1 — B0 B1 | B2 B3 | A0 A1 | A2 A3 —
+  // and each wave counts its DMA twice per K-tile: at the end of slot 6, vmcnt(2) retires everything but the
+  // two pieces just issued (B and A0 A1 of u + 1: B is read by both groups from interval 8(u + 1), group 1's
+  // copy retired at the end of 8u + 7, group 0's at 8u + 6; A0 A1 by their own group from slot 0 / 2), and at
+  // the end of slot 3 of u + 1, vmcnt(4) retires A2 A3 (read from slot 4) past the four B pieces of u + 2
+  // (+ NST when the epilogue's stores sit between them).  Buffer reuse: position u + 1 overwrites u - 1, whose
+  // last reads (group 1's A3, interval 8u - 1) retired in interval 8u, the first issue's.
+  constexpr int DD = DEEP == 1 ? 13 : 9, NW = DEEP == 1 ? 8 : 3;
+  constexpr int OFF = DEEP >= 2 ? 0 : DD & 7;               // slot s issues piece (s + OFF) % 8 ...
   static_assert(DD - 3 >= NW + 2 && DD - 4 >= NW + 1 && DD <= 13, "DMA schedule");
   auto opaque = [](int v) { asm volatile("" : "+s"(v)); return v; };
   const int cq = (lane & 7) ^ ((lane >> 3) & 7);          // this lane's swizzled 16-byte chunk (rows are 8-aligned)
@@ -302,7 +311,8 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
 #pragma unroll
   for (int k = 0; k < OFF; ++k)
     if (dlive) issue(k, dkt, dbuf);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OFF) : "memory");
+  if constexpr (DEEP >= 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OFF) : "memory");
   barrier();
   if (g == 1) barrier();                              // the stagger: group 1 runs one interval behind
 
@@ -311,15 +321,34 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   int u = ustart;
   while (SK ? u < uend : tile < ntiles) {
     const bool tlast = kt == nk - 1, rlast = SK && u == uend - 1;
+    const bool live = dlive;                          // (DEEP 2) pieces of the next position are issued in this one
     // the 8 intervals of this K-tile, each a compile-time slot (a runtime slot index would put the
     // accumulators in scratch)
     auto slot = [&](auto S_) {
       constexpr int s = decltype(S_)::value, ph = s >> 1, piece = (s + OFF) & 7;
-      if (piece == 0) advance();                      // the cursor moves to the next stream position
-      if (dlive) issue(piece, dkt, dbuf);
+      constexpr bool PAIRED = DEEP >= 2, READS_FIRST = DEEP == 3;
+      auto dma = [&]() {
+        if constexpr (PAIRED) {
+          if constexpr ((s & 1) == 0) {
+            if (live) {
+              issue(s, dkt, dbuf);
+              issue(s + 1, dkt, dbuf);
+            }
+            if constexpr (s == 6) advance();          // the cursor moves on once position u + 1 is issued
+          }
+        } else {
+          if (piece == 0) advance();                  // the cursor moves to the next stream position
+          if (dlive) issue(piece, dkt, dbuf);
+        }
+      };
+      if constexpr (!READS_FIRST) dma();
       if constexpr ((s & 1) == 0) {                   // ---- load interval
         if constexpr (ph == 0) read_b(buf);
         read_a(buf, ph);
+        if constexpr (READS_FIRST) {                  // (DEEP 3) fragment reads issued ahead of the DMA pair
+          __builtin_amdgcn_sched_barrier(0);
+          dma();
+        }
       } else {                                        // ---- compute interval
         mfma_phase(ph);
         if (s == 7 && (tlast || rlast)) {
@@ -337,7 +366,17 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
       // the epilogue's NST stores are younger than the NW pieces issued before them: for the NW + 1 intervals
       // until the last of those pieces is due, the count leaves them out as well.  Past the end of the stream no
       // piece is issued, so a count of NW would leave the last pieces in flight into their reads: drain.
-      if (!dlive) {
+      if constexpr (PAIRED) {
+        if constexpr (s == 3) {
+          if (!live) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          else if (post > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + 4) : "memory");
+          else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          post = 0;
+        } else if constexpr (s == 6) {
+          if (!live) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        }
+      } else if (!dlive) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       } else if (post > 0) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST + NW) : "memory");
@@ -431,8 +470,8 @@ int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant) {
   // 32-bit byte offsets of the DMA rows
   if ((long)a.M * a.lda * 2 + 256 >= (1L << 32) || (long)a.N * a.ldw * 2 + 256 >= (1L << 32)) return 1;
   // variant: 0 = first DMA schedule, 1 = deep DMA schedule, 2 = deep + stream-K (needs the stream's workspace)
-  if (variant == 0) return pp::launch_bn<T, 256, 0, false>(a, st);
-  if (variant == 1) return pp::launch_bn<T, 256, 1, false>(a, st);
+  if (variant == 0) return pp::launch_bn<T, 256, 3, false>(a, st);
+  if (variant == 1) return pp::launch_bn<T, 256, 2, false>(a, st);
   // variant 2 (stream-K) is not instantiated: hipcc spills ~55-67 VGPRs of its in-loop partial-sum path, and a
   // scratch access is a vector-memory operation the counted DMA waits do not know about (isa_check rejects it)
   (void)variant;

@@ -101,6 +101,12 @@ class Mlp(nn.Module):
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")
             y = ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
+        elif (ops.DW_FC2 and x.dtype in ops.H16 and H == W and residual is not None
+              and ops.mixffn_dw_fc2_supported(x.dtype, W, self.fc2.out_features, hid)):
+            # fc1 GEMM, then DWConv + GELU fused into fc2 (the GELU map never leaves the chip)
+            h = ops.gemm(x, p["w1"], p["b1"])
+            pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
+            y = ops.mixffn_dw_fc2(h.view(B, H, W, hid), pd["taps"], pd["b"], p["w2"], p["b2"], residual=residual)
         else:
             h = ops.gemm(x, p["w1"], p["b1"])
             h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)

@@ -396,6 +396,41 @@ def mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=None):
 
 
 MIXFFN_RW = os.environ.get("SVK_MIXFFN_RW", "1") == "1"
+DW_FC2 = os.environ.get("SVK_DW_FC2", "1") == "1"
+
+
+def mixffn_dw_fc2_supported(dtype, W, N, K):
+    """True when svk_mixffn_dw_fc2 (dwconv3x3 + GELU fused into fc2) has an instantiation for the map."""
+    return dtype in H16 and bool(_lib.load().svk_mixffn_dw_fc2_supported(dtype_code(dtype), int(W), int(N), int(K)))
+
+
+def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None):
+    """fc2(GELU(dwconv3x3(h) + dbias)) + b2 (+ residual) with the GELU map kept on chip (svk_mixffn_dw_fc2):
+    h [B, H, W, K] fc1 output (16-bit NHWC), taps [9, K] / dbias [K] f32 as DWConv packs them, w2 [N, K];
+    returns [B, H * W, N]."""
+    if h.dtype not in H16:
+        raise _lib.SvkError("svk.mixffn_dw_fc2: bf16 / f16 only")
+    _chk(h, "h"); _chk(w2, "w2", h.dtype); _chk(residual, "residual", h.dtype)
+    for t, nm in ((taps, "taps"), (dbias, "dbias"), (b2, "b2")):
+        _chk(t, nm, torch.float32)
+    B, H, W, K = h.shape
+    N = w2.shape[0]
+    for t, nm in ((h, "h"), (w2, "w2"), (taps, "taps"), (dbias, "dbias"), (b2, "b2")):
+        if not t.is_contiguous():
+            raise _lib.SvkError(f"svk.mixffn_dw_fc2: {nm} must be contiguous")
+    if w2.shape != (N, K) or taps.shape != (9, K) or dbias.numel() != K or b2.numel() != N:
+        raise _lib.SvkError("svk.mixffn_dw_fc2: shape mismatch")
+    if residual is not None and (residual.numel() != B * H * W * N or not residual.is_contiguous()):
+        raise _lib.SvkError("svk.mixffn_dw_fc2: residual must be a contiguous [B, H*W, N] map")
+    out = torch.empty(B, H * W, N, device=h.device, dtype=h.dtype)
+    t0 = _prof_begin()
+    _lib.call("svk_mixffn_dw_fc2", dtype_code(h.dtype), _p(h), _p(taps), _p(dbias), _p(w2), _p(b2), _p(residual),
+              _p(out), B, H, W, K, N, _stream())
+    if t0 is not None:
+        M = B * H * W
+        _prof_end(t0, _last_kernel(), 2.0 * M * N * K + 2.0 * 9 * M * K,
+                  (M * K + N * K + M * N * (2 if residual is not None else 1)) * h.element_size(), (M, N, K, "dw_fc2"))
+    return out
 
 
 def mixffn_rw_supported(dtype, W, C):
@@ -959,7 +994,7 @@ def conv2d_wgrad(x, dy, k, stride, pad, dw, db=None):
     _lib.call("svk_conv2d_wgrad_nhwc", dtype_code(x.dtype), _p(x), B, H, W, Cin, _p(dy), Cout, k, stride, pad, _p(dw),
               _p(db), _stream())
     M = dy.numel() // Cout
-    _prof_end(t0, "wgrad_kernel", 2.0 * M * Cout * k * k * Cin, (x.numel() + dy.numel()) * x.element_size(),
+    _prof_end(t0, _last_kernel(), 2.0 * M * Cout * k * k * Cin, (x.numel() + dy.numel()) * x.element_size(),
               (M, Cout, k * k * Cin, f"convwgrad{k}s{stride}"))
     return dw
 

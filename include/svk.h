@@ -125,6 +125,17 @@ int svk_mixffn_rw(int dtype, const void* XN, const void* X, const void* W1, cons
                   const float* dbias, const void* W2, const float* b2, void* Y, void* Yn, const float* gamma,
                   const float* beta, float eps, int B, int H, int W, int C, void* stream);
 
+/* MixFFN back half for the stage-3 / stage-4 shapes (csrc/dwfc2.hip): Y = GELU(dwconv3x3(H) + dbias) W2^T + b2
+ * (+ R), the depthwise output never written: each 64-token tile builds its GELU map per 64-channel K-step in
+ * LDS from a halo'd H tile and runs the fc2 MFMAs on it (mix_transformer_evp.py:60-67, 24-30; replaces
+ * svk_dwconv3x3 + svk_gemm).  H [B, Himg, Wimg, K] (fc1 output, 16-bit), taps [9][K] f32 (row dy*3+dx), dbias
+ * [K] f32, W2 [N][K], b2 [N] f32, R / Y [B*Himg*Wimg][N]; H, W2, taps, dbias, b2 16-byte aligned, R / Y 8-byte.
+ * Instantiated where svk_mixffn_dw_fc2_supported(dtype, W, N, K) (stage 3 of MiT-b1..b5 at 224x224: 14 x 14,
+ * N = 320); SVK_EUNSUPPORTED otherwise. */
+int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K);
+int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2, const float* b2,
+                      const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, void* stream);
+
 /* MixFFN front half, G = act(dwconv3x3(XN W1^T + b1) + dbias) over NHWC maps (Mlp.fc1 -> DWConv -> GELU,
  * mix_transformer_evp.py:60-63, 24-30): the 4C-wide hidden map stays on chip (fc1 recomputed on one
  * halo row above / below each strip).  bf16, C in {32, 64, 128}, hidden % 64 == 0; W1 [hidden][C] bf16,

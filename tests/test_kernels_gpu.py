@@ -163,6 +163,35 @@ def test_gemm_pingpong_configs(cuda, cfg, dt, act):
         ops.tune("pk_cfg", -1)
 
 
+@pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,res", [(3, True), (1, False), (5, True)])
+def test_mixffn_dw_fc2(cuda, dt, B, res):
+    """dwconv3x3 + GELU fused into fc2 (svk_mixffn_dw_fc2, the stage-3 shape 14 x 14, hidden 1280 -> 320) against
+    the unfused svk path (dwconv3x3 + gemm: same roundings, expected within one 16-bit ulp) and fp64.  B = 1 / 5:
+    token counts that are not a multiple of the 64-token tile (the last tile's masked rows)."""
+    from svk import ops
+    K, N, W = 1280, 320, 14
+    h = _rand(B, W, W, K, dt=dt, dev=cuda, seed=71)
+    taps = _rand(9, K, dt=torch.float32, dev=cuda, scale=0.3, seed=72)
+    db = _rand(K, dt=torch.float32, dev=cuda, scale=0.1, seed=73)
+    w2 = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=74)
+    b2 = _rand(N, dt=torch.float32, dev=cuda, seed=75)
+    r = _rand(B, W * W, N, dt=dt, dev=cuda, seed=76) if res else None
+    got = ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r)
+    assert ops._last_kernel().startswith("dw_fc2"), ops._last_kernel()
+    g = ops.dwconv3x3(h, taps, db, act="gelu")
+    ref16 = ops.gemm(g.view(B, W * W, K), w2, b2, residual=r)
+    d = (got.float() - ref16.float()).abs().max().item()
+    assert d <= 4 * float(ref16.float().abs().max()) * (2 ** -8 if dt == torch.bfloat16 else 2 ** -11), d
+    hd = h.double().cpu().permute(0, 3, 1, 2)
+    cv = F.conv2d(hd, taps.double().cpu().t().reshape(K, 1, 3, 3), db.double().cpu(), padding=1, groups=K)
+    gd = F.gelu(cv).permute(0, 2, 3, 1).reshape(B, W * W, K)
+    ref = gd @ w2.double().cpu().t() + b2.double().cpu()
+    if res:
+        ref = ref + r.double().cpu()
+    _close(got, ref, dt)
+
+
 @pytest.mark.parametrize("lds,rows", [(1, 1), (1, 3), (1, 8), (2, -1)])
 def test_dwconv_lds_variant(cuda, lds, rows):
     """The LDS-tiled depthwise conv (svk_tune dw_lds = 1) at several strip heights, with the

@@ -1,0 +1,37 @@
+"""Stage-3 MixFFN back half (B = 256, 14 x 14, 1280 -> 320, f16): fused dw_fc2 vs dwconv3x3 + gemm.
+GPU box: python tools/dwfc2_bench.py"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                "deep-learning-for-surgical-video-analysis_amd"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from svk import ops  # noqa: E402
+from pk_cfg_sweep import timeit  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    for dt in (torch.float16, torch.bfloat16):
+        B, W, K, N = 256, 14, 1280, 320
+        h = torch.randn(B, W, W, K, device=dev).to(dt)
+        taps = torch.randn(9, K, device=dev) * 0.3
+        db = torch.randn(K, device=dev) * 0.1
+        w2 = (torch.randn(N, K, device=dev) * K ** -0.5).to(dt)
+        b2 = torch.randn(N, device=dev)
+        r = torch.randn(B, W * W, N, device=dev).to(dt)
+        f = lambda: ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r)
+        u = lambda: ops.gemm(ops.dwconv3x3(h, taps, db, act="gelu").view(B, W * W, K), w2, b2, residual=r)
+        d = (f().float() - u().float()).abs().max().item()
+        tf, tu = timeit(f, 20), timeit(u, 20)
+        g = ops.dwconv3x3(h, taps, db, act="gelu")
+        tdw = timeit(lambda: ops.dwconv3x3(h, taps, db, act="gelu"), 20)
+        tg = timeit(lambda: ops.gemm(g.view(B, W * W, K), w2, b2, residual=r), 20)
+        print(f"{dt}: fused {tf * 1e3:.1f} us | unfused {tu * 1e3:.1f} us (dwconv {tdw * 1e3:.1f} + fc2 {tg * 1e3:.1f}) "
+              f"| max|fused - unfused| {d:.3e}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -19,7 +19,7 @@ def main():
         w = (torch.rand(N, K, device=dev) * 2 - 1).half()
         out = torch.empty(M, N, device=dev, dtype=torch.half)
         row = []
-        for cfg, name in ((60, "128x128e"), (70, "pp256"), (71, "pp256d")):
+        for cfg, name in ((60, "128x128e"), (70, "ppRF"), (71, "ppPair")):
             ops.tune("pk_cfg", cfg)
             ops.gemm(a, w, None, out=out)
             kn = ops._last_kernel()
