@@ -10,7 +10,7 @@
 // edges), then runs the fc2 MFMAs on it.
 //
 //  * workgroup = 4 waves, 64 tokens x all N output channels (so each G value is made once); wave w owns
-//    columns 80 w .. (N = 320: 5 n-blocks of 16), 4 x 5 accumulator blocks (80 f32);
+//    columns N/4 w .. (N = 320: 5 n-blocks of 16, 80 accumulator registers; N = 512: 8 blocks, 128);
 //  * G production: thread (token t, 8-channel group cg) for tokens t and t + 32: acc = bias, 9 taps in the
 //    dwconv3x3_strip order (fma over f32 taps), GELU (the same gelu_rl), rounded to 16 bits -> LDS, rows
 //    XOR-swizzled (16-byte chunk c of row r at c ^ (r & 7)) so the MFMA fragment reads are conflict-free;
@@ -52,9 +52,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-template <int N_, int WI_>
+template <int N_, int WI_, int BM_>
 struct Cfg {
-  static constexpr int N = N_, WI = WI_, BM = 64, BK = 64, NT = 256;
+  static constexpr int N = N_, WI = WI_, BM = BM_, BK = 64, NT = 256;
+  static constexpr int MB = BM / 16, IT = BM / 32;    // m-blocks per wave, G items per thread
   static constexpr int WNB = N / 64;                  // 16-column n-blocks per wave (4 waves split N)
   static constexpr int HR = BM + 2 * WI + 2;          // halo rows: tokens m0 - WI - 1 .. m0 + BM + WI
   static constexpr int HBYTES = HR * BK * 2;
@@ -67,7 +68,7 @@ struct Cfg {
   static constexpr int HSTRIDE = HBLK * 1024, TSTRIDE = TBLK * 1024;   // buffers in whole DMA blocks
   static constexpr int H_OFF = 0, T_OFF = 2 * HSTRIDE, G_OFF = T_OFF + 2 * TSTRIDE;
   static constexpr int LDS = G_OFF + 2 * GBYTES;
-  static_assert(N % 64 == 0 && LDS <= 64 * 1024, "shape");
+  static_assert(N % 64 == 0 && LDS <= 64 * 1024 && BM % 32 == 0, "shape");
 };
 
 template <typename T, class C>
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const
                                                const float* __restrict__ b2, const T* __restrict__ R,
                                                T* __restrict__ Y, int M, int K) {
   typedef v8_t<T> tx8;
-  constexpr int BM = C::BM, WI = C::WI, WNB = C::WNB;
+  constexpr int BM = C::BM, WI = C::WI, WNB = C::WNB, MB = C::MB, IT = C::IT;
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -87,9 +88,9 @@ __global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const
 
   // ---- G production mapping: tokens tok and tok + 32, channels 8 cg .. 8 cg + 7 of the K-step
   const int cg = tid & 7, tok = tid >> 3;
-  uint32_t vmask[2];                                   // bit t: tap t's neighbour is inside the image
+  uint32_t vmask[IT];                                  // bit t: tap t's neighbour is inside the image
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < IT; ++i) {
     const int m = m0 + tok + 32 * i;
     const int pix = m % (WI * WI), y = pix / WI, x = pix - y * WI;
     uint32_t v = 0;
@@ -129,7 +130,7 @@ __global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const
     // one token at a time, one tap at a time (sched barriers): hipcc otherwise hoists all 18 halo and 18 tap
     // reads of the step ahead of the FMAs and spills
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < IT; ++i) {
       float acc[8];
       {
         const float4 b0 = *reinterpret_cast<const float4*>(ts + 9 * 64), b1 = *reinterpret_cast<const float4*>(ts + 9 * 64 + 4);
@@ -172,9 +173,9 @@ __global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const
     for (int nb = 0; nb < WNB; ++nb)
       w2f[nb] = *reinterpret_cast<const tx8*>(W2 + (long)(n0w + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
   };
-  f32x4 acc[4][WNB];
+  f32x4 acc[MB][WNB];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto mma = [&](int gb, int kt) {
@@ -186,7 +187,7 @@ __global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const
         load_w2(kt, 1);
       }
 #pragma unroll
-      for (int mb = 0; mb < 4; ++mb) {
+      for (int mb = 0; mb < MB; ++mb) {
         const int row = mb * 16 + fr;
         const tx8 g = *reinterpret_cast<const tx8*>(gs + row * 128 + (((ks * 4 + fq) ^ (row & 7)) << 4));
 #pragma unroll
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(256, 2) void dw_fc2(const T* __restrict__ Hm, const
 
   // ---- epilogue: lane (fr, fq) of block (mb, nb) holds Y[m0 + 16 mb + fr][n0w + 16 nb + 4 fq .. + 3]
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+  for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + mb * 16 + fr;
     if (m >= M) continue;
 #pragma unroll
@@ -246,7 +247,7 @@ static int launch(const void* H, const float* taps, const float* db, const void*
   hipLaunchKernelGGL((dw_fc2<T, C>), dim3(grid), dim3(C::NT), 0, st, (const T*)H, taps, db, (const T*)W2, b2,
                      (const T*)R, (T*)Y, M, K);
   static char name[64];
-  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2<%s, Cfg<%d, %d>>", type_name<T>(), C::N, C::WI);
+  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2<%s, Cfg<%d, %d, %d>>", type_name<T>(), C::N, C::WI, C::BM);
   set_last_kernel(name);
   return check_launch("dw_fc2");
 }
@@ -257,7 +258,8 @@ static int launch(const void* H, const float* taps, const float* db, const void*
 using namespace svk;
 
 extern "C" int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K) {
-  return (dtype == SVK_F16 || dtype == SVK_BF16) && W == 14 && N == 320 && K % 64 == 0 && K >= 64;
+  return (dtype == SVK_F16 || dtype == SVK_BF16) && ((W == 14 && N == 320) || (W == 7 && N == 512)) && K % 64 == 0 &&
+         K >= 64;
 }
 
 extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2,
@@ -279,6 +281,7 @@ extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, co
   if (M * K > 0x7fffffffL) { set_error("svk_mixffn_dw_fc2: too many tokens"); return SVK_EUNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
-    return dwfc::launch<T, dwfc::Cfg<320, 14>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
+    if (N == 512) return dwfc::launch<T, dwfc::Cfg<512, 7, 32>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
+    return dwfc::launch<T, dwfc::Cfg<320, 14, 64>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
   });
 }

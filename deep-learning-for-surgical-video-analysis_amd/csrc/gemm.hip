@@ -451,6 +451,57 @@ __global__ __launch_bounds__(NTHREADS) void gemm_kernel(GemmArgs p) {
 
 static bool aligned16(const void* ptr) { return ((uintptr_t)ptr & 15) == 0; }
 
+// f32 GEMMs with few rows (the train step's f32 classifier heads and their gradients: M = 88 frames,
+// K = 512 - 2048): the 64 x 64 register-staged tiles give 16 workgroups on 256 CUs (1-7 TF/s).  Here a
+// workgroup owns 16 x 16 outputs and its four waves split K (lane: one row, 4 consecutive columns, 16-byte
+// loads along k when aligned); the partial sums meet in LDS and one thread per output runs the same epilogue
+// as gemm_kernel (act(acc + bias), row scale, activation backward, residual).
+template <bool VK>
+__global__ __launch_bounds__(256) void gemm_f32_smallm(GemmArgs p) {
+  __shared__ float red[4][16][17];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tn = (p.N + 15) / 16;
+  const int m0 = (blockIdx.x / tn) * 16, n0 = (blockIdx.x % tn) * 16;
+  const int mi = lane & 15, nj = (lane >> 4) * 4;
+  const float* A = static_cast<const float*>(p.A) + (long)min(m0 + mi, p.M - 1) * p.lda;
+  const float* Wr[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) Wr[j] = static_cast<const float*>(p.W) + (long)min(n0 + nj + j, p.N - 1) * p.ldw;
+  const int chunk = ((p.K + 15) / 16) * 4;            // per wave, a multiple of 4
+  const int k0 = w * chunk, k1 = min(k0 + chunk, p.K);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  int k = k0;
+  if constexpr (VK) {
+    for (; k + 4 <= k1; k += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(A + k);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 b = *reinterpret_cast<const float4*>(Wr[j] + k);
+        acc[j] = fmaf(a.x, b.x, acc[j]);
+        acc[j] = fmaf(a.y, b.y, acc[j]);
+        acc[j] = fmaf(a.z, b.z, acc[j]);
+        acc[j] = fmaf(a.w, b.w, acc[j]);
+      }
+    }
+  }
+  for (; k < k1; ++k) {
+    const float a = A[k];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = fmaf(a, Wr[j][k], acc[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) red[w][mi][nj + j] = acc[j];
+  __syncthreads();
+  const int row = tid >> 4, col = tid & 15, m = m0 + row, n = n0 + col;
+  if (m >= p.M || n >= p.N) return;
+  float v = red[0][row][col] + red[1][row][col] + red[2][row][col] + red[3][row][col];
+  v = apply_act(v + (p.bias ? p.bias[n] : 0.f), p.act);
+  if (p.rscale) v *= p.rscale[m / p.rdiv];
+  if (p.U) v *= act_grad(static_cast<const float*>(p.U)[(long)m * p.ldu + n], p.uact);
+  if (p.R) v += static_cast<const float*>(p.R)[(long)m * p.ldr + n];
+  static_cast<float*>(p.C)[(long)m * p.ldc + n] = v;
+}
+
 template <typename T, int ASRC>
 static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
   const int M = a.M, N = a.N;
@@ -463,6 +514,18 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
     if (vec && gemm_pk_try<T>(a, st, ASRC) == 0) return SVK_OK;
   } else {
     set_pk_reject(sizeof(T) == 2 ? "asrc" : "f32");
+  }
+  if constexpr (sizeof(T) == 4 && ASRC == 0) {
+    // few rows, long K: the 64 x 64 tiles would leave most CUs idle
+    const long tiles64 = (long)((M + 63) / 64) * ((N + 63) / 64);
+    if (a.out_mode == 0 && M <= 256 && a.K >= 128 && tiles64 < 128) {
+      const bool vk = aligned16(a.A) && aligned16(a.W) && a.lda % 4 == 0 && a.ldw % 4 == 0;
+      const dim3 grid((unsigned)(((M + 15) / 16) * ((N + 15) / 16)));
+      if (vk) hipLaunchKernelGGL(gemm_f32_smallm<true>, grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL(gemm_f32_smallm<false>, grid, dim3(256), 0, st, a);
+      set_last_kernel(vk ? "gemm_f32_smallm<true>" : "gemm_f32_smallm<false>");
+      return check_launch("gemm_f32_smallm");
+    }
   }
   auto go = [&](auto bm_c, auto bn_c) {
     constexpr int BM = decltype(bm_c)::value, BN = decltype(bn_c)::value;

@@ -509,6 +509,7 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
 // plain epilogue, C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when
 // not eligible.  asrc: 0 dense A, 1 implicit-GEMM conv (A = NHWC map, GemmArgs conv geometry).
 static const int g_pk_policy = getenv("SVK_PK_POLICY") ? atoi(getenv("SVK_PK_POLICY")) : 1;   // 0: round-2 picks
+static const int g_pp_policy = getenv("SVK_PP") ? atoi(getenv("SVK_PP")) : 1;                  // 0: no gemm_pp
 
 template <typename T>
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
@@ -550,6 +551,15 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
       // register-epilogue 128 x 128 and 128 x 64 wherever N % 128 == 0 and K >= 320 (s3 kv 15.7 -> 13.7 us,
       // s4 fc1 50 -> 43, s4 kv 33 -> 29, s2 fc2 79 -> 70, head 80 -> 77, s3 fc1 91 -> 80)
       if (g_pk_policy && a.N % 128 == 0 && a.K >= 320) cfg = 60;
+      // round 4: the 256 x 256 ping-pong kernel (gemm_pp, paired DMA schedule) where its faster tile is neither
+      // short of tiles (< 192: most CUs idle, e.g. s4 fc2 / q at N = 512) nor lost to a last partial round:
+      // one round, long K, or >= 90 % full rounds (MiT-b2 B = 256: head 75.3 -> 71.7 us, s3 fc1 79.7 -> 71.9,
+      // s4 kv 27.9 -> 25.0; s4 fc1 (K = 512, 392 tiles) stays on 128 x 128, profiles/r04/pk_cfg_sweep_pp.txt)
+      if (g_pp_policy && a.N % 256 == 0 && a.M >= 8192 && a.K >= 320) {
+        const long t256 = (long)((a.M + 255) / 256) * (a.N / 256);
+        const long rounds = (t256 + 255) / 256;
+        if (t256 >= 192 && (t256 <= 256 || a.K >= 1024 || t256 * 10 >= rounds * 256 * 9)) cfg = 71;
+      }
       // (round-2 sweep: 128 x 128 for the stage-3 fc1 and 128 x 160 for its fc2 win 5-7 us each in
       // isolation but lost 2 % of the whole graph-replayed step: kept 128 x 64)
     }

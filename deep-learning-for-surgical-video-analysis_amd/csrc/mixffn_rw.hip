@@ -170,24 +170,31 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
     };
     // fc1 of hidden row yy: MFMAs issued early, packed (+ b1, f16, zero outside the image) late, so the
     // dwconv of the current row runs while they are in flight
+    // (the accumulators start from b1: the bias add rides on the MFMA)
     auto fc1_mma = [&](const f16x8 (&wf)[4][KS], const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        a[j] = *reinterpret_cast<const f32x4*>(b1l + 16 * j);
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(wf[j][ks], xf[ks], a[j]);
       }
     };
     // hidden values rounded to f16 (the autocast Linear output) and kept as f32: the depthwise taps then
     // run as full-rate v_fmac_f32 with the horizontal shift folded in as a DPP operand
+    // the zero padding of the conv: only tiles at the image's left / right edge (lanes 0 / 15 outside) and the
+    // rows above / below the image need the mask (a wave-uniform test)
+    const bool edge = x0 == 0 || x0 + 15 > W;
     auto fc1_pack = [&](int yy, const f32x4 (&a)[4], float (&hw)[4][4]) __attribute__((always_inline)) {
-      const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 bb = *reinterpret_cast<const float4*>(b1l + 16 * j);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) hw[j][c] = __uint_as_float(__float_as_uint((float)(f16)(a[j][c] + bv[c])) & m);
+        for (int c = 0; c < 4; ++c) hw[j][c] = (float)(f16)a[j][c];
+      if (edge || yy < 0 || yy >= H) {
+        const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hw[j][c] = __uint_as_float(__float_as_uint(hw[j][c]) & m);
       }
     };
     float win[3][4][4];
@@ -376,19 +383,23 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
     auto fc1_mma = [&](const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        a[j] = *reinterpret_cast<const f32x4*>(b1l + 16 * j);   // bias add on the MFMA
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(w1f[j][ks], xf[ks], a[j]);
       }
     };
+    const bool edge = x0 == 0 || x0 + 15 > W;          // (see mixffn_rw)
     auto fc1_pack = [&](int yy, const f32x4 (&a)[4], float (&hw)[4][4]) __attribute__((always_inline)) {
-      const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 bb = *reinterpret_cast<const float4*>(b1l + 16 * j);
-        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) hw[j][c] = __uint_as_float(__float_as_uint((float)(f16)(a[j][c] + bv[c])) & m);
+        for (int c = 0; c < 4; ++c) hw[j][c] = (float)(f16)a[j][c];
+      if (edge || yy < 0 || yy >= H) {
+        const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hw[j][c] = __uint_as_float(__float_as_uint(hw[j][c]) & m);
       }
     };
     auto tload = [&](int jd, float (&t)[12]) __attribute__((always_inline)) {

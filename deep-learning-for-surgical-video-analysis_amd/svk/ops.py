@@ -396,7 +396,10 @@ def mixffn_fused(xn, x, w1, b1, tpk, w2, b2, ln=None):
 
 
 MIXFFN_RW = os.environ.get("SVK_MIXFFN_RW", "1") == "1"
-DW_FC2 = os.environ.get("SVK_DW_FC2", "1") == "1"
+# off by default: bit-identical to dwconv3x3 + gemm but measured no faster (stage 3 188.8 vs 186.8 us, stage 4
+# 137.8 vs 99.6 us at B = 256, profiles/r04/dwfc2_bench.log): the per-tap LDS reads and masks of the G
+# production are latency-bound at 2 waves per SIMD
+DW_FC2 = os.environ.get("SVK_DW_FC2", "0") == "1"
 
 
 def mixffn_dw_fc2_supported(dtype, W, N, K):

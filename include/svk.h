@@ -130,8 +130,8 @@ int svk_mixffn_rw(int dtype, const void* XN, const void* X, const void* W1, cons
  * LDS from a halo'd H tile and runs the fc2 MFMAs on it (mix_transformer_evp.py:60-67, 24-30; replaces
  * svk_dwconv3x3 + svk_gemm).  H [B, Himg, Wimg, K] (fc1 output, 16-bit), taps [9][K] f32 (row dy*3+dx), dbias
  * [K] f32, W2 [N][K], b2 [N] f32, R / Y [B*Himg*Wimg][N]; H, W2, taps, dbias, b2 16-byte aligned, R / Y 8-byte.
- * Instantiated where svk_mixffn_dw_fc2_supported(dtype, W, N, K) (stage 3 of MiT-b1..b5 at 224x224: 14 x 14,
- * N = 320); SVK_EUNSUPPORTED otherwise. */
+ * Instantiated where svk_mixffn_dw_fc2_supported(dtype, W, N, K) (stages 3 / 4 of MiT-b1..b5 at 224x224:
+ * 14 x 14 with N = 320, 7 x 7 with N = 512); SVK_EUNSUPPORTED otherwise. */
 int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K);
 int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2, const float* b2,
                       const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, void* stream);

@@ -165,12 +165,12 @@ def test_gemm_pingpong_configs(cuda, cfg, dt, act):
 
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,res", [(3, True), (1, False), (5, True)])
-def test_mixffn_dw_fc2(cuda, dt, B, res):
-    """dwconv3x3 + GELU fused into fc2 (svk_mixffn_dw_fc2, the stage-3 shape 14 x 14, hidden 1280 -> 320) against
-    the unfused svk path (dwconv3x3 + gemm: same roundings, expected within one 16-bit ulp) and fp64.  B = 1 / 5:
-    token counts that are not a multiple of the 64-token tile (the last tile's masked rows)."""
+@pytest.mark.parametrize("W,K,N", [(14, 1280, 320), (7, 2048, 512)])
+def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N):
+    """dwconv3x3 + GELU fused into fc2 (svk_mixffn_dw_fc2; the stage-3 / stage-4 shapes 14 x 14, 1280 -> 320 and
+    7 x 7, 2048 -> 512) against the unfused svk path (dwconv3x3 + gemm: same roundings, expected within a few
+    16-bit ulps) and fp64.  Token counts that are not a multiple of the 64 / 32-token tile (masked rows)."""
     from svk import ops
-    K, N, W = 1280, 320, 14
     h = _rand(B, W, W, K, dt=dt, dev=cuda, seed=71)
     taps = _rand(9, K, dt=torch.float32, dev=cuda, scale=0.3, seed=72)
     db = _rand(K, dt=torch.float32, dev=cuda, scale=0.1, seed=73)

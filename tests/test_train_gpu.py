@@ -311,6 +311,29 @@ def test_gemm_activation_backward_epilogue(cuda, dt, act):
     _close(out, ur.grad, 1e-5 if dt == torch.float32 else 2e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(88, 512, 2048), (88, 2048, 512), (88, 7, 512), (37, 19, 130)])
+@pytest.mark.parametrize("mode", ["relu_bias", "residual", "dact_scale"])
+def test_gemm_f32_smallm(cuda, M, N, K, mode):
+    """The few-row f32 GEMM (the train step's f32 heads: 16 x 16 tiles, K split over 4 waves) with each
+    epilogue the head uses, against fp64."""
+    from svk import ops
+    a, w = _rand(M, K, seed=11), _rand(N, K, seed=12, scale=K ** -0.5)
+    b, r, u = _rand(N, seed=13), _rand(M, N, seed=14), _rand(M, N, seed=15)
+    s = torch.rand(M, generator=torch.Generator().manual_seed(16))
+    ref = a.double() @ w.double().t()
+    if mode == "relu_bias":
+        out = ops.gemm(a.to(cuda), w.to(cuda), b.to(cuda), act="relu")
+        ref = torch.relu(ref + b.double())
+    elif mode == "residual":
+        out = ops.gemm(a.to(cuda), w.to(cuda), residual=r.to(cuda))
+        ref = ref + r.double()
+    else:
+        out = ops.gemm(a.to(cuda), w.to(cuda), row_scale=s.to(cuda), rows_per=1, dact="relu", dact_src=u.to(cuda))
+        ref = ref * s.double()[:, None] * (u.double() > 0)
+    assert ops._last_kernel().startswith("gemm_f32_smallm"), ops._last_kernel()
+    _close(out, ref, 1e-5)
+
+
 @pytest.mark.parametrize("M,N,K", [(5000, 16, 16), (3001, 64, 16), (3000, 16, 64), (2048, 32, 128),
                                    (2100, 48, 40), (2500, 10, 12), (4096, 64, 128)])
 @pytest.mark.parametrize("mode", ["plain", "gelu_bias", "residual", "dact"])

@@ -14,8 +14,9 @@ from pk_cfg_sweep import timeit  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    for dt in (torch.float16, torch.bfloat16):
-        B, W, K, N = 256, 14, 1280, 320
+    for dt, (W, K, N) in ((torch.float16, (14, 1280, 320)), (torch.bfloat16, (14, 1280, 320)),
+                          (torch.float16, (7, 2048, 512))):
+        B = 256
         h = torch.randn(B, W, W, K, device=dev).to(dt)
         taps = torch.randn(9, K, device=dev) * 0.3
         db = torch.randn(K, device=dev) * 0.1
@@ -29,7 +30,7 @@ def main():
         g = ops.dwconv3x3(h, taps, db, act="gelu")
         tdw = timeit(lambda: ops.dwconv3x3(h, taps, db, act="gelu"), 20)
         tg = timeit(lambda: ops.gemm(g.view(B, W * W, K), w2, b2, residual=r), 20)
-        print(f"{dt}: fused {tf * 1e3:.1f} us | unfused {tu * 1e3:.1f} us (dwconv {tdw * 1e3:.1f} + fc2 {tg * 1e3:.1f}) "
+        print(f"{dt} {W}x{W} {K}->{N}: fused {tf * 1e3:.1f} us | unfused {tu * 1e3:.1f} us (dwconv {tdw * 1e3:.1f} + fc2 {tg * 1e3:.1f}) "
               f"| max|fused - unfused| {d:.3e}", flush=True)
 
 
