@@ -509,7 +509,10 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
 // plain epilogue, C / R rows 8-byte aligned with N % 4 == 0, bias 16-byte aligned.  Returns 1 when
 // not eligible.  asrc: 0 dense A, 1 implicit-GEMM conv (A = NHWC map, GemmArgs conv geometry).
 static const int g_pk_policy = getenv("SVK_PK_POLICY") ? atoi(getenv("SVK_PK_POLICY")) : 1;   // 0: round-2 picks
-static const int g_pp_policy = getenv("SVK_PP") ? atoi(getenv("SVK_PP")) : 1;                  // 0: no gemm_pp
+// gemm_pp by policy: off by default — faster in isolation on its shapes, but the graph-replayed extraction step
+// ran 8.60 ms with it vs 8.42 ms without (same box, profiles/r04/bench_pp_ab.txt): one 128 KiB-LDS workgroup per
+// CU for the whole persistent launch leaves no room for the side stream's kernels to co-run
+static const int g_pp_policy = getenv("SVK_PP") ? atoi(getenv("SVK_PP")) : 0;
 
 template <typename T>
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {

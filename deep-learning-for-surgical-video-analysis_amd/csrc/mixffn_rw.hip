@@ -40,9 +40,10 @@
 namespace svk {
 namespace ffnrw {
 
-template <int C_, int W_, int R_, int OCC_ = 2>
+template <int C_, int W_, int R_, int OCC_ = 2, bool BI_ = true>
 struct Cfg {
   static constexpr int C = C_, W = W_, R = R_, OCC = OCC_;
+  static constexpr bool BIAS_INIT = BI_;   // fc1's bias as the MFMA accumulator's initial value (else added after)
   static constexpr int HID = 4 * C, NW = HID / 64, NT = 64 * NW;
   static constexpr int KS = C / 32;                 // fc1 k-steps
   static constexpr int NC2 = C / 16;                // fc2 output n-tiles
@@ -112,6 +113,7 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      float eps, int H, int nstrip, int total) {
   constexpr int C = K::C, W = K::W, R = K::R, HID = K::HID, KS = K::KS, NC2 = K::NC2, NW = K::NW;
+  constexpr bool BIAS_INIT = K::BIAS_INIT;
   extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
   char* const smem = reinterpret_cast<char*>(smem4);
   float* const slab0 = reinterpret_cast<float*>(smem + K::LDS_T);
@@ -174,7 +176,7 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
     auto fc1_mma = [&](const f16x8 (&wf)[4][KS], const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = *reinterpret_cast<const f32x4*>(b1l + 16 * j);
+        a[j] = BIAS_INIT ? *reinterpret_cast<const f32x4*>(b1l + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(wf[j][ks], xf[ks], a[j]);
       }
@@ -186,9 +188,12 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
     const bool edge = x0 == 0 || x0 + 15 > W;
     auto fc1_pack = [&](int yy, const f32x4 (&a)[4], float (&hw)[4][4]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j) {
+        const float4 bb = BIAS_INIT ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4*>(b1l + 16 * j);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) hw[j][c] = (float)(f16)a[j][c];
+        for (int c = 0; c < 4; ++c) hw[j][c] = (float)(f16)(BIAS_INIT ? a[j][c] : a[j][c] + bv[c]);
+      }
       if (edge || yy < 0 || yy >= H) {
         const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
 #pragma unroll
@@ -330,9 +335,10 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
 // walks only units of its own hidden block).  No cross-wave reduction, no per-row barrier.  Per row and
 // wave: 4 KS fc1 MFMAs (hidden row y + 2, X loaded a row ahead), the 3x3 taps as DPP-fused v_fmac (taps
 // streamed from LDS one step ahead), GELU, 8-byte f16 stores of the 4 x 4 channels of the lane's token.
-template <int C_, int W_, int R_>
+template <int C_, int W_, int R_, bool BI_ = true>
 struct DwCfg {
   static constexpr int C = C_, W = W_, R = R_;
+  static constexpr bool BIAS_INIT = BI_;
   static constexpr int KS = C / 32, XT = (W + 13) / 14, NT = 256;
   static constexpr int TBLK = 160;                  // tap block (wave, n-tile, fq): taps [9][4], dwb [4] (f32)
   static constexpr int LDS_TP = 256 * 4;            // b1 of the workgroup's 256 channels | tap blocks
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
     auto fc1_mma = [&](const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        a[j] = *reinterpret_cast<const f32x4*>(b1l + 16 * j);   // bias add on the MFMA
+        a[j] = K::BIAS_INIT ? *reinterpret_cast<const f32x4*>(b1l + 16 * j) : f32x4{0.f, 0.f, 0.f, 0.f};   // bias on the MFMA
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(w1f[j][ks], xf[ks], a[j]);
       }
@@ -391,9 +397,12 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
     const bool edge = x0 == 0 || x0 + 15 > W;          // (see mixffn_rw)
     auto fc1_pack = [&](int yy, const f32x4 (&a)[4], float (&hw)[4][4]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 4; ++j) {
+        const float4 bb = K::BIAS_INIT ? float4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const float4*>(b1l + 16 * j);
+        const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) hw[j][c] = (float)(f16)a[j][c];
+        for (int c = 0; c < 4; ++c) hw[j][c] = (float)(f16)(K::BIAS_INIT ? a[j][c] : a[j][c] + bv[c]);
+      }
       if (edge || yy < 0 || yy >= H) {
         const uint32_t m = (xok && yy >= 0 && yy < H) ? ~0u : 0u;
 #pragma unroll
@@ -490,9 +499,21 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
 }  // namespace ffnrw
 
 // svk_mixffn_fc1_dwconv's f16 GELU path for the instantiated shapes; 1 = not eligible
+template <class K>
+static int fc1dw_rw_launch(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
+                           const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act, hipStream_t st);
+
 int fc1dw_rw_try(int dtype, const void* XN, const void* W1, const float* b1, const float* taps, const float* dbias,
                  void* G, int B, int H, int W, int C, int hidden, int act, hipStream_t st) {
-  using K = ffnrw::DwCfg<128, 28, 28>;
+  static const int var = getenv("SVK_RW_VAR") ? atoi(getenv("SVK_RW_VAR")) : 0;   // 2: bias added after the MFMAs
+  if (var == 2)
+    return fc1dw_rw_launch<ffnrw::DwCfg<128, 28, 28, false>>(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, st);
+  return fc1dw_rw_launch<ffnrw::DwCfg<128, 28, 28>>(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, st);
+}
+
+template <class K>
+static int fc1dw_rw_launch(int dtype, const void* XN, const void* W1, const float* b1, const float* taps,
+                           const float* dbias, void* G, int B, int H, int W, int C, int hidden, int act, hipStream_t st) {
   if (dtype != SVK_F16 || act != SVK_ACT_GELU || W != K::W || C != K::C || hidden % 256 || B <= 0 ||
       ((((uintptr_t)b1) | ((uintptr_t)dbias) | ((uintptr_t)taps)) & 15) || getenv("SVK_NO_FC1DW_RW"))
     return 1;
@@ -541,5 +562,6 @@ extern "C" int svk_mixffn_rw(int dtype, const void* XN, const void* X, const voi
   hipStream_t st = (hipStream_t)stream;
   // strips of 28 rows (two per 56-row frame): measured 335 us vs 341 (14 rows), 342 (8 rows) at B = 256
   if (var == 1) return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  if (var == 2) return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2, false>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
   return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
 }

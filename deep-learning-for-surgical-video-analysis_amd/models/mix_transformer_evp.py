@@ -248,6 +248,13 @@ class OverlapPatchEmbed(nn.Module):
         if not ops.stem_s2d_ok(dt, x.shape[1], k, self.stride) or x.shape[1] != self.proj.weight.shape[1]:
             return self.embed_nhwc(to_nhwc(x, dt))
         p = get_packed(self, dt, self._pack)
+        C = self.proj.weight.shape[0]
+        OH, OW = (x.shape[2] + 2 * (k // 2) - k) // self.stride + 1, (x.shape[3] + 2 * (k // 2) - k) // self.stride + 1
+        if ops.conv2d_s2d_ln_supported(dt, p["w_s2d"].shape[1] // 4, C, OW):
+            # s2d packing, then conv + bias + LayerNorm in one kernel
+            xs = ops.nchw_to_s2d(x if x.dtype == torch.float32 else x.float(), dt, self.stride, k // 2, OH + 1, OW + 1)
+            y = ops.conv2d_s2d_ln(xs, p["w_s2d"], p["b"], p["g"], p["beta"], self.norm.eps)
+            return y.view(y.shape[0], OH * OW, C), OH, OW
         y = ops.conv2d_stem_s2d(x, p["w_s2d"], k, self.stride, k // 2, bias=p["b"])
         return self._tokens(y, p)
 
@@ -258,6 +265,10 @@ class OverlapPatchEmbed(nn.Module):
         """xs: the input already as space-to-depth blocks [B, OH + 1, OW + 1, 16 * Cin] (e.g. the Gaussian
         filter's s2d output) -> (tokens, OH, OW)."""
         p = get_packed(self, xs.dtype, self._pack)
+        C = self.proj.weight.shape[0]
+        if ops.conv2d_s2d_ln_supported(xs.dtype, xs.shape[-1], C, xs.shape[2] - 1):
+            y = ops.conv2d_s2d_ln(xs.contiguous(), p["w_s2d"], p["b"], p["g"], p["beta"], self.norm.eps)
+            return y.view(y.shape[0], -1, C), y.shape[1], y.shape[2]
         return self._tokens(ops.conv2d_nhwc(xs, p["w_s2d"], 2, 1, 0, bias=p["b"]), p)
 
     def _tokens(self, y, p):

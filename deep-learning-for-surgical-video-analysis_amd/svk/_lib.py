@@ -70,6 +70,7 @@ SIGNATURES = {
     "svk_mixffn_fused": [c_int, P, P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P],
     "svk_mixffn_rw": [c_int, P, P, P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P],
     "svk_mixffn_dw_fc2": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_conv2d_s2d_ln": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
     # training step
     "svk_dwconv3x3_ex": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
@@ -111,7 +112,8 @@ LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int,
               "svk_mamba_scan_ragged_workspace": [c_int, c_int, c_int],
               "svk_mstcn_bwd_workspace": [c_int, c_int]}
 INT_QUERIES = {"svk_mixffn_supported": [c_int, c_int], "svk_mixffn_rw_supported": [c_int, c_int, c_int],
-               "svk_mixffn_dw_fc2_supported": [c_int, c_int, c_int, c_int], "svk_mstcn_tile_size": []}
+               "svk_mixffn_dw_fc2_supported": [c_int, c_int, c_int, c_int],
+               "svk_conv2d_s2d_ln_supported": [c_int, c_int, c_int, c_int], "svk_mstcn_tile_size": []}
 
 _lib = None
 

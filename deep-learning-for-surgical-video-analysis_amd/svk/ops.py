@@ -577,6 +577,35 @@ def conv2d_stem_s2d(x, w_s2d, k, stride, pad, bias=None, act=None):
     return conv2d_nhwc(xs, w_s2d, 2, 1, 0, bias=bias, act=act)
 
 
+STEM_LN = os.environ.get("SVK_STEM_LN", "1") == "1"
+
+
+def conv2d_s2d_ln_supported(dtype, cs, cout, ow):
+    """True when svk_conv2d_s2d_ln (stage-1 patch embedding over s2d blocks + LayerNorm in one kernel) covers it."""
+    return (STEM_LN and dtype in H16
+            and bool(_lib.load().svk_conv2d_s2d_ln_supported(dtype_code(dtype), int(cs), int(cout), int(ow))))
+
+
+def conv2d_s2d_ln(xs, w_s2d, bias, gamma=None, beta=None, eps=1e-6):
+    """xs [B, HB, WB, CS] space-to-depth blocks -> LN(conv2x2(xs) + bias) [B, HB-1, WB-1, Cout] (no LN when gamma
+    is None); w_s2d [Cout, 4*CS] as svk.pack.conv_w_s2d packs it (svk_conv2d_s2d_ln)."""
+    _chk(xs, "xs"); _chk(w_s2d, "w", xs.dtype); _chk(bias, "bias", torch.float32)
+    _chk(gamma, "gamma", torch.float32); _chk(beta, "beta", torch.float32)
+    B, HB, WB, CS = xs.shape
+    Cout = w_s2d.shape[0]
+    if not xs.is_contiguous() or not w_s2d.is_contiguous() or w_s2d.shape[1] != 4 * CS:
+        raise _lib.SvkError("svk.conv2d_s2d_ln: layout mismatch")
+    out = torch.empty(B, HB - 1, WB - 1, Cout, device=xs.device, dtype=xs.dtype)
+    t0 = _prof_begin()
+    _lib.call("svk_conv2d_s2d_ln", dtype_code(xs.dtype), _p(xs), B, HB, WB, CS, _p(w_s2d), _p(bias), _p(gamma),
+              _p(beta), float(eps), _p(out), Cout, _stream())
+    if t0 is not None:
+        M = B * (HB - 1) * (WB - 1)
+        _prof_end(t0, _last_kernel(), 2.0 * M * Cout * 4 * CS, (xs.numel() + M * Cout) * xs.element_size(),
+                  (M, Cout, 4 * CS, "stem_s2d_ln"))
+    return out
+
+
 def gauss5x5_reflect(x, dtype, cpad=None):
     _chk(x, "x", torch.float32)
     x = x.contiguous()

@@ -125,6 +125,15 @@ int svk_mixffn_rw(int dtype, const void* XN, const void* X, const void* W1, cons
                   const float* dbias, const void* W2, const float* b2, void* Y, void* Yn, const float* gamma,
                   const float* beta, float eps, int B, int H, int W, int C, void* stream);
 
+/* Stage-1 patch embedding over space-to-depth blocks + its LayerNorm (csrc/stem.hip; OverlapPatchEmbed,
+ * mix_transformer_evp.py:174-215): Y = LN(conv2x2(Xs, W) + bias) with Xs [B, HB, WB, CS] the s2d map
+ * (svk_nchw_to_s2d / svk_gauss5x5_s2d), W [Cout][2][2][CS] (svk.pack.conv_w_s2d), gamma / beta [Cout] f32
+ * (gamma = nullptr: no LayerNorm), Y [B, HB-1, WB-1, Cout].  Instantiated where
+ * svk_conv2d_s2d_ln_supported(dtype, CS, Cout, OW) (16-bit, CS in {32, 48}, Cout = 64, OW <= 64). */
+int svk_conv2d_s2d_ln_supported(int dtype, int CS, int Cout, int OW);
+int svk_conv2d_s2d_ln(int dtype, const void* Xs, int B, int HB, int WB, int CS, const void* W, const float* bias,
+                      const float* gamma, const float* beta, float eps, void* Y, int Cout, void* stream);
+
 /* MixFFN back half for the stage-3 / stage-4 shapes (csrc/dwfc2.hip): Y = GELU(dwconv3x3(H) + dbias) W2^T + b2
  * (+ R), the depthwise output never written: each 64-token tile builds its GELU map per 64-channel K-step in
  * LDS from a halo'd H tile and runs the fc2 MFMAs on it (mix_transformer_evp.py:60-67, 24-30; replaces

@@ -164,6 +164,34 @@ def test_gemm_pingpong_configs(cuda, cfg, dt, act):
 
 
 @pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,HB,CS,ln", [(3, 57, 48, True), (2, 57, 32, True), (1, 20, 48, False), (5, 57, 48, True)])
+def test_conv2d_s2d_ln(cuda, dt, B, HB, CS, ln):
+    """The stage-1 patch embedding over s2d blocks + LayerNorm in one kernel (svk_conv2d_s2d_ln) against the
+    unfused svk path (conv2d_nhwc, then layernorm: same conv rounding, LN statistics summed in another order)
+    and fp64."""
+    from svk import ops
+    C = 64
+    xs = _rand(B, HB, HB, CS, dt=dt, dev=cuda, seed=81)
+    w = _rand(C, 4 * CS, dt=dt, dev=cuda, scale=(4 * CS) ** -0.5, seed=82)
+    b = _rand(C, dt=torch.float32, dev=cuda, seed=83)
+    g = (1 + 0.1 * _rand(C, dt=torch.float32, dev=cuda, seed=84)) if ln else None
+    bt = 0.1 * _rand(C, dt=torch.float32, dev=cuda, seed=85) if ln else None
+    got = ops.conv2d_s2d_ln(xs, w, b, g, bt, 1e-6)
+    assert ops._last_kernel().startswith("stem_s2d_ln"), ops._last_kernel()
+    y = ops.conv2d_nhwc(xs, w, 2, 1, 0, bias=b)
+    ref16 = ops.layernorm(y.view(-1, C), g, bt, 1e-6).view_as(y) if ln else y
+    ulp = 2 ** -8 if dt == torch.bfloat16 else 2 ** -11
+    d = (got.float() - ref16.float()).abs().max().item()
+    assert d <= 4 * ulp * max(1.0, float(ref16.float().abs().max())), d
+    xd = xs.double().cpu().permute(0, 3, 1, 2)
+    wd = w.double().cpu().view(C, 2, 2, CS).permute(0, 3, 1, 2)
+    yd = F.conv2d(xd, wd, b.double().cpu()).permute(0, 2, 3, 1)
+    if ln:
+        yd = F.layer_norm(yd, (C,), g.double().cpu(), bt.double().cpu(), 1e-6)
+    _close(got, yd, dt)
+
+
+@pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,res", [(3, True), (1, False), (5, True)])
 @pytest.mark.parametrize("W,K,N", [(14, 1280, 320), (7, 2048, 512)])
 def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N):
