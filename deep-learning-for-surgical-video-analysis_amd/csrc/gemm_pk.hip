@@ -548,6 +548,9 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     if (asrc == 1) {
       const long t128 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64);
       cfg = (t128 < 512 && a.N <= 128) ? 30 : (a.N % 128 == 0 ? 20 : 10);
+      // round 4 (profiles/r04/conv_bench.log, B = 256): 128 x 128 now wins the long-K convs with N % 128 == 0 —
+      // stage-2 patch embed 67.3 -> 57.9 us, stage-4 patch embed 72.7 -> 64.5 us
+      if (g_pk_policy && cfg == 20 && a.K >= 512) cfg = 0;
     } else {
       cfg = (big || (a.N % 128 == 0 && a.M < 32768)) ? 0 : 10;
       // round 3 (profiles/r03/pk_cfg_sweep_elds.txt): 128 x 128 with the LDS-staged epilogue beats both the
