@@ -519,7 +519,9 @@ static int launch_gemm(GemmArgs a, bool vec, hipStream_t st) {
     // few rows, long K: the 64 x 64 tiles would leave most CUs idle
     const long tiles64 = (long)((M + 63) / 64) * ((N + 63) / 64);
     static const bool smallm_on = !getenv("SVK_NO_F32_SMALLM");
-    if (smallm_on && a.out_mode == 0 && M <= 256 && a.K >= 128 && tiles64 < 128) {
+    // (N >= 256: the classifier heads; narrower few-row GEMMs — e.g. a short video's MS-TCN input layer — keep
+    // gemm_kernel's summation order, so a video's rows come out the same alone and in a ragged batch)
+    if (smallm_on && a.out_mode == 0 && M <= 256 && a.N >= 256 && a.K >= 128 && tiles64 < 128) {
       const bool vk = aligned16(a.A) && aligned16(a.W) && a.lda % 4 == 0 && a.ldw % 4 == 0;
       const dim3 grid((unsigned)(((M + 15) / 16) * ((N + 15) / 16)));
       if (vk) hipLaunchKernelGGL(gemm_f32_smallm<true>, grid, dim3(256), 0, st, a);

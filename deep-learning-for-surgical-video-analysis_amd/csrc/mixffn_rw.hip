@@ -36,6 +36,7 @@
 // Numerics as mixffn.hip: fc1 output, taps and GELU output rounded to f16 (the reference's autocast
 // stores), accumulation / bias / GELU / LayerNorm statistics in f32.
 #include "svk_common.h"
+#include <type_traits>
 
 namespace svk {
 namespace ffnrw {
@@ -276,7 +277,10 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
     // dwconv + GELU + fc2 MFMAs of row y; the last row's reduction drains after the loop.
     f32x4 a2[NC2];
     uint2 res_prev = {0u, 0u};
-    for (int r = 0; r < R; ++r) {
+    // one row; the 3-row window rotates through the slots instead of being copied: at row r the rows y - 1, y,
+    // y + 1 sit in slots (ROT + 0, 1, 2) % 3 with ROT = r % 3, and the new row y + 2 replaces slot ROT
+    auto row = [&](int r, auto ROT_) __attribute__((always_inline)) {
+      constexpr int ROT = decltype(ROT_)::value;
       const int y = y0 + r;
       // this row's residual (its epilogue runs one row later), then the fc1 MFMAs of hidden row y + 2
       // and the X row of hidden row y + 3, a row ahead of its use
@@ -303,7 +307,7 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
         for (int dy = 0; dy < 3; ++dy) {
           const int jd = 3 * j + dy;
           if (jd + 1 < 12) tload(jd + 1, tq[(jd + 1) & 1]);
-          taps3(acc, win[dy][j], tq[jd & 1]);
+          taps3(acc, win[(ROT + dy) % 3][j], tq[jd & 1]);
         }
 #pragma unroll
         for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)gelu_rw(acc[c]);
@@ -314,15 +318,17 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
         a2[c] = mfma16x16x32(w2f[0][c], g[0], f32x4{0.f, 0.f, 0.f, 0.f});
         a2[c] = mfma16x16x32(w2f[1][c], g[1], a2[c]);
       }
-      // window roll: rows y, y + 1, and the new row y + 2 (its fc1 MFMAs have long retired)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) { win[0][j][c] = win[1][j][c]; win[1][j][c] = win[2][j][c]; }
-      fc1_pack(y + 2, a1, win[2]);
+      fc1_pack(y + 2, a1, win[ROT]);   // the new row y + 2 (its fc1 MFMAs have long retired)
       res_prev = res;
       buf ^= 1;
+    };
+    for (int r = 0; r + 3 <= R; r += 3) {
+      row(r, std::integral_constant<int, 0>{});
+      row(r + 1, std::integral_constant<int, 1>{});
+      row(r + 2, std::integral_constant<int, 2>{});
     }
+    if constexpr (R % 3 >= 1) row(R - R % 3, std::integral_constant<int, 0>{});
+    if constexpr (R % 3 == 2) row(R - 1, std::integral_constant<int, 1>{});
     slab_sync(a2, buf ^ 1);
     epilogue(y0 + R - 1, res_prev, buf ^ 1);
   }
@@ -435,7 +441,9 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
     }
     f16x8 xn[KS];
     load_x(y0 + 2, xn);
-    for (int r = 0; r < R; ++r) {
+    // (the window rotates through its slots as in mixffn_rw)
+    auto row = [&](int r, auto ROT_) __attribute__((always_inline)) {
+      constexpr int ROT = decltype(ROT_)::value;
       const int y = y0 + r;
       f32x4 a1[4];
       fc1_mma(xn, a1);
@@ -453,18 +461,21 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
         for (int dy = 0; dy < 3; ++dy) {
           const int jd = 3 * j + dy;
           if (jd + 1 < 12) tload(jd + 1, tq[(jd + 1) & 1]);
-          taps3(acc, win[dy][j], tq[jd & 1]);
+          taps3(acc, win[(ROT + dy) % 3][j], tq[jd & 1]);
         }
         if (st)
           *reinterpret_cast<f16x4*>(gy + 16 * j) =
               f16x4{(f16)gelu_rw(acc[0]), (f16)gelu_rw(acc[1]), (f16)gelu_rw(acc[2]), (f16)gelu_rw(acc[3])};
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) { win[0][j][c] = win[1][j][c]; win[1][j][c] = win[2][j][c]; }
-      fc1_pack(y + 2, a1, win[2]);
+      fc1_pack(y + 2, a1, win[ROT]);
+    };
+    for (int r = 0; r + 3 <= R; r += 3) {
+      row(r, std::integral_constant<int, 0>{});
+      row(r + 1, std::integral_constant<int, 1>{});
+      row(r + 2, std::integral_constant<int, 2>{});
     }
+    if constexpr (R % 3 >= 1) row(R - R % 3, std::integral_constant<int, 0>{});
+    if constexpr (R % 3 == 2) row(R - 1, std::integral_constant<int, 1>{});
   }
 }
 

@@ -262,7 +262,7 @@ int wgrad_pk_try(const void* dY, long ldy, long sa_o, long sa_i, const void* X, 
 template <typename T>
 int wgrad_pk_conv_try(const void* X, int B, int H, int W, int Cin, const void* dY, int Cout, int k, int stride, int pad,
                       int OH, int OW, float* dW, float* db, hipStream_t st) {
-  if (getenv("SVK_NO_WGRAD_PK")) return 1;
+  if (getenv("SVK_NO_WGRAD_PK") || getenv("SVK_NO_WGRAD_PK_CONV")) return 1;
   auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
   if (Cin % 8 || Cout % 8 || !al(X) || !al(dY)) return 1;
   if ((long)B * H * W * Cin > 0x7fffffffL) return 1;

@@ -168,9 +168,10 @@ class EVPTrainStep:
         # stay zero (zero gradient, zero momentum, SGD keeps them at 0)
         self.off = {}
         o = 0
+        align = 4 if os.environ.get("SVK_FLAT_ALIGN", "1") == "1" else 1
         for n, p in tr:
             self.off[n] = o
-            o += (p.numel() + 3) // 4 * 4
+            o += (p.numel() + align - 1) // align * align
         total = o
         self.flat = torch.zeros(total, device=self.dev, dtype=torch.float32)
         self.grad = torch.zeros(total, device=self.dev, dtype=torch.float32)

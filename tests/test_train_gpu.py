@@ -311,7 +311,7 @@ def test_gemm_activation_backward_epilogue(cuda, dt, act):
     _close(out, ur.grad, 1e-5 if dt == torch.float32 else 2e-2)
 
 
-@pytest.mark.parametrize("M,N,K", [(88, 512, 2048), (88, 2048, 512), (88, 7, 512), (37, 19, 130)])
+@pytest.mark.parametrize("M,N,K", [(88, 512, 2048), (88, 2048, 512), (256, 512, 2048), (37, 259, 130)])
 @pytest.mark.parametrize("mode", ["relu_bias", "residual", "dact_scale"])
 def test_gemm_f32_smallm(cuda, M, N, K, mode):
     """The few-row f32 GEMM (the train step's f32 heads: 16 x 16 tiles, K split over 4 waves) with each
