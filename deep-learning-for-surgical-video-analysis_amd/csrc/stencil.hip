@@ -59,13 +59,25 @@ __device__ __forceinline__ float gelu_rl(float x) {
 }
 __device__ __forceinline__ f32x2 gelu_fast2(f32x2 x) { return f32x2{gelu_rl(x.x), gelu_rl(x.y)}; }
 
+// Physical block b runs on XCD b % 8 (observed dispatch order, MI355X_MICROARCH.md: speed only, no
+// correctness depends on it).  Returns the logical block so that XCD k walks logical blocks
+// [start_k, start_k + count_k) — a bijection on [0, n) for any n.
+__device__ __forceinline__ long xcd_group(unsigned b, unsigned n) {
+  const unsigned per = n >> 3, rem = n & 7, x = b & 7, slot = b >> 3;
+  return x < rem ? (long)x * (per + 1) + slot : (long)rem * (per + 1) + (long)(x - rem) * per + slot;
+}
+
 template <typename T, int R>
 __global__ __launch_bounds__(256) void dwconv3x3_strip(const T* __restrict__ X, const float* __restrict__ w,
                                                        const float* __restrict__ bias, T* __restrict__ Y,
                                                        T* __restrict__ Ypre, int B, int H, int W, int C, int act,
-                                                       int nstrip) {
+                                                       int nstrip, int xcd) {
   const int CG = C >> 3;
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  // xcd: blocks are dealt round-robin over the 8 XCDs; regroup them so each XCD walks one contiguous
+  // range of (image, strip, column) — a column's left / right neighbours and the strip halos then come
+  // from the same L2 instead of being fetched again by up to three XCDs
+  const long blk = xcd ? xcd_group(blockIdx.x, gridDim.x) : (long)blockIdx.x;
+  const long idx = blk * blockDim.x + threadIdx.x;
   const long total = (long)B * nstrip * W * CG;
   if (idx >= total) return;
   const int cg = (int)(idx % CG);
@@ -808,8 +820,9 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
       constexpr int R = sizeof(T) == 2 ? 7 : 2;   // 16-bit: 56 / 28 / 14 / 7-row maps in whole strips
       const int nstrip = (H + R - 1) / R;
       const long n = (long)B * nstrip * W * (C / 8);
+      static const int xcd = getenv("SVK_DW_XCD") ? atoi(getenv("SVK_DW_XCD")) : 1;
       hipLaunchKernelGGL((dwconv3x3_strip<T, R>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B,
-                         H, W, C, act, nstrip);
+                         H, W, C, act, nstrip, xcd);
     } else {
       const long n = (long)B * H * W * C;
       hipLaunchKernelGGL((dwconv3x3_scalar<T>), grid1d(n), dim3(256), 0, st, (const T*)X, w, bias, (T*)Y, (T*)Ypre, B,

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 closing GPU session: full GPU suite -> smoke -> extraction profiles + PMC + bench line with the
-# CPU baseline (tools/gpu_prof.sh, R=r03) -> train-step rocprofv3 stats, FETCH/WRITE passes and bench line
-# with its CPU baseline.  Everything lands in gpurun_out/profiles_r03.  A failing step ends the session.
+# CPU baseline (tools/gpu_prof.sh, R=r04) -> train-step rocprofv3 stats, FETCH/WRITE passes and bench line
+# with its CPU baseline.  Everything lands in gpurun_out/profiles_r04.  A failing step ends the session.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out

@@ -64,6 +64,13 @@ def analyse(args):
         foreign = collections.Counter(r["Kernel_Name"][:90] for r in st if "svk" not in r["Kernel_Name"])
         print(f"step {k}: {len(st)} launches, span {(e1 - s0) / 1e6:.3f} ms, sum of kernel times {busy / 1e6:.3f} ms, "
               f"non-svk: {dict(foreign) if foreign else 'none'}")
+    if args.seq and steps:   # the last step's launch sequence: start offset, duration (us), queue, kernel
+        st = steps[-1]
+        s0 = int(st[0]["Start_Timestamp"])
+        with open(args.seq, "w") as f:
+            for r in st:
+                t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+                f.write(f"{(t0 - s0) / 1e3:8.1f} {(t1 - t0) / 1e3:7.1f} q{r['Queue_Id']} {r['Kernel_Name'][:90]}\n")
 
 
 def main():
@@ -72,6 +79,7 @@ def main():
     ap.add_argument("trace", nargs="?")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--replays", type=int, default=6)
+    ap.add_argument("--seq", default="", help="analyse: write the last step's launch sequence here")
     args = ap.parse_args()
     (run if args.mode == "run" else analyse)(args)
 

@@ -17,7 +17,7 @@ SHAPES = [  # (M, N, K, residual, what)
     (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"), (200704, 128, 128, True, "s2 q/proj"),
     (802816, 64, 64, True, "s1 q/proj"),
 ]
-CFGS = [(-1, "auto"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair")]
+CFGS = [(-1, "auto"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair"), (80, "lib")]
 
 
 def timeit(fn, reps):
@@ -36,8 +36,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--no-sk", action="store_true", help="skip the stream-K variant")
+    ap.add_argument("--cfgs", default="", help="comma-separated pk_cfg values to run (default: all)")
     args = ap.parse_args()
     cfgs = [c for c in CFGS if not (args.no_sk and c[0] == 72)]
+    if args.cfgs:
+        want = [int(v) for v in args.cfgs.split(",")]
+        cfgs = [c for c in CFGS if c[0] in want]
     dt, dev = torch.float16, torch.device("cuda:0")
     lib = _lib.load()
     for M, N, K, res, what in SHAPES:
@@ -57,7 +61,8 @@ def main():
             err = float((y.float() - ref.float()).abs().max())
             ms = timeit(lambda: ops.gemm(a, w, b, residual=r, out=out), args.reps)
             row.append(f"{name} {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF d={err:.1e}"
-                       + ("" if cfg < 70 or kname.startswith("gemm_pp") else " (fallback)"))
+                       + ("" if cfg < 70 or kname.startswith("gemm_pp") or (cfg == 80 and kname == "hipblaslt")
+                             else " (fallback)"))
         lib.svk_tune(b"pk_cfg", -1)
         ms = timeit(lambda: torch.matmul(a, w.t(), out=out), args.reps)   # hipBLASLt, no epilogue (yardstick)
         row.append(f"torch {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF")
