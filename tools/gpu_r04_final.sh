@@ -8,7 +8,7 @@ O=gpurun_out
 R=r04
 mkdir -p $O/profiles_$R
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ "$rc" -eq 0 ] || exit $rc; }
-step precheck timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "conv2d_s2d_ln or mixffn_rw or fc1dw or pingpong" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_precheck.log 2>&1
+step precheck timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "conv2d_s2d_ln or mixffn_rw or fc1dw or pingpong or library_backend" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_precheck.log 2>&1
 tail -1 $O/pytest_precheck.log
 step pytest timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 tail -1 $O/pytest_gpu.log
@@ -16,12 +16,12 @@ cp $O/pytest_gpu.log $O/profiles_$R/pytest_gpu_final.log
 step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 tail -1 $O/smoke.log
 R=$R bash tools/gpu_prof.sh || exit $?
-B="python bench.py --no-cpu-baseline"
+B="python bench.py --no-cpu-baseline --no-other-workloads"
 step prof_t timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_t -o run -- $B --workload train --no-graph --steps 5 --warmup 2 > $O/prof_t.log 2>&1
 python tools/prof_stats.py $O/prof_t/run_kernel_stats.csv auto:sgd_kernel 45 > $O/profiles_$R/rocprof_train_stats.txt
 head -1 $O/profiles_$R/rocprof_train_stats.txt
-step pmc_tf timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_tf -o run -- $B --workload train --no-graph --steps 2 --warmup 1 > $O/pmc_tf.log 2>&1
-step pmc_tw timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_tw -o run -- $B --workload train --no-graph --steps 2 --warmup 1 > $O/pmc_tw.log 2>&1
+step pmc_tf timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc_tf -o run -- $B --workload train --no-graph --steps 1 --warmup 1 > $O/pmc_tf.log 2>&1
+step pmc_tw timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc_tw -o run -- $B --workload train --no-graph --steps 1 --warmup 1 > $O/pmc_tw.log 2>&1
 cp $O/profiles_$R/pmc_traffic.json $O/pmc_traffic.json
 python tools/pmc_traffic.py $O/pmc_tf/run_counter_collection.csv $O/pmc_tw/run_counter_collection.csv $O/pmc_traffic.json train | head -5
 cp $O/pmc_traffic.json $O/profiles_$R/pmc_traffic.json
