@@ -446,9 +446,23 @@ def test_train_step_grads_fp32_vs_oracle(cuda, variant):
     for n in names:
         a, b = tr.params[n].grad.detach().double().cpu(), grads[n]
         scale = max(b.abs().max().item(), 1e-3 * gmax)
-        err = (a - b).abs().max().item()
+        diff = (a - b).abs()
+        err = diff.max().item()
         if err > 2e-3 * scale:
-            bad.append(f"{n}: err {err:.3e} scale {scale:.3e}")
+            at = np.unravel_index(int(diff.argmax()), tuple(diff.shape))
+            nbad = int((diff > 2e-3 * scale).sum())
+            bad.append(f"{n}: err {err:.3e} scale {scale:.3e} at {tuple(int(i) for i in at)} "
+                       f"(got {a[at].item():.4e} want {b[at].item():.4e}; {nbad} of {diff.numel()} over)")
+    if bad:
+        # diagnostics for an intermittent full-suite failure: is the GPU step or the oracle the side that moved?
+        g1 = {n: tr.params[n].grad.detach().double().cpu().clone() for n in names}
+        tr.forward_backward(x.to(cuda), y.to(cuda), fl.to(cuda), lab.to(cuda), at.to(cuda), masks=masks)
+        torch.cuda.synchronize()
+        gpu_self = max((tr.params[n].grad.detach().double().cpu() - g1[n]).abs().max().item() for n in names)
+        _, _, grads2, _ = TR.loss_and_grads(x, y, fl, lab, at, sd, variant, masks)
+        oracle_self = max((grads2[n] - grads[n]).abs().max().item() for n in names)
+        bad.append(f"GPU rerun self-diff {gpu_self:.3e}, oracle rerun self-diff {oracle_self:.3e}, "
+                   f"torch threads {torch.get_num_threads()}, default dtype {torch.get_default_dtype()}")
     assert not bad, "\n".join(bad)
     for prefix, (mean, var) in stats.items():
         bn = m.get_submodule(prefix)
