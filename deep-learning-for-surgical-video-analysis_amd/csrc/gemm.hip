@@ -805,7 +805,8 @@ static int conv_ln_ksplit(int dtype, long M, int N, int K, int Cin) {
   // at N = 320 (490 128 x 64 tiles) the extra slab pass costs more than the occupancy gains
   if ((dtype != SVK_BF16 && dtype != SVK_F16) || K % 64 || Cin % 8 || N % 4 || N > 128) return 1;
   const int nk = K / 64;
-  const long tiles = ((M + 63) / 64) * ((N + 63) / 64);
+  const int bm = splitk_bm();
+  const long tiles = ((M + bm - 1) / bm) * ((N + 63) / 64);
   int ks = 1;
   while (tiles * ks < 768 && nk % (2 * ks) == 0 && nk / (2 * ks) >= 4) ks *= 2;
   return ks;

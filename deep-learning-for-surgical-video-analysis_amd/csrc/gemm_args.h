@@ -1,6 +1,7 @@
 // Argument block of the GEMM / implicit-GEMM conv kernels (gemm.hip, gemm_pk.hip).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 namespace svk {
 
@@ -35,6 +36,12 @@ struct GemmArgs {
 // T = __bf16 or _Float16 (instantiated in gemm_pk.hip).
 template <typename T> int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc);
 template <typename T> int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st);
+// Row-tile height of the split-K patchify convs for N <= 128 (SVK_SPLITK_BM = 64 / 128): each unit reads its W
+// slice once per row tile, so at N = 64 a 64-row tile moves as many W bytes (from L2) as A bytes (from HBM)
+inline int splitk_bm() {
+  static const int bm = getenv("SVK_SPLITK_BM") ? atoi(getenv("SVK_SPLITK_BM")) : 64;
+  return bm == 128 ? 128 : 64;
+}
 // gemm_pp.hip: 256 x 256 ping-pong persistent GEMM, dense A, plain epilogue; variant 0 / 1 = first / deep DMA
 // schedule, 2 = deep + stream-K; returns 1 when not eligible.
 template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant);

@@ -634,7 +634,7 @@ int gemm_pk_conv_splitk(const GemmArgs& a, hipStream_t st) {
   if (a.ksplit < 2 || !a.slab || a.K % 64 || ((a.K / 64) % a.ksplit) || a.N % 4 || a.Cin % 8 || !al(a.A, 16) ||
       !al(a.W, 16) || !al(a.slab, 16) || (long)a.H * a.Wd * a.Cin * (a.M / (a.OH * a.OW)) > 0x7fffffffL)
     return 1;
-  if (a.N <= 128) return launch_pk<T, PkCfg<64, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
+  if (a.N <= 128 && splitk_bm() == 64) return launch_pk<T, PkCfg<64, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
   return launch_pk<T, PkCfg<128, 64, 2, 2, 2>, false, false, 1, false, true>(a, st);
 }
 
