@@ -30,13 +30,13 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
 
-template <int CS_>
+template <int CS_, int COUT_ = 64>
 struct Cfg {
-  static constexpr int CS = CS_, COUT = 64, ROWS = 4, MAXW = 64;
+  static constexpr int CS = CS_, COUT = COUT_, NB = COUT_ / 16, ROWS = 4, MAXW = 64;   // NB: 16-channel n-blocks
   static constexpr int KS = 4 * CS / 32;                       // 32-wide k-steps (CS = 32: 4, CS = 48: 6)
   static constexpr int CPT = CS / 8;                           // 16-byte chunks per tap
   static constexpr int LDS = ((ROWS + 1) * (MAXW + 1) * CS * 2 + 1023) / 1024 * 1024;
-  static_assert(CS % 16 == 0, "channels");
+  static_assert(CS % 16 == 0 && COUT % 16 == 0 && NB >= 1 && NB <= 4, "channels");
 };
 
 template <typename T, class C>
@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_ln(const T* __restrict__ Xs, 
                                                     const float* __restrict__ beta, float eps, T* __restrict__ Y, int B,
                                                     int OH, int OW) {
   typedef v8_t<T> tx8;
-  constexpr int CS = C::CS, KS = C::KS, CPT = C::CPT, ROWS = C::ROWS;
+  constexpr int CS = C::CS, KS = C::KS, CPT = C::CPT, ROWS = C::ROWS, NB = C::NB;
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -53,15 +53,15 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_ln(const T* __restrict__ Xs, 
   const int fr = lane & 15, fq = lane >> 4;
   const int WB = OW + 1, HB = OH + 1;
 
-  // W fragments (4 n-blocks x KS k-steps), resident: lane (fr, fq) holds W[16 nb + fr][32 ks + 8 fq .. + 7]
-  tx8 wf[4][KS];
+  // W fragments (NB n-blocks x KS k-steps), resident: lane (fr, fq) holds W[16 nb + fr][32 ks + 8 fq .. + 7]
+  tx8 wf[NB][KS];
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
+  for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) wf[nb][ks] = *reinterpret_cast<const tx8*>(W + (long)(nb * 16 + fr) * 4 * CS + ks * 32 + fq * 8);
-  float bs[4][4], gm[4][4], bt[4][4];
+  float bs[NB][4], gm[NB][4], bt[NB][4];
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
+  for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int n = nb * 16 + fq * 4 + c;
@@ -94,11 +94,11 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_ln(const T* __restrict__ Xs, 
     __syncthreads();
     const int oy = oy0 + wave;
     if (oy < OH) {                                               // wave-uniform
-      f32x4 acc[4][4];
+      f32x4 acc[4][NB];
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
       const T* rowp = reinterpret_cast<const T*>(smem) + (long)wave * WB * CS;
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
@@ -107,48 +107,48 @@ __global__ __launch_bounds__(256, 2) void stem_s2d_ln(const T* __restrict__ Xs, 
         for (int ks = 0; ks < KS; ++ks) {
           const tx8 a = *reinterpret_cast<const tx8*>(rowp + px * CS + aoff[ks]);
 #pragma unroll
-          for (int nb = 0; nb < 4; ++nb) acc[mb][nb] = mfma16x16x32(wf[nb][ks], a, acc[mb][nb]);
+          for (int nb = 0; nb < NB; ++nb) acc[mb][nb] = mfma16x16x32(wf[nb][ks], a, acc[mb][nb]);
         }
       }
       // epilogue per pixel slot: lane (fr, fq) of block (mb, nb) holds channels 16 nb + 4 fq .. + 3 of pixel 16 mb + fr
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) {
         const int px = mb * 16 + fr;
-        float v[4][4], s = 0.f;
+        float v[NB][4], s = 0.f;
 #pragma unroll
-        for (int nb = 0; nb < 4; ++nb)
+        for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             v[nb][c] = (float)(T)(acc[mb][nb][c] + bs[nb][c]);   // the conv output as the unfused path stores it
             s += v[nb][c];
           }
-        T o[4][4];
+        T o[NB][4];
         if (gamma) {
           s += __shfl_xor(s, 16, 64);
           s += __shfl_xor(s, 32, 64);
           const float mean = s / C::COUT;
           float q = 0.f;
 #pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int c = 0; c < 4; ++c) { const float d = v[nb][c] - mean; q += d * d; }
           q += __shfl_xor(q, 16, 64);
           q += __shfl_xor(q, 32, 64);
           const float rstd = 1.0f / sqrtf(q / C::COUT + eps);
 #pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int c = 0; c < 4; ++c) o[nb][c] = (T)((v[nb][c] - mean) * rstd * gm[nb][c] + bt[nb][c]);
         } else {
 #pragma unroll
-          for (int nb = 0; nb < 4; ++nb)
+          for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
             for (int c = 0; c < 4; ++c) o[nb][c] = (T)v[nb][c];
         }
         if (px < OW) {
           T* dst = Y + (((long)b * OH + oy) * OW + px) * C::COUT + fq * 4;
 #pragma unroll
-          for (int nb = 0; nb < 4; ++nb) *reinterpret_cast<uint2*>(dst + nb * 16) = *reinterpret_cast<const uint2*>(o[nb]);
+          for (int nb = 0; nb < NB; ++nb) *reinterpret_cast<uint2*>(dst + nb * 16) = *reinterpret_cast<const uint2*>(o[nb]);
         }
       }
     }
@@ -171,7 +171,7 @@ static int launch(const void* Xs, const void* W, const float* bias, const float*
   hipLaunchKernelGGL((stem_s2d_ln<T, C>), dim3(grid), dim3(256), 0, st, (const T*)Xs, (const T*)W, bias, gamma, beta, eps,
                      (T*)Y, B, OH, OW);
   static char name[64];
-  if (!name[0]) snprintf(name, sizeof(name), "stem_s2d_ln<%s, Cfg<%d>>", type_name<T>(), C::CS);
+  if (!name[0]) snprintf(name, sizeof(name), "stem_s2d_ln<%s, Cfg<%d, %d>>", type_name<T>(), C::CS, C::COUT);
   set_last_kernel(name);
   return check_launch("stem_s2d_ln");
 }
@@ -182,7 +182,8 @@ static int launch(const void* Xs, const void* W, const float* bias, const float*
 using namespace svk;
 
 extern "C" int svk_conv2d_s2d_ln_supported(int dtype, int CS, int Cout, int OW) {
-  return (dtype == SVK_F16 || dtype == SVK_BF16) && (CS == 32 || CS == 48) && Cout == 64 && OW >= 1 && OW <= 64;
+  return (dtype == SVK_F16 || dtype == SVK_BF16) && (CS == 32 || CS == 48) && (Cout == 64 || Cout == 16) && OW >= 1 &&
+         OW <= 64;
 }
 
 extern "C" int svk_conv2d_s2d_ln(int dtype, const void* Xs, int B, int HB, int WB, int CS, const void* W, const float* bias,
@@ -201,6 +202,11 @@ extern "C" int svk_conv2d_s2d_ln(int dtype, const void* Xs, int B, int HB, int W
   if ((long)B * HB * WB * CS > 0x7fffffffL) { set_error("svk_conv2d_s2d_ln: map too large"); return SVK_EUNSUPPORTED; }
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
+    // Cout 16: the handcrafted prompt generator's first stem (embed_dim / scale_factor = 64 / 4 channels)
+    if (Cout == 16) {
+      if (CS == 32) return stem::launch<T, stem::Cfg<32, 16>>(Xs, W, bias, gamma, beta, eps, Y, B, HB - 1, WB - 1, st);
+      return stem::launch<T, stem::Cfg<48, 16>>(Xs, W, bias, gamma, beta, eps, Y, B, HB - 1, WB - 1, st);
+    }
     if (CS == 32) return stem::launch<T, stem::Cfg<32>>(Xs, W, bias, gamma, beta, eps, Y, B, HB - 1, WB - 1, st);
     return stem::launch<T, stem::Cfg<48>>(Xs, W, bias, gamma, beta, eps, Y, B, HB - 1, WB - 1, st);
   });

@@ -962,19 +962,40 @@ __global__ __launch_bounds__(256) void gauss5x5_s2d_kernel(const float* __restri
 // The same filter, one 64-lane workgroup per block row: the 8 reflect-mapped input rows of every channel
 // are staged in LDS with float4 loads (W % 4 == 0), then each lane filters one block from LDS — the
 // per-lane 8-column windows of the direct kernel cost 192 scalar loads per block.  Same arithmetic.
-template <typename T>
+__device__ __forceinline__ void dma16_lds(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+
+template <typename T, bool DMA>
 __global__ __launch_bounds__(64) void gauss5x5_s2d_lds_kernel(const float* __restrict__ X, T* __restrict__ Y, int C,
                                                               int H, int W, int pad, int NBH, int NBW) {
-  extern __shared__ __attribute__((aligned(16))) float srow[];      // [C][8][W]
+  extern __shared__ __attribute__((aligned(1024))) float srow[];    // [C][8][W] (+ pad to a 1 KiB multiple)
   const int by = blockIdx.x % NBH;
   const long b = blockIdx.x / NBH;
   const int py0 = 4 * by - pad;
   const int W4 = W >> 2;
-  for (int e = threadIdx.x; e < C * 8 * W4; e += 64) {
-    const int c = e / (8 * W4), r = (e / W4) % 8, x4 = e % W4;
-    const int yy = min(max(reflect(min(max(py0 - 2 + r, -2), H + 1), H), 0), H - 1);
-    reinterpret_cast<float4*>(srow)[(c * 8 + r) * W4 + x4] =
-        reinterpret_cast<const float4*>(X + (((long)b * C + c) * H + yy) * W)[x4];
+  if (DMA) {
+    // the 8 reflect-mapped rows x C channels as 16-byte chunks straight into LDS (global_load_lds_dwordx4: lane-
+    // linear 1 KiB per instruction), every chunk in flight before one wait — the register-staged loop below
+    // waited out one load round trip per iteration (21 per workgroup at 224 x 224)
+    const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void*)srow;
+    const int total = C * 8 * W4;
+    for (int e0 = 0; e0 < total; e0 += 64) {
+      const int e = min(e0 + (int)threadIdx.x, total - 1);   // tail lanes re-copy the last chunk into the LDS pad
+      const int c = e / (8 * W4), r = (e / W4) % 8, x4 = e % W4;
+      const int yy = min(max(reflect(min(max(py0 - 2 + r, -2), H + 1), H), 0), H - 1);
+      dma16_lds(X + (((long)b * C + c) * H + yy) * W + 4 * x4, __builtin_amdgcn_readfirstlane(lds0 + e0 * 16));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    for (int e = threadIdx.x; e < C * 8 * W4; e += 64) {
+      const int c = e / (8 * W4), r = (e / W4) % 8, x4 = e % W4;
+      const int yy = min(max(reflect(min(max(py0 - 2 + r, -2), H + 1), H), 0), H - 1);
+      reinterpret_cast<float4*>(srow)[(c * 8 + r) * W4 + x4] =
+          reinterpret_cast<const float4*>(X + (((long)b * C + c) * H + yy) * W)[x4];
+    }
   }
   __syncthreads();
   const int bx = threadIdx.x;
@@ -1031,12 +1052,17 @@ extern "C" int svk_gauss5x5_s2d(int dtype_out, const float* X, void* Y, int B, i
   }
   if (B == 0) return SVK_OK;
   const long nblk = (long)B * NBH * NBW;
-  const size_t lds = (size_t)C * 8 * W * sizeof(float);
+  const size_t lds = ((size_t)C * 8 * W * sizeof(float) + 1023) / 1024 * 1024;
+  static const bool dma = getenv("SVK_GAUSS_DMA") ? atoi(getenv("SVK_GAUSS_DMA")) != 0 : true;
   SVK_DISPATCH_H16(dtype_out, T, {
     if (g_s2d_pack_vec && W % 4 == 0 && NBW <= 64 && ((uintptr_t)X & 15) == 0 && lds <= 65536 &&
         (long)B * NBH < 0x7fffffffL) {
-      hipLaunchKernelGGL((gauss5x5_s2d_lds_kernel<T>), dim3((unsigned)(B * NBH)), dim3(64), lds, (hipStream_t)stream, X,
-                         (T*)Y, C, H, W, pad, NBH, NBW);
+      if (dma)
+        hipLaunchKernelGGL((gauss5x5_s2d_lds_kernel<T, true>), dim3((unsigned)(B * NBH)), dim3(64), lds,
+                           (hipStream_t)stream, X, (T*)Y, C, H, W, pad, NBH, NBW);
+      else
+        hipLaunchKernelGGL((gauss5x5_s2d_lds_kernel<T, false>), dim3((unsigned)(B * NBH)), dim3(64), lds,
+                           (hipStream_t)stream, X, (T*)Y, C, H, W, pad, NBH, NBW);
       return check_launch("gauss5x5_s2d_lds");
     }
     hipLaunchKernelGGL((gauss5x5_s2d_kernel<T>), grid1d(nblk), dim3(256), 0, (hipStream_t)stream, X, (T*)Y, C, H, W, pad,

@@ -382,13 +382,15 @@ class PromptGenerator(nn.Module):
             x = f.view(f.shape[0], H, W, -1)
         return tuple(feats)
 
-    def init_prompt(self, embedding_feature, handcrafted_feature, block_num):
+    def init_prompt(self, embedding_feature, handcrafted_feature, block_num, with_embedding=True):
         """(mix_transformer_evp.py:749-756) -> (handcrafted, embedding); the returned tuple also carries
-        their sum, formed in the embedding GEMM's epilogue, which get_prompt consumes."""
+        their sum, formed in the embedding GEMM's epilogue, which get_prompt consumes.  ``with_embedding=False``
+        (the model's own forward, which only reads the sum) skips the stand-alone embedding GEMM: the tuple's
+        second item is then None."""
         lin = getattr(self, f"embedding_generator{block_num}")
         dt = embedding_feature.dtype
         p = get_packed(lin, dt, lambda d: dict(w=lin_w(lin, d), b=lin_b(lin)))
-        emb = ops.gemm(embedding_feature, p["w"], p["b"])
+        emb = ops.gemm(embedding_feature, p["w"], p["b"]) if with_embedding else None
         summed = ops.gemm(embedding_feature, p["w"], p["b"], residual=handcrafted_feature)
         return _Prompt((handcrafted_feature, emb), summed)
 
@@ -597,7 +599,7 @@ class MixVisionTransformerEVP(nn.Module):
             t, H, W = pe.embed_image(x) if s == 0 else pe.embed_nhwc(h)
             if s == 0 and hc_ready is not None:
                 torch.cuda.current_stream(t.device).wait_event(hc_ready)
-            prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1)
+            prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1, with_embedding=False)
             norm = getattr(self, f"norm{s + 1}")
             pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
             blocks = getattr(self, f"block{s + 1}")

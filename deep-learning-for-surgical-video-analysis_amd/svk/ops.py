@@ -578,11 +578,12 @@ def conv2d_stem_s2d(x, w_s2d, k, stride, pad, bias=None, act=None):
 
 
 STEM_LN = os.environ.get("SVK_STEM_LN", "1") == "1"
+STEM_LN16 = os.environ.get("SVK_STEM_LN16", "1") == "1"     # the 16-channel (handcrafted prompt) stem alone
 
 
 def conv2d_s2d_ln_supported(dtype, cs, cout, ow):
     """True when svk_conv2d_s2d_ln (stage-1 patch embedding over s2d blocks + LayerNorm in one kernel) covers it."""
-    return (STEM_LN and dtype in H16
+    return (STEM_LN and dtype in H16 and (int(cout) != 16 or STEM_LN16)
             and bool(_lib.load().svk_conv2d_s2d_ln_supported(dtype_code(dtype), int(cs), int(cout), int(ow))))
 
 

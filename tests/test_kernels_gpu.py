@@ -194,12 +194,12 @@ def test_gemm_library_backend(cuda, dt, act):
 
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,HB,CS,ln", [(3, 57, 48, True), (2, 57, 32, True), (1, 20, 48, False), (5, 57, 48, True)])
-def test_conv2d_s2d_ln(cuda, dt, B, HB, CS, ln):
+@pytest.mark.parametrize("C", [64, 16])
+def test_conv2d_s2d_ln(cuda, dt, B, HB, CS, ln, C):
     """The stage-1 patch embedding over s2d blocks + LayerNorm in one kernel (svk_conv2d_s2d_ln) against the
     unfused svk path (conv2d_nhwc, then layernorm: same conv rounding, LN statistics summed in another order)
-    and fp64."""
+    and fp64; C = 16 is the handcrafted prompt generator's first stem (64 / scale_factor 4 channels)."""
     from svk import ops
-    C = 64
     xs = _rand(B, HB, HB, CS, dt=dt, dev=cuda, seed=81)
     w = _rand(C, 4 * CS, dt=dt, dev=cuda, scale=(4 * CS) ** -0.5, seed=82)
     b = _rand(C, dt=torch.float32, dev=cuda, seed=83)
