@@ -8,7 +8,7 @@ O=gpurun_out
 R=r04
 mkdir -p $O/profiles_$R
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ "$rc" -eq 0 ] || exit $rc; }
-step precheck timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "conv2d_s2d_ln or mixffn_rw or fc1dw or pingpong or library_backend" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_precheck.log 2>&1
+step precheck timeout -k 10 300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k "conv2d_s2d_ln or mixffn_rw or fc1dw or pingpong or library_backend or gauss" --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_precheck.log 2>&1
 tail -1 $O/pytest_precheck.log
 step pytest timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 tail -1 $O/pytest_gpu.log
