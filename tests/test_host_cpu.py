@@ -50,6 +50,22 @@ def test_mixffn_supported_query():
     assert lib.svk_mixffn_supported(28, 128) == 0 and lib.svk_mixffn_supported(14, 320) == 0
 
 
+def test_fused_stem_supported_query():
+    """svk_conv2d_s2d_ln_supported needs no GPU: the RGB stem (48-channel blocks -> 64) and the handcrafted prompt
+    stem (48 -> 16 channels) are covered at the 224x224 width (OW = 56), other widths / channel counts are not."""
+    from svk import _lib
+    lib = _lib.load()
+    BF16, F16 = 1, 2   # include/svk.h: SVK_F32 = 0, SVK_BF16 = 1, SVK_F16 = 2
+    for dt in (F16, BF16):
+        assert lib.svk_conv2d_s2d_ln_supported(dt, 48, 64, 56) == 1
+        assert lib.svk_conv2d_s2d_ln_supported(dt, 48, 16, 56) == 1
+        assert lib.svk_conv2d_s2d_ln_supported(dt, 32, 16, 56) == 1
+        assert lib.svk_conv2d_s2d_ln_supported(dt, 48, 32, 56) == 0
+        assert lib.svk_conv2d_s2d_ln_supported(dt, 48, 64, 65) == 0
+        assert lib.svk_conv2d_s2d_ln_supported(dt, 64, 64, 56) == 0
+    assert lib.svk_conv2d_s2d_ln_supported(0, 48, 64, 56) == 0   # f32: the stem runs unfused
+
+
 def test_library_version_and_error_path():
     from svk import _lib
     lib = _lib.load()
