@@ -358,9 +358,10 @@ class PromptGenerator(nn.Module):
     def init_handcrafted(self, x):
         return self.init_prompts(x)
 
-    def init_prompts(self, segmap):
+    def init_prompts(self, segmap, ready=None):
         """Gaussian-filtered segmap -> handcrafted cascade (mix_transformer_evp.py:718-747);
-        returns the 4 token maps [B, N_s, C_s/4]."""
+        returns the 4 token maps [B, N_s, C_s/4].  ``ready``: 4 events, event s recorded on the current stream
+        as soon as map s exists (a consumer on another stream can start stage s without waiting for the rest)."""
         hg1 = self.handcrafted_generator1
         dt = compute_dtype(self)
         # gauss5x5_s2d always writes 3-channel (48-wide) blocks: only a 3-channel stem takes the blocks path
@@ -379,6 +380,8 @@ class PromptGenerator(nn.Module):
             g = getattr(self, f"handcrafted_generator{s + 1}")
             f, H, W = g.embed_blocks(x) if s == 0 and blocks else g.embed_nhwc(x)
             feats[s] = f
+            if ready is not None:
+                ready[s].record()
             x = f.view(f.shape[0], H, W, -1)
         return tuple(feats)
 
@@ -597,8 +600,10 @@ class MixVisionTransformerEVP(nn.Module):
         for s in range(4):
             pe = getattr(self, f"patch_embed{s + 1}")
             t, H, W = pe.embed_image(x) if s == 0 else pe.embed_nhwc(h)
-            if s == 0 and hc_ready is not None:
-                torch.cuda.current_stream(t.device).wait_event(hc_ready)
+            if hc_ready is not None:      # one event, or one per stage (the stage-s map is all stage s needs)
+                ev = hc_ready[s] if isinstance(hc_ready, (list, tuple)) else (hc_ready if s == 0 else None)
+                if ev is not None:
+                    torch.cuda.current_stream(t.device).wait_event(ev)
             prompt = self.prompt_generator.init_prompt(t, hcs[s], s + 1, with_embedding=False)
             norm = getattr(self, f"norm{s + 1}")
             pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
@@ -647,9 +652,13 @@ class MixVisionTransformerEVP(nn.Module):
             side = _side_stream(flow.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                hcs = self.prompt_generator.init_prompts(y.reshape(-1, 3, y.shape[-2], y.shape[-1]))
-                hc_ready = torch.cuda.Event()
-                hc_ready.record(side)
+                if PROMPT_STAGE_EVENTS:     # stage 1 starts once the first handcrafted map exists
+                    hc_ready = [torch.cuda.Event() for _ in range(4)]
+                    hcs = self.prompt_generator.init_prompts(y.reshape(-1, 3, y.shape[-2], y.shape[-1]), ready=hc_ready)
+                else:
+                    hcs = self.prompt_generator.init_prompts(y.reshape(-1, 3, y.shape[-2], y.shape[-1]))
+                    hc_ready = torch.cuda.Event()
+                    hc_ready.record(side)
                 f3, f4 = self.flow_encoder(flow)
             outs = self._stages(x, y, hcs=tuple(hcs), hc_ready=hc_ready)
         else:
@@ -669,6 +678,7 @@ class MixVisionTransformerEVP(nn.Module):
 
 
 FLOW_STREAM = os.environ.get("SVK_FLOW_STREAM", "1") == "1"
+PROMPT_STAGE_EVENTS = os.environ.get("SVK_PROMPT_STAGE_EVENTS", "1") == "1"
 _SIDE = {}
 
 
