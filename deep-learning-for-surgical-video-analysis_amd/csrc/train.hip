@@ -208,14 +208,24 @@ __global__ void act_bwd_kernel(const T* __restrict__ U, const T* __restrict__ dY
 }
 
 // ---- column statistics: sum and sum of squares over M rows (BN batch statistics) --------------
+// Deterministic two-phase reduction (round 5).  Phase 1: block (bx, cy) sums rows bx*4 + rl, stride
+// nblk*4, of 64 columns and writes its partial to ws[bx][c] (and ws[nblk + bx][c] for the squares); phase 2
+// sums the nblk partials of a column in block order and adds the total to the output.  No atomics: the
+// batch statistics, hence every BN + ReLU gate of the train forward, are bit-reproducible run to run.
+// (The former per-block atomicAdd made the last bit of the batch mean depend on the arrival order of the
+// blocks; a pre-ReLU value within that rounding of 0 then flipped its gate between runs, which is what moved
+// head.linear_fuse.conv.weight's gradient by 1.6 % in the intermittent round-4 test failure.)
+__host__ __device__ inline int stats_blocks(int M) { return M <= 0 ? 1 : (M + 63) / 64 < 1024 ? (M + 63) / 64 : 1024; }
+
 template <typename T>
-__global__ __launch_bounds__(256) void colstats_kernel(const T* __restrict__ X, long ldx, int M, int C,
-                                                       float* __restrict__ sum, float* __restrict__ sq) {
+__global__ __launch_bounds__(256) void colstats_part_kernel(const T* __restrict__ X, long ldx, int M, int C,
+                                                            float* __restrict__ ws, int want_sq) {
   const int c = blockIdx.y * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
+  const int nblk = gridDim.x;
   float s = 0.f, q = 0.f;
   if (c < C)
-    for (long r = (long)blockIdx.x * 4 + rl; r < M; r += (long)gridDim.x * 4) {
+    for (long r = (long)blockIdx.x * 4 + rl; r < M; r += (long)nblk * 4) {
       const float v = to_f(X[r * ldx + c]);
       s += v;
       q += v * v;
@@ -226,8 +236,37 @@ __global__ __launch_bounds__(256) void colstats_kernel(const T* __restrict__ X, 
   __syncthreads();
   if (rl == 0 && c < C) {
     const int t = threadIdx.x & 63;
-    atomicAdd(sum + c, ss[0][t] + ss[1][t] + ss[2][t] + ss[3][t]);
-    if (sq) atomicAdd(sq + c, sqq[0][t] + sqq[1][t] + sqq[2][t] + sqq[3][t]);
+    ws[(long)blockIdx.x * C + c] = (ss[0][t] + ss[1][t]) + (ss[2][t] + ss[3][t]);
+    if (want_sq) ws[(long)(nblk + blockIdx.x) * C + c] = (sqq[0][t] + sqq[1][t]) + (sqq[2][t] + sqq[3][t]);
+  }
+}
+
+// out0[c] += sum_b ws[b][c], out1[c] += sum_b ws[nblk + b][c]; tot (optional) receives the two totals as well
+// ([2][C]).  Block = 64 columns x 4 lanes, lane rl sums partials rl, rl + 4, ... in order, the four lane sums
+// meet in LDS in a fixed order: the result does not depend on scheduling.
+__global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, int nblk, int C,
+                                                           float* __restrict__ out0, float* __restrict__ out1,
+                                                           float* __restrict__ tot) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int rl = threadIdx.x >> 6;
+  const bool two = out1 || tot;
+  float a = 0.f, b = 0.f;
+  if (c < C)
+    for (int i = rl; i < nblk; i += 4) {
+      a += ws[(long)i * C + c];
+      if (two) b += ws[(long)(nblk + i) * C + c];
+    }
+  __shared__ float sa[4][64], sb[4][64];
+  sa[rl][threadIdx.x & 63] = a;
+  sb[rl][threadIdx.x & 63] = b;
+  __syncthreads();
+  if (rl == 0 && c < C) {
+    const int t = threadIdx.x & 63;
+    a = (sa[0][t] + sa[1][t]) + (sa[2][t] + sa[3][t]);
+    b = (sb[0][t] + sb[1][t]) + (sb[2][t] + sb[3][t]);
+    if (out0) out0[c] += a;
+    if (out1) out1[c] += b;
+    if (tot) { tot[c] = a; tot[C + c] = b; }
   }
 }
 
@@ -247,19 +286,22 @@ __global__ void bn_apply_kernel(const T* __restrict__ X, const float* __restrict
 
 // BN train-mode backward (with an optional ReLU after the BN, recomputed from X):
 // dxhat = dy' * g, dx = rstd/M * (M*dxhat - sum(dxhat) - xhat*sum(dxhat*xhat)).
-// sdy = sum dy', sdyx = sum dy'*xhat must be precomputed (bn_bwd_reduce_kernel).
+// Phase 1 writes per-block partials of sdy = sum dy' and sdyx = sum dy'*xhat (same row split as colstats),
+// colsum_final_kernel sums them in block order into tot [2][C] and adds them to dbeta / dgamma (which are
+// exactly those sums), and the apply kernel reads tot — the gradient buffers may hold earlier contributions.
 template <typename T>
-__global__ void bn_bwd_reduce_kernel(const T* __restrict__ X, const T* __restrict__ dY, const float* __restrict__ sum,
-                                     const float* __restrict__ sq, const float* __restrict__ g,
-                                     const float* __restrict__ b, int M, int C, float eps, int relu,
-                                     float* __restrict__ sdy, float* __restrict__ sdyx) {
+__global__ __launch_bounds__(256) void bn_bwd_part_kernel(const T* __restrict__ X, const T* __restrict__ dY,
+                                                          const float* __restrict__ sum, const float* __restrict__ sq,
+                                                          const float* __restrict__ g, const float* __restrict__ b,
+                                                          int M, int C, float eps, int relu, float* __restrict__ ws) {
   const int c = blockIdx.y * 64 + (threadIdx.x & 63);
   const int rl = threadIdx.x >> 6;
+  const int nblk = gridDim.x;
   float a1 = 0.f, a2 = 0.f;
   if (c < C) {
     const float mean = sum[c] / M;
     const float rstd = rsqrtf(fmaxf(sq[c] / M - mean * mean, 0.f) + eps);
-    for (long r = (long)blockIdx.x * 4 + rl; r < M; r += (long)gridDim.x * 4) {
+    for (long r = (long)blockIdx.x * 4 + rl; r < M; r += (long)nblk * 4) {
       const float xh = (to_f(X[r * C + c]) - mean) * rstd;
       float d = to_f(dY[r * C + c]);
       if (relu && xh * g[c] + b[c] <= 0.f) d = 0.f;
@@ -273,17 +315,16 @@ __global__ void bn_bwd_reduce_kernel(const T* __restrict__ X, const T* __restric
   __syncthreads();
   if (rl == 0 && c < C) {
     const int t = threadIdx.x & 63;
-    atomicAdd(sdy + c, s1[0][t] + s1[1][t] + s1[2][t] + s1[3][t]);
-    atomicAdd(sdyx + c, s2[0][t] + s2[1][t] + s2[2][t] + s2[3][t]);
+    ws[(long)blockIdx.x * C + c] = (s1[0][t] + s1[1][t]) + (s1[2][t] + s1[3][t]);
+    ws[(long)(nblk + blockIdx.x) * C + c] = (s2[0][t] + s2[1][t]) + (s2[2][t] + s2[3][t]);
   }
 }
 
 template <typename T>
 __global__ void bn_bwd_apply_kernel(const T* __restrict__ X, const T* __restrict__ dY, const float* __restrict__ sum,
                                     const float* __restrict__ sq, const float* __restrict__ g,
-                                    const float* __restrict__ b, const float* __restrict__ sdy,
-                                    const float* __restrict__ sdyx, T* __restrict__ dX, long n, int C, int M,
-                                    float eps, int relu) {
+                                    const float* __restrict__ b, const float* __restrict__ tot, T* __restrict__ dX,
+                                    long n, int C, int M, float eps, int relu) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int c = (int)(i % C);
@@ -292,7 +333,7 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ X, const T* __restrict
   const float xh = (to_f(X[i]) - mean) * rstd;
   float d = to_f(dY[i]);
   if (relu && xh * g[c] + b[c] <= 0.f) d = 0.f;
-  const float v = g[c] * rstd / M * (M * d - sdy[c] - xh * sdyx[c]);
+  const float v = g[c] * rstd / M * (M * d - tot[c] - xh * tot[C + c]);
   dX[i] = from_f<T>(v);
 }
 
@@ -659,13 +700,22 @@ extern "C" int svk_act_bwd(int dtype, const void* U, const void* dY, const void*
   });
 }
 
-extern "C" int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, void* stream) {
-  if (M < 0 || C <= 0 || !X || !sum) { set_error("svk_colstats: bad args"); return SVK_EINVAL; }
+extern "C" long svk_stats_ws_floats(int M, int C) {
+  if (M < 0 || C <= 0) return -1;
+  return 2L * stats_blocks(M) * C + 2L * C;
+}
+
+extern "C" int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, float* ws,
+                            void* stream) {
+  if (M < 0 || C <= 0 || !X || !sum || !ws) { set_error("svk_colstats: bad args"); return SVK_EINVAL; }
   if (M == 0) return SVK_OK;
-  const int bx = (int)std::min<long>((M + 63) / 64, 1024);
+  const int nb = stats_blocks(M);
+  hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
-    hipLaunchKernelGGL((colstats_kernel<T>), dim3(bx, (C + 63) / 64), dim3(256), 0, (hipStream_t)stream, (const T*)X,
-                       ldx, M, C, sum, sumsq);
+    hipLaunchKernelGGL((colstats_part_kernel<T>), dim3(nb, (C + 63) / 64), dim3(256), 0, st, (const T*)X, ldx, M, C,
+                       ws, sumsq ? 1 : 0);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 63) / 64), dim3(256), 0, st, (const float*)ws, nb, C, sum,
+                       sumsq, (float*)nullptr);
     return check_launch("colstats");
   });
 }
@@ -684,19 +734,22 @@ extern "C" int svk_bn_apply(int dtype, const void* X, const float* sum, const fl
 
 extern "C" int svk_bn_bwd(int dtype, const void* X, const void* dY, const float* sum, const float* sumsq,
                           const float* gamma, const float* beta, void* dX, float* dgamma, float* dbeta, int M, int C,
-                          float eps, int relu, void* stream) {
-  if (M <= 0 || C <= 0 || !X || !dY || !sum || !sumsq || !gamma || !beta || !dX || !dgamma || !dbeta) {
+                          float eps, int relu, float* ws, void* stream) {
+  if (M <= 0 || C <= 0 || !X || !dY || !sum || !sumsq || !gamma || !beta || !dX || !dgamma || !dbeta || !ws) {
     set_error("svk_bn_bwd: bad args"); return SVK_EINVAL;
   }
   const long n = (long)M * C;
-  const int bx = (int)std::min<long>((M + 63) / 64, 1024);
+  const int nb = stats_blocks(M);
+  float* tot = ws + 2L * nb * C;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_DTYPE(dtype, T, {
-    // dgamma/dbeta accumulate sum(dy'*xhat) / sum(dy') directly (they are exactly those sums)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T>), dim3(bx, (C + 63) / 64), dim3(256), 0, st, (const T*)X, (const T*)dY,
-                       sum, sumsq, gamma, beta, M, C, eps, relu, dbeta, dgamma);
+    hipLaunchKernelGGL((bn_bwd_part_kernel<T>), dim3(nb, (C + 63) / 64), dim3(256), 0, st, (const T*)X, (const T*)dY,
+                       sum, sumsq, gamma, beta, M, C, eps, relu, ws);
+    // dbeta += sum dy', dgamma += sum dy'*xhat (exactly the two sums)
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 63) / 64), dim3(256), 0, st, (const float*)ws, nb, C, dbeta,
+                       dgamma, tot);
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), g1(n), dim3(256), 0, st, (const T*)X, (const T*)dY, sum, sumsq, gamma,
-                       beta, dbeta, dgamma, (T*)dX, n, C, M, eps, relu);
+                       beta, (const float*)tot, (T*)dX, n, C, M, eps, relu);
     return check_launch("bn_bwd");
   });
 }

@@ -90,9 +90,9 @@ SIGNATURES = {
                           c_int, c_int, c_float, P],
     "svk_layernorm_bwd": [c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
     "svk_act_bwd": [c_int, P, P, P, P, c_long, c_int, P],
-    "svk_colstats": [c_int, P, c_long, c_int, c_int, P, P, P],
+    "svk_colstats": [c_int, P, c_long, c_int, c_int, P, P, P, P],
     "svk_bn_apply": [c_int, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P],
-    "svk_bn_bwd": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P],
+    "svk_bn_bwd": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P, P],
     "svk_bn_update_running": [P, P, c_int, c_int, c_float, P, P, P],
     "svk_resize_bilinear_bwd": [c_int, P, c_long, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_bcast_rows": [c_int, P, P, c_float, P, c_int, c_int, c_int, P],
@@ -110,7 +110,8 @@ LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int,
               "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int],
               "svk_mamba_scan_ragged_workspace": [c_int, c_int, c_int],
-              "svk_mstcn_bwd_workspace": [c_int, c_int]}
+              "svk_mstcn_bwd_workspace": [c_int, c_int],
+              "svk_stats_ws_floats": [c_int, c_int]}
 INT_QUERIES = {"svk_mixffn_supported": [c_int, c_int], "svk_mixffn_rw_supported": [c_int, c_int, c_int],
                "svk_mixffn_dw_fc2_supported": [c_int, c_int, c_int, c_int],
                "svk_conv2d_s2d_ln_supported": [c_int, c_int, c_int, c_int], "svk_mstcn_tile_size": []}

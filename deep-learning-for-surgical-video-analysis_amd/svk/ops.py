@@ -1157,11 +1157,20 @@ def act_bwd(u, dy, act, dres=None, out=None):
     return out
 
 
+def _stats_ws(M, C, device):
+    """Workspace of the deterministic column reductions (svk_colstats / svk_bn_bwd): per-block partials."""
+    n = _lib.load().svk_stats_ws_floats(M, C)
+    if n < 0:
+        raise _lib.SvkError(f"svk: bad statistics shape M={M} C={C}")
+    return torch.empty(n, device=device, dtype=torch.float32)
+
+
 def colstats(x, s, sq=None):
-    """s (+ sq) f32 [C] += column sums (of squares) of x [M, C]."""
+    """s (+ sq) f32 [C] += column sums (of squares) of x [M, C] (deterministic: fixed-order reduction)."""
     _chk(x, "x"); _chk(s, "sum", torch.float32); _chk(sq, "sumsq", torch.float32)
     M, C, ldx = _rows(x, "x")
-    _lib.call("svk_colstats", dtype_code(x.dtype), _p(x), ldx, M, C, _p(s), _p(sq), _stream())
+    _lib.call("svk_colstats", dtype_code(x.dtype), _p(x), ldx, M, C, _p(s), _p(sq), _p(_stats_ws(M, C, x.device)),
+              _stream())
     return s
 
 
@@ -1183,7 +1192,7 @@ def bn_bwd(x, dy, s, sq, gamma, beta, eps, dgamma, dbeta, relu=True, out=None):
     if out is None:
         out = torch.empty_like(x)
     _lib.call("svk_bn_bwd", dtype_code(x.dtype), _p(x), _p(dy), _p(s), _p(sq), _p(gamma), _p(beta), _p(out),
-              _p(dgamma), _p(dbeta), M, C, float(eps), 1 if relu else 0, _stream())
+              _p(dgamma), _p(dbeta), M, C, float(eps), 1 if relu else 0, _p(_stats_ws(M, C, x.device)), _stream())
     return out
 
 

@@ -133,6 +133,7 @@ class EVPTrainStep:
         self.group = process_group
         self.world = world_size
         self._bn_flat = None
+        self.keep_saved, self.last_saved = False, None
         self.steps = 0
         dev = next(model.parameters()).device
         if dev.type != "cuda":
@@ -726,6 +727,8 @@ class EVPTrainStep:
         self.grad.zero_()
         self.conv_scratch.zero_()
         sv, logits, ant = self._forward(x, y, flow, masks)
+        if self.keep_saved:                   # tests: the forward's saved tensors (BN sums, ReLU outputs)
+            self.last_saved = sv
         loss, dl, da = ops.phase_loss(logits, ant, labels, ant_targets)
         self._pending = (sv, self._backward_head(sv, dl, da))
         return loss, logits, ant

@@ -471,17 +471,22 @@ int svk_layernorm_bwd(int dtype, const void* X, long ldx, const void* dY, long l
 /* dX = dY * act'(U) (+ dR), elementwise over n (GELU erf / ReLU / tanh). */
 int svk_act_bwd(int dtype, const void* U, const void* dY, const void* dR, void* dX, long n, int act, void* stream);
 
-/* Column sums (and sums of squares, optional) over M rows, += into f32 sum/sumsq: batch statistics
- * and bias gradients. */
-int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, void* stream);
+/* Column sums (and sums of squares, optional) over M rows, += into f32 sum/sumsq: batch statistics.
+ * Deterministic (round 5): per-block partials into the caller's workspace ws, then a fixed-order sum — no
+ * atomics, so the batch statistics (and every BN + ReLU gate after them) are bit-reproducible run to run.
+ * ws holds svk_stats_ws_floats(M, C) floats (shared by svk_colstats and svk_bn_bwd). */
+long svk_stats_ws_floats(int M, int C);
+int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, float* ws,
+                 void* stream);
 
 /* BatchNorm2d train mode on [M = B*H*W, C]: Y = act((X - mean) rsqrt(var + eps) g + b) from colstats
- * sums (biased variance), and its backward with the optional ReLU recomputed from X (dgamma/dbeta +=). */
+ * sums (biased variance), and its backward with the optional ReLU recomputed from X (dgamma/dbeta +=;
+ * the same deterministic two-phase reduction through ws). */
 int svk_bn_apply(int dtype, const void* X, const float* sum, const float* sumsq, const float* gamma,
                  const float* beta, void* Y, int M, int C, float eps, int act, void* stream);
 int svk_bn_bwd(int dtype, const void* X, const void* dY, const float* sum, const float* sumsq,
                const float* gamma, const float* beta, void* dX, float* dgamma, float* dbeta, int M, int C,
-               float eps, int relu, void* stream);
+               float eps, int relu, float* ws, void* stream);
 /* running_mean/var momentum update (unbiased variance), as nn.BatchNorm2d does in train mode. */
 int svk_bn_update_running(const float* sum, const float* sumsq, int M, int C, float momentum,
                           float* running_mean, float* running_var, void* stream);

@@ -76,6 +76,18 @@ def _bn_train(x, sd, p, stats, eps=1e-5):
     return xh * sd[p + ".weight"][None, :, None, None] + sd[p + ".bias"][None, :, None, None]
 
 
+def _relu(x, site, gates, pre):
+    """F.relu at a named ReLU site.  ``pre`` (a dict) records the pre-activation; ``gates`` maps a site to a
+    boolean tensor of x's shape that replaces the gate (x > 0) — used to evaluate the oracle on the branch an
+    f32 implementation took for elements within its rounding of the kink (ReLU is not differentiable at 0, and
+    torch's relu backward takes the x > 0 side there)."""
+    if pre is not None:
+        pre[site] = x.detach().clone()
+    if gates is not None and site in gates:
+        return x * gates[site].to(device=x.device, dtype=x.dtype)
+    return F.relu(x)
+
+
 def _block_train(x, H, W, sd, p, heads, sr, ma, mm):
     """Block.forward with DropPath (mix_transformer_evp.py:167-171)."""
     x = x + ma[:, None, None] * M.attention(M._ln(x, sd, p + ".norm1", M.BLOCK_EPS), H, W, sd, p + ".attn", heads, sr)
@@ -83,8 +95,10 @@ def _block_train(x, H, W, sd, p, heads, sr, ma, mm):
     return x
 
 
-def forward_train(x, y, flow, sd, variant, masks, stats):
-    """MixVisionTransformerEVP.forward in train mode -> (logits [B, 7], anticipation [B, 7])."""
+def forward_train(x, y, flow, sd, variant, masks, stats, gates=None, pre=None):
+    """MixVisionTransformerEVP.forward in train mode -> (logits [B, 7], anticipation [B, 7]).  ReLU sites
+    (``gates`` / ``pre``, see _relu): flow_encoder.bn1..4 and head.linear_fuse.bn (NCHW), head.fc.0 and
+    head.fc_ant.0 ([B, 512])."""
     depths = M.CONFIGS[variant]["depths"]
     x = x.reshape(-1, 3, 224, 224)
     y = y.reshape(-1, 3, 224, 224)
@@ -107,7 +121,7 @@ def forward_train(x, y, flow, sd, variant, masks, stats):
     feats = []
     for i, st, pad in ((1, 4, 3), (2, 2, 1), (3, 2, 1), (4, 2, 1)):
         f = F.conv2d(f, sd[f"flow_encoder.conv{i}.weight"], sd[f"flow_encoder.conv{i}.bias"], stride=st, padding=pad)
-        f = F.relu(_bn_train(f, sd, f"flow_encoder.bn{i}", stats))
+        f = _relu(_bn_train(f, sd, f"flow_encoder.bn{i}", stats), f"flow_encoder.bn{i}", gates, pre)
         feats.append(f)
     f3, f4 = feats[2].flatten(2).transpose(1, 2), feats[3].flatten(2).transpose(1, 2)
     c3, H3, W3 = outs[2]
@@ -119,17 +133,20 @@ def forward_train(x, y, flow, sd, variant, masks, stats):
     for (t, h, w), name in zip(reversed(outs), ("linear_c4", "linear_c3", "linear_c2", "linear_c1")):
         maps.append(M._resize_nhwc(M._lin(t, sd, f"head.{name}.proj"), h, w, H4))
     c = F.conv2d(torch.cat(maps, dim=1), sd["head.linear_fuse.conv.weight"])
-    c = F.relu(_bn_train(c, sd, "head.linear_fuse.bn", stats))
+    c = _relu(_bn_train(c, sd, "head.linear_fuse.bn", stats), "head.linear_fuse.bn", gates, pre)
     c = c * masks["dropout2d"].to(c.dtype)[:, :, None, None]
     feat = c.mean(dim=(2, 3))
-    yl = F.linear(F.relu(M._lin(feat, sd, "head.fc.0")), sd["head.fc.2.weight"], sd["head.fc.2.bias"])
-    ya = F.linear(F.relu(M._lin(feat, sd, "head.fc_ant.0")), sd["head.fc_ant.2.weight"], sd["head.fc_ant.2.bias"])
+    yl = F.linear(_relu(M._lin(feat, sd, "head.fc.0"), "head.fc.0", gates, pre), sd["head.fc.2.weight"],
+                  sd["head.fc.2.bias"])
+    ya = F.linear(_relu(M._lin(feat, sd, "head.fc_ant.0"), "head.fc_ant.0", gates, pre), sd["head.fc_ant.2.weight"],
+                  sd["head.fc_ant.2.bias"])
     return yl, ya
 
 
-def loss_and_grads(x, y, flow, labels, ant_targets, sd, variant, masks, dtype=torch.float64):
+def loss_and_grads(x, y, flow, labels, ant_targets, sd, variant, masks, dtype=torch.float64, gates=None, pre=None):
     """One train_model inner iteration up to backward (train_evp.py:473-512).  Returns
-    (loss_phase, loss_ant, {trainable name: grad}, {bn prefix: (batch mean, unbiased var)})."""
+    (loss_phase, loss_ant, {trainable name: grad}, {bn prefix: (batch mean, unbiased var)}).  ``gates`` /
+    ``pre``: ReLU gate overrides / pre-activation capture (forward_train)."""
     p = {k: (v.detach().to(dtype).clone() if v.is_floating_point() else v) for k, v in sd.items()}
     for k in p:
         if is_trainable(k) and p[k].is_floating_point():
@@ -137,7 +154,7 @@ def loss_and_grads(x, y, flow, labels, ant_targets, sd, variant, masks, dtype=to
     m = {"blocks": [[(a.to(dtype), b.to(dtype)) for a, b in st] for st in masks["blocks"]],
          "dropout2d": masks["dropout2d"].to(dtype)}
     stats = {}
-    yl, ya = forward_train(x.to(dtype), y.to(dtype), flow.to(dtype), p, variant, m, stats)
+    yl, ya = forward_train(x.to(dtype), y.to(dtype), flow.to(dtype), p, variant, m, stats, gates, pre)
     lp = F.cross_entropy(yl, labels, reduction="sum")
     la = F.smooth_l1_loss(ya, ant_targets.to(dtype), reduction="sum")
     (lp + la).backward()
