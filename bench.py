@@ -848,10 +848,8 @@ def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value
                 f.write(f"{ms / prof_steps:8.3f} ms/step n={n // prof_steps:3d} {fl / ms / 1e9:8.1f} TF/s "
                         f"{nb / ms / 1e6:8.1f} GB/s  {shape:28s} {name}\n")
     gemm_ms = sum(v[0] for v in per.values())
-    # the dominant HAND-WRITTEN kernel: library GEMMs (libgemm.hip, hipBLASLt) are reported beside it
-    lib = {k: v for k, v in per.items() if k.startswith("hipblaslt")}
-    own = {k: v for k, v in per.items() if k not in lib} or per
-    name, (ms, flops, nbytes, n) = max(own.items(), key=lambda kv: kv[1][0])
+    # the dominant kernel (every GEMM of the step is a hand-written svk kernel: no library backend since round 5)
+    name, (ms, flops, nbytes, n) = max(per.items(), key=lambda kv: kv[1][0])
     peak = PEAK_TFLOPS[dtype_name]
     # bound by arithmetic intensity vs the machine balance (peak FLOP/s / 8 TB/s): tall-skinny
     # token GEMMs (K or N <= 128) are HBM-bound, the head / 4096-wide GEMMs MFMA-bound
@@ -870,11 +868,6 @@ def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value
                 "kernel_tflops": round(tflops, 2), "kernel_gbs": round(gbs, 1),
                 "all_gemm_tflops": round(sum(v[1] for v in per.values()) / (gemm_ms * 1e-3) / 1e12, 2),
                 "gemm_share_of_step": round(gemm_ms / prof_steps / (elapsed * 1e3 / steps), 3)}
-    if lib:
-        lms = sum(v[0] for v in lib.values())
-        roofline["library_gemm"] = {"backend": "hipBLASLt", "launches_per_step": sum(v[3] for v in lib.values()) // prof_steps,
-                                    "ms_per_step": round(lms / prof_steps, 3),
-                                    "tflops": round(sum(v[1] for v in lib.values()) / (lms * 1e-3) / 1e12, 2)}
     if workload in ("extract", "e2e"):
         # whole-step MFMA utilisation: measured frames/s x algorithmic work / dense peak
         roofline["step_mfma_util"] = round(value / world * EXTRACT_GFLOP_PER_FRAME * 1e9 / (peak * 1e12), 4)

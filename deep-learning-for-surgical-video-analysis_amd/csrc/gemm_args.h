@@ -46,9 +46,6 @@ inline int splitk_bm() {
 // schedule, 2 = deep + stream-K; returns 1 when not eligible.
 template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant);
 
-// libgemm.hip: hipBLASLt for plain-epilogue dense GEMMs (act none / ReLU, bias, residual with act none);
-// dtype SVK_F16 / SVK_BF16; returns 1 when not eligible or no algorithm.
-int libgemm_try(const GemmArgs& a, hipStream_t st, int dtype);
 
 // wgrad_pk.hip: dW (+ db) += dY^T X (16-bit operands, LDS-DMA slabs + ds_read_b64_tr_b16 fragments),
 // batched over Z = (Z / nzi, Z % nzi) element offsets; returns 1 when not eligible (caller: wgrad_kernel).

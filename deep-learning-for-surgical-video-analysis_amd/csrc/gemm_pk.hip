@@ -513,27 +513,6 @@ static const int g_pk_policy = getenv("SVK_PK_POLICY") ? atoi(getenv("SVK_PK_POL
 // ran 8.60 ms with it vs 8.42 ms without (same box, profiles/r04/bench_pp_ab.txt): one 128 KiB-LDS workgroup per
 // CU for the whole persistent launch leaves no room for the side stream's kernels to co-run
 static const int g_pp_policy = getenv("SVK_PP") ? atoi(getenv("SVK_PP")) : 0;
-// library GEMM by policy (SVK_LIBGEMM, default 1 = on, 0 = off): the long-K token
-// GEMMs of stages 3-4 and the head, where hipBLASLt measures faster than every hand-written tile in isolation
-// (profiles/r04/pk_cfg_sweep_lib.txt) AND the graph-replayed step gains in a same-box A/B (profiles/r04/libgemm_ab.txt:
-// 32.68 k -> 33.40 k frames/s with classes 1 | 4 | 8 | 16).  The stage-3 fc1 (class 2) stays hand-written: it is
-// slower inside the step than alone (73 vs 63 us) and no faster than gemm_pk there, and the all-classes run on
-// another box lowered sclk for the whole step (2.38 -> 2.22 GHz).  bf16: the extraction step gains 2 % (30.2 / 30.5 k ->
-// 30.8 / 31.0 k frames/s), the B = 88 train step's stage-3 fc2 (M = 17 248) does not (5 940 -> 5 922): class 1 needs
-// M >= 32768 (profiles/r04/libgemm_ab.txt)
-static const int g_lib_policy = getenv("SVK_LIBGEMM") ? atoi(getenv("SVK_LIBGEMM")) : 1;
-template <typename T>
-static bool libgemm_policy(const GemmArgs& a) {
-  if (a.M < 8192 || a.K < 320 || a.U || a.rscale) return false;
-  // shape classes (bit mask): 1 long K narrow N (s3 fc2), 2 wide N short K (s3 fc1), 4 long K N = 512 (s4 fc2),
-  // 8 N = 1024 K = 512 (s4 kv), 16 long K wide N (the head)
-  static const int mask = getenv("SVK_LIBGEMM_MASK") ? atoi(getenv("SVK_LIBGEMM_MASK")) : 29;
-  const int cls = (a.K >= 1024 && a.N < 512) ? 1 : (a.N >= 1024 && a.K < 512) ? 2 : (a.K >= 1024 && a.N == 512) ? 4
-                : (a.N == 1024 && a.K == 512) ? 8 : (a.K >= 1024 && a.N >= 1024) ? 16 : 0;
-  if (cls == 1 && a.M < 32768) return false;
-  return (cls & mask) != 0;
-}
-
 template <typename T>
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   const int force = g_tune[TUNE_PK_CFG];
@@ -586,7 +565,6 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
         const long rounds = (t256 + 255) / 256;
         if (t256 >= 192 && (t256 <= 256 || a.K >= 1024 || t256 * 10 >= rounds * 256 * 9)) cfg = 71;
       }
-      if (g_lib_policy && libgemm_policy<T>(a)) cfg = 80;
       // (round-2 sweep: 128 x 128 for the stage-3 fc1 and 128 x 160 for its fc2 win 5-7 us each in
       // isolation but lost 2 % of the whole graph-replayed step: kept 128 x 64)
     }
@@ -598,9 +576,6 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   // and 256x256 with 8 waves spills (128 accumulator + 96 epilogue-operand VGPRs): not instantiated.  The
   // kernel keeps NSTAGE generic (epilogue loads issued NSTAGE - 2 steps before a tile's last step).
   if (cfg == 40 && a.N % 160 != 0) cfg = 10;
-  // 80: the library GEMM (libgemm.hip: hipBLASLt, plain epilogues only)
-  if (asrc == 0 && cfg == 80 && libgemm_try(a, st, std::is_same<T, _Float16>::value ? SVK_F16 : SVK_BF16) == 0) return 0;
-  if (cfg == 80) cfg = -1;
   // 70 / 71 / 72: the 256 x 256 ping-pong kernel (gemm_pp.hip: first / deep DMA schedule / deep + stream-K)
   if (asrc == 0 && cfg >= 70 && cfg <= 72 && gemm_pp_try<T>(a, st, cfg - 70) == 0) return 0;
   if (cfg >= 70 && cfg <= 72) cfg = 60;
