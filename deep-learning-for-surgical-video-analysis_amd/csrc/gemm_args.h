@@ -45,6 +45,9 @@ inline int splitk_bm() {
 // gemm_pp.hip: 256 x 256 ping-pong persistent GEMM, dense A, plain epilogue; variant 0 / 1 = first / deep DMA
 // schedule, 2 = deep + stream-K; returns 1 when not eligible.
 template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant);
+// gemm_wt.hip: wide-tile (one 256-thread workgroup per CU, 2 x 2 waves of 128-row sub-tiles) persistent GEMM,
+// dense A, plain epilogue; cfg 0 / 1 / 2 = 256 x 256 / 256 x 160 / 256 x 128 tiles; returns 1 when not eligible.
+template <typename T> int gemm_wt_try(const GemmArgs& a, hipStream_t st, int cfg);
 
 
 // wgrad_pk.hip: dW (+ db) += dY^T X (16-bit operands, LDS-DMA slabs + ds_read_b64_tr_b16 fragments),

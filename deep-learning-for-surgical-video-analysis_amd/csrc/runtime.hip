@@ -46,7 +46,7 @@ int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3
 // Caller-owned per-stream workspaces (svk_set_stream_workspace): the stream-K GEMM's partial sums and flags.
 struct StreamWs { hipStream_t st; void* part; long bytes; int* flags; int nflags; };
 static StreamWs g_ws[16];
-static int g_nws = 0;
+static int g_nws = 0, g_ws_next = 0;   // full table: entries are replaced oldest first
 static std::mutex g_ws_mu;
 
 bool stream_workspace(hipStream_t st, void** part, long* bytes, int** flags, int* nflags) {
@@ -72,7 +72,11 @@ extern "C" int svk_set_stream_workspace(void* stream, void* part, long part_byte
       svk::g_ws[i] = svk::StreamWs{st, part, part_bytes, flags, nflags};
       return SVK_OK;
     }
-  if (svk::g_nws == 16) { svk::set_error("svk_set_stream_workspace: too many streams"); return SVK_EUNSUPPORTED; }
+  if (svk::g_nws == 16) {                 // evict the oldest registration instead of failing the 17th stream
+    svk::g_ws[svk::g_ws_next] = svk::StreamWs{st, part, part_bytes, flags, nflags};
+    svk::g_ws_next = (svk::g_ws_next + 1) % 16;
+    return SVK_OK;
+  }
   svk::g_ws[svk::g_nws++] = svk::StreamWs{st, part, part_bytes, flags, nflags};
   return SVK_OK;
 }

@@ -67,6 +67,9 @@ class TrainAugment:
             transforms = (RandomCrop(crop), ColorJitter(0.1, 0.1, 0.1, 0.05) if use_flip else None,
                           RandomHorizontalFlip(), RandomRotation(5) if use_flip else None)
         self.crop, self.jitter, self.flip, self.rotation = transforms
+        if getattr(self.crop, "padding", 0):
+            # the GPU pass crops the resized image itself (train_evp.py:146-163 uses RandomCrop(224), no padding)
+            raise _lib.SvkError("svk.augment: RandomCrop(padding > 0) is not implemented by the GPU pass")
         self._ws = {}
 
     # ---- parameter draws, in CholecFlowDataset.__getitem__'s order ---------------------------------------
@@ -113,6 +116,21 @@ class TrainAugment:
         t = lambda rows: torch.tensor(rows, dtype=torch.int32) if rows else None
         return t(img), t(seg), t(fl)
 
+    def _check_params(self, prm, flow):
+        """Host-side validation of per-sample parameters (the kernels trust them): crop offsets inside the resized
+        image, flag fields 0 / 1.  A device tensor is copied to the host for the check."""
+        OH, OW = self.size
+        C = self.crop_size
+        q = prm.cpu() if prm.is_cuda else prm
+        if q.numel() == 0:
+            return
+        x1, y1 = q[:, 0], q[:, 1]
+        if bool(((x1 < 0) | (x1 > OW - C) | (y1 < 0) | (y1 > OH - C)).any()):
+            raise _lib.SvkError(f"svk.augment: crop offsets must lie in [0, {OW - C}] x [0, {OH - C}]")
+        flags = (2, 3) if flow else (2, 3, 10)
+        if bool(((q[:, list(flags)] != 0) & (q[:, list(flags)] != 1)).any()):
+            raise _lib.SvkError("svk.augment: flip / rotation / jitter flags must be 0 or 1")
+
     # ---- GPU passes ---------------------------------------------------------------------------------------
     def images(self, frames, params, out=None):
         """frames [B, H, W, 3] uint8 (GPU), params [B, 16] int32 -> [B, 3, 224, 224] f32."""
@@ -125,6 +143,7 @@ class TrainAugment:
         prm = params.to(frames.device, torch.int32).contiguous()
         if tuple(prm.shape) != (B, NP):
             raise _lib.SvkError(f"svk.augment: params must be [{B}, {NP}] int32")
+        self._check_params(params, flow=False)
         xb, xk, ksx = _coeffs(W, OW, frames.device)
         yb, yk, ksy = _coeffs(H, OH, frames.device)
         key = (B, H, frames.device)
@@ -152,6 +171,9 @@ class TrainAugment:
         OH, OW = self.size
         C = self.crop_size
         prm = params.to(flow.device, torch.int32).contiguous()
+        if tuple(prm.shape) != (B, NP):
+            raise _lib.SvkError(f"svk.augment: params must be [{B}, {NP}] int32")
+        self._check_params(params, flow=True)
         key = (H, W, OH, OW, flow.device)
         if key not in _CV_CACHE:
             xo, xa = cv2_linear_table(W, OW)

@@ -72,10 +72,7 @@ def set_profiler(records):
 
 def tune(knob, value):
     """Set a kernel-selection knob (svk_tune: "pk_cfg", "pk_elds", "dw_lds", "dw_rows"; -1 = auto)."""
-    global _SK_WANTED
     _lib.call("svk_tune", knob.encode(), int(value))
-    if knob == "pk_cfg" and int(value) == 72:
-        _SK_WANTED = True
 
 
 def _last_kernel():
@@ -121,8 +118,6 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
     if (SKINNY and row_scale is None and a.dtype in H16 and N <= 64 and K <= 128 and M >= 2048
             and a.data_ptr() % 16 == 0 and (K % 8 or lda % 8 == 0)):
         return gemm_skinny(a, w, bias, act, residual, out, N, dact, dact_src)
-    if _SK_WANTED and a.dtype in H16:
-        _stream_workspace(a.device)
     t0 = _prof_begin()
     if row_scale is None and dact is None:
         _lib.call("svk_gemm", dtype_code(a.dtype), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
@@ -151,26 +146,6 @@ def gemm(a, w, bias=None, act=None, residual=None, out=None, n=None, row_scale=N
 
 
 SKINNY = os.environ.get("SVK_SKINNY", "1") == "1"
-
-# Stream-K workspace of the 256-row ping-pong GEMM (gemm_pp): partial sums of up to 256 workgroups (8 waves x 32 f32x4
-# x 64 lanes each = 256 KiB) and one zeroed flag per (workgroup, wave).  Caller-owned (the library allocates
-# nothing): registered once per (device, stream) with svk_set_stream_workspace; a capture stream gets its own
-# from the graph's pool, kept alive here.
-SK_SLOTS = 256
-_SK_WS = {}
-_SK_WANTED = os.environ.get("SVK_PP_SK") == "1"   # registered only while a stream-K variant can be chosen
-
-
-def _stream_workspace(device):
-    st = _stream()
-    key = (device.index, st)
-    if key in _SK_WS:
-        return
-    part = torch.empty(SK_SLOTS * 8 * 32 * 64 * 4, device=device, dtype=torch.float32)
-    flags = torch.zeros(SK_SLOTS * 8, device=device, dtype=torch.int32)
-    _SK_WS[key] = (part, flags)
-    _lib.call("svk_set_stream_workspace", st, _p(part), part.numel() * 4, _p(flags), flags.numel())
-
 
 def gemm_skinny(a, w, bias=None, act=None, residual=None, out=None, n=None, dact=None, dact_src=None):
     """svk_gemm_skinny (bf16 / f16, N <= 64, K <= 128): same contract as gemm() without row_scale."""

@@ -118,3 +118,24 @@ def test_train_flow_transform_matches_host_classes():
         ref = rot(fl(crop(t.clone())))
         got = AU.train_flow_transform(flow, (x1, y1), do_flip, ang)
         torch.testing.assert_close(got, ref, rtol=0, atol=0)
+
+
+def test_train_augment_rejects_bad_params():
+    """the GPU passes trust the per-sample parameters, so TrainAugment validates them on the host —
+    crop offsets inside the 250 x 250 resized image, 0 / 1 flags — and refuses a padded RandomCrop it does not
+    implement."""
+    from models import data_process as DP
+    from svk import SvkError
+    from svk.augment import TrainAugment, NP
+    ta = TrainAugment()
+    ok = torch.zeros(2, NP, dtype=torch.int32)
+    ok[:, 0], ok[:, 1] = 26, 3
+    ta._check_params(ok, flow=False)
+    ta._check_params(ok, flow=True)
+    for col, v in ((0, 27), (1, -1), (2, 2), (3, 5), (10, 3)):
+        bad = ok.clone()
+        bad[1, col] = v
+        with pytest.raises(SvkError):
+            ta._check_params(bad, flow=False)
+    with pytest.raises(SvkError):
+        TrainAugment(transforms=(DP.RandomCrop(224, padding=4), None, DP.RandomHorizontalFlip(), None))

@@ -163,6 +163,34 @@ def test_gemm_pingpong_configs(cuda, cfg, dt, act):
         ops.tune("pk_cfg", -1)
 
 
+@pytest.mark.parametrize("cfg", [90, 91, 92])
+@pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("act", [None, "gelu", "relu"])
+def test_gemm_wide_tile_configs(cuda, cfg, dt, act):
+    """The wide-tile GEMM (gemm_wt: one 256-thread workgroup per CU, 256 x 256 / 256 x 160 / 256 x 128 tiles, forced
+    through svk_tune) against fp64: M / N / K tails, residual on / off, more tiles than workgroups (the persistent
+    walk crossing tiles), one K-tile per tile, and the MiT-b2 shapes it is meant for."""
+    from svk import ops
+    try:
+        ops.tune("pk_cfg", cfg)
+        for M, N, K, res in ((5000, 320, 1280, True), (777, 136, 200, False), (12544, 512, 512, True),
+                             (12544, 2048, 1024, False), (3000, 640, 72, True), (300, 1280, 64, False),
+                             (50176, 320, 320, True), (70000, 256, 128, False)):
+            a = _rand(M, K, dt=dt, dev=cuda, seed=61)
+            w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=62)
+            b = _rand(N, dt=torch.float32, dev=cuda, seed=63)
+            r = _rand(M, N, dt=dt, dev=cuda, seed=64) if res else None
+            got = ops.gemm(a, w, b, act=act, residual=r)
+            ref = a.double() @ w.double().t() + b.double()
+            ref = {None: lambda t: t, "gelu": lambda t: F.gelu(t), "relu": torch.relu}[act](ref)
+            if res:
+                ref = ref + r.double()
+            assert ops._last_kernel().startswith("gemm_wt"), ops._last_kernel()
+            _close(got, ref.cpu(), dt)
+    finally:
+        ops.tune("pk_cfg", -1)
+
+
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,HB,CS,ln", [(3, 57, 48, True), (2, 57, 32, True), (1, 20, 48, False), (5, 57, 48, True)])
 @pytest.mark.parametrize("C", [64, 16])

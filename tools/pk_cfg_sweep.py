@@ -17,7 +17,7 @@ SHAPES = [  # (M, N, K, residual, what)
     (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"), (200704, 128, 128, True, "s2 q/proj"),
     (802816, 64, 64, True, "s1 q/proj"),
 ]
-CFGS = [(-1, "auto"), (10, "128x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair")]
+CFGS = [(-1, "auto"), (10, "128x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair"), (90, "wt256"), (91, "wt160"), (92, "wt128")]
 
 
 def timeit(fn, reps):
@@ -61,7 +61,7 @@ def main():
             err = float((y.float() - ref.float()).abs().max())
             ms = timeit(lambda: ops.gemm(a, w, b, residual=r, out=out), args.reps)
             row.append(f"{name} {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF d={err:.1e}"
-                       + ("" if cfg < 70 or kname.startswith("gemm_pp")
+                       + ("" if cfg < 70 or kname.startswith(("gemm_pp", "gemm_wt"))
                              else " (fallback)"))
         lib.svk_tune(b"pk_cfg", -1)
         ms = timeit(lambda: torch.matmul(a, w.t(), out=out), args.reps)   # hipBLASLt, no epilogue (yardstick)
