@@ -576,9 +576,9 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   // and 256x256 with 8 waves spills (128 accumulator + 96 epilogue-operand VGPRs): not instantiated.  The
   // kernel keeps NSTAGE generic (epilogue loads issued NSTAGE - 2 steps before a tile's last step).
   if (cfg == 40 && a.N % 160 != 0) cfg = 10;
-  // 90 / 91 / 92: the wide-tile kernel (gemm_wt.hip: 256 x 256 / 256 x 160 / 256 x 128)
-  if (asrc == 0 && cfg >= 90 && cfg <= 92 && gemm_wt_try<T>(a, st, cfg - 90) == 0) return 0;
-  if (cfg >= 90 && cfg <= 92) cfg = 60;
+  // 90 / 91 / 92 / 93: the wide-tile kernel (gemm_wt.hip: 256 x 256 / 256 x 160 / 256 x 128 / 256 x 192)
+  if (asrc == 0 && cfg >= 90 && cfg <= 93 && gemm_wt_try<T>(a, st, cfg - 90) == 0) return 0;
+  if (cfg >= 90 && cfg <= 93) cfg = 60;
   // 70 / 71 / 72: the 256 x 256 ping-pong kernel (gemm_pp.hip: first / deep DMA schedule / deep + stream-K)
   if (asrc == 0 && cfg >= 70 && cfg <= 72 && gemm_pp_try<T>(a, st, cfg - 70) == 0) return 0;
   if (cfg >= 70 && cfg <= 72) cfg = 60;

@@ -163,7 +163,7 @@ def test_gemm_pingpong_configs(cuda, cfg, dt, act):
         ops.tune("pk_cfg", -1)
 
 
-@pytest.mark.parametrize("cfg", [90, 91, 92])
+@pytest.mark.parametrize("cfg", [90, 91, 92, 93])
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("act", [None, "gelu", "relu"])
 def test_gemm_wide_tile_configs(cuda, cfg, dt, act):
@@ -173,9 +173,9 @@ def test_gemm_wide_tile_configs(cuda, cfg, dt, act):
     from svk import ops
     try:
         ops.tune("pk_cfg", cfg)
-        for M, N, K, res in ((5000, 320, 1280, True), (777, 136, 200, False), (12544, 512, 512, True),
-                             (12544, 2048, 1024, False), (3000, 640, 72, True), (300, 1280, 64, False),
-                             (50176, 320, 320, True), (70000, 256, 128, False)):
+        for M, N, K, res in ((5000, 320, 1280, True), (777, 136, 192, False), (12544, 512, 512, True),
+                             (12544, 2048, 1024, False), (3000, 640, 64, True), (300, 1280, 64, False),
+                             (50176, 320, 320, True), (70000, 256, 128, False), (1000, 2052, 128, True)):
             a = _rand(M, K, dt=dt, dev=cuda, seed=61)
             w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=62)
             b = _rand(N, dt=torch.float32, dev=cuda, seed=63)

@@ -17,7 +17,7 @@ SHAPES = [  # (M, N, K, residual, what)
     (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"), (200704, 128, 128, True, "s2 q/proj"),
     (802816, 64, 64, True, "s1 q/proj"),
 ]
-CFGS = [(-1, "auto"), (10, "128x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair"), (90, "wt256"), (91, "wt160"), (92, "wt128")]
+CFGS = [(-1, "auto"), (10, "128x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair"), (90, "wt256"), (91, "wt160"), (92, "wt128"), (93, "wt192")]
 
 
 def timeit(fn, reps):
