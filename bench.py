@@ -917,6 +917,16 @@ def run_leg(args, dev, rank, world, dtype):
                 check(o2)
                 other[name] = {"value": round(world * units * n2 / el2, 2), "ms_per_step": round(el2 * 1e3 / n2, 3),
                                "steps": n2}
+                # this dtype's own dominant-kernel roofline (fp32 = generate_evp_LFB.py's precision,
+                # priced against the 157 TF f32 MFMA peak), from profiled eager iterations of the same step
+                rec2 = []
+                ops.set_profiler(rec2)
+                for _ in range(prof_steps):
+                    (step.profile if hasattr(step, "profile") else step)()
+                torch.cuda.synchronize()
+                ops.set_profiler(None)
+                other[name]["roofline"] = roofline_of(rec2, prof_steps, el2, n2, args.workload, name,
+                                                      world * units * n2 / el2, world, None)
             step.set_dtype(dtype)
     value = world * units * args.steps / elapsed
     f32_only = args.workload in ("mstcn", "mamba", "preproc", "tecno_train", "augment")

@@ -13,18 +13,17 @@
 // at TM = TN = 8 a wave reads 16 fragment vectors per 64 MFMAs (4x the reuse) and the 256 accumulator registers
 // sit in the AGPR half of the register file.
 //
-// Pipeline (measured lesson of the first version: with one 64-deep K-tile in flight the LDS-DMA landing time,
-// ~1-2 us under load, was exposed every K-tile — 2.6x the MFMA time):
-//  * the K axis is cut into 32-deep stages; a ring of NS stages in LDS (NS = 4: 128 KiB at 256 x 256), filled by
-//    LDS-DMA (`global_load_lds_dwordx4`), NS - 1 stages in flight — ~1.5 us of landing time at the MFMA rate;
-//  * stage image: rows paired into 128-byte "double rows" (row 2d + h, 16-byte k-chunk c of 4 -> chunk slot
-//    ((h << 2) | c) ^ (d & 7) of double row d), so every ds_read_b128 fragment read of the 16x16x32 MFMA is
-//    bank-conflict-free and a lane's fragment offset inside a 16-row group is a per-lane constant;
-//  * one barrier per stage, in the MIDDLE of the stage's row groups: after the reads of stage u are all issued
-//    (row group TM - 2) every wave waits for its share of stage u + 1, then the barrier; behind it stage u's
-//    buffer is refilled (DMA of stage u + NS, spread over the next row groups: an LDS-DMA issue costs ~60 cycles
-//    among MFMAs) and the fragments of stage u + 1 are read under the MFMAs of stage u's last row group — the
-//    matrix pipe does not wait for LDS at stage boundaries;
+// Pipeline (measured: with one whole 64-deep K-tile issued at the top of each K-tile the LDS-DMA landing time was
+// exposed every K-tile; 32-deep stages in a 4-deep ring were slower still — each DMA wave-instruction then covers
+// 16 rows x 64 B, twice the cache-line requests per byte, and the chip's LDS-DMA rate is request-bound):
+//  * 64-deep stages (128-byte rows, the gemm_pk image: chunk c of row r in slot c ^ (r & 7), conflict-free
+//    ds_read_b128 fragments), a ring of NS = 160 KiB / stage stages (2 at 256 x 256 / 256 x 192, 3 at
+//    256 x 160 / 256 x 128), filled by LDS-DMA (`global_load_lds_dwordx4`);
+//  * one barrier per stage, in the MIDDLE: after the reads of stage u are all issued (row group 2 TM - 2 of the
+//    2 TM (k-step, row block) groups) every wave waits for its share of stage u + 1, then the barrier; behind it
+//    stage u's slot is refilled (DMA of stage u + NS, spread over the next stage's row groups: an LDS-DMA issue
+//    costs ~60 cycles among MFMAs) and the k-step-0 fragments of stage u + 1 are read under the MFMAs of stage u's
+//    last row group — the matrix pipe does not wait for LDS at stage boundaries;
 //  * persistent: the grid (one workgroup per CU) walks its tiles; the next tile's first stages are in flight
 //    during the current tile's last ones and its epilogue;
 //  * transposed MFMA (W fragment x A fragment): each lane holds 4 consecutive output columns of a row; the
@@ -44,19 +43,13 @@ typedef __attribute__((address_space(3))) void* las_ptr;
 template <int TM_, int TN_, int NS_>
 struct Cfg {
   static constexpr int TM = TM_, TN = TN_, NS = NS_;
-  static constexpr int WM = 16 * TM, WN = 16 * TN, BM = 2 * WM, BN = 2 * WN, BK = 32, NT = 256;
+  static constexpr int WM = 16 * TM, WN = 16 * TN, BM = 2 * WM, BN = 2 * WN, BK = 64, NT = 256;
   static constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  // DMA wave-instructions (1 KiB each) of one stage, dealt round-robin to the 4 waves; a wave whose share is
-  // short issues a padding DMA of the zero block into the TRASH KiB, so every wave counts the same LD
+  // DMA wave-instructions (1 KiB each) of one stage, dealt round-robin to the 4 waves
   static constexpr int NI_A = A_BYTES / 1024, NI_B = B_BYTES / 1024;
-  static constexpr int LDA = (NI_A + 3) / 4, LDB = (NI_B + 3) / 4, LD = LDA + LDB;
-  static constexpr bool PAD = NI_A % 4 != 0 || NI_B % 4 != 0;
-  // ring, the padding-DMA sink, and the bias vector (f32, up to MAXN columns: loaded once per launch, so the
-  // epilogue's bias reads are LDS reads — a compiler-visible global load there would make hipcc wait for every
-  // older vector-memory operation, i.e. for the DMA stages in flight)
-  static constexpr int MAXN = 4096;
-  static constexpr int STAGE = A_BYTES + B_BYTES, TRASH = NS * STAGE, BIAS = TRASH + 1024, LDS = BIAS + MAXN * 4;
-  static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "tile rows must be whole DMA instructions");
+  static constexpr int LDA = NI_A / 4, LDB = NI_B / 4, LD = LDA + LDB;
+  static constexpr int STAGE = A_BYTES + B_BYTES, TRASH = NS * STAGE, LDS = NS * STAGE + 1024;
+  static_assert(NI_A % 4 == 0 && NI_B % 4 == 0, "tile rows must split into whole DMA rounds");
   static_assert(LDS <= 160 * 1024, "LDS");
   static_assert((NS - 2) * LD <= 63, "vmcnt range");
   // mid-stage wait right after a tile's epilogue: its TM * TN stores sit between the stage waited for and the
@@ -113,41 +106,26 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
   const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
   const long ldab = p.lda * 2, ldwb = p.ldw * 2;
 
-  // bias -> LDS (before any DMA is in flight: the loads' wait drains nothing else)
-  float* sbias = reinterpret_cast<float*>(smem + C::BIAS);
-  for (int n = tid; n < p.N; n += 256) sbias[n] = p.bias ? p.bias[n] : 0.f;
-  __syncthreads();
-
-  // ---- DMA.  Instruction t of a stage's A (or W) image moves slots q = t * 64 + lane: double row d = q / 8,
-  // slot s = q % 8 holds chunk c = s ^ (d & 7) = (h << 2) | kc of row 2d + h.  This lane's (h, kc) is the same
-  // for every t (t * 64 moves d by multiples of 8); its row is 16 t + 2 (lane / 8) + h.
-  const int dl = lane >> 3, cs = (lane & 7) ^ (dl & 7), hl = cs >> 2, kl = cs & 3;
+  // ---- DMA.  Instruction t of a stage's A (or W) image moves slots q = t * 64 + lane: row 8 t + lane / 8, slot
+  // lane % 8 holding chunk (lane % 8) ^ ((lane / 8) & 7) — the same chunk for every t.
+  const int lr = lane >> 3, cq = (lane & 7) ^ (lr & 7);
   uint32_t offA[C::LDA], offB[C::LDB];
   auto set_rows = [&](int tile) __attribute__((always_inline)) {
-    const int m0 = (tile / ntn) * BM + 2 * dl + hl, n0 = (tile % ntn) * BN + 2 * dl + hl;
+    const int m0 = (tile / ntn) * BM + lr, n0 = (tile % ntn) * BN + lr;
 #pragma unroll
     for (int i = 0; i < C::LDA; ++i)
-      offA[i] = (uint32_t)min(m0 + 16 * (i * 4 + wave), p.M - 1) * (uint32_t)ldab + kl * 16;
+      offA[i] = (uint32_t)min(m0 + 8 * (i * 4 + wave), p.M - 1) * (uint32_t)ldab + cq * 16;
 #pragma unroll
     for (int i = 0; i < C::LDB; ++i)
-      offB[i] = (uint32_t)min(n0 + 16 * (i * 4 + wave), p.N - 1) * (uint32_t)ldwb + kl * 16;
+      offB[i] = (uint32_t)min(n0 + 8 * (i * 4 + wave), p.N - 1) * (uint32_t)ldwb + cq * 16;
   };
-  // DMA instruction idx (A for idx < LDA, then W) of stage ks (32-deep K slice) into ring slot buf
+  // DMA instruction idx (A for idx < LDA, then W) of stage ks (64-deep K slice) into ring slot buf
   auto issue1 = [&](int ks, int buf, int idx) __attribute__((always_inline)) {
     const bool isA = idx < C::LDA;
     const int i = isA ? idx : idx - C::LDA;
-    const int t = i * 4 + wave;                                   // the stage's instruction number
-    const bool pad = t >= (isA ? C::NI_A : C::NI_B);             // wave-uniform
-    const uint32_t lds = __builtin_amdgcn_readfirstlane(
-        pad ? lds0 + C::TRASH : lds0 + buf * C::STAGE + (isA ? 0 : C::A_BYTES) + t * 1024);
-    const uint32_t off = isA ? offA[isA ? i : 0] : offB[isA ? 0 : i];
-    const char* base = (isA ? Ab : Wb) + ks * 64;
-    if constexpr (KTAIL || C::PAD) {
-      const bool ok = !pad && (!KTAIL || ks * 32 + kl * 8 < p.K);
-      dma16(ok ? base + off : zero, lds);
-    } else {
-      dma16s(base, off, lds);
-    }
+    const int t = i * 4 + wave;
+    const uint32_t lds = __builtin_amdgcn_readfirstlane(lds0 + buf * C::STAGE + (isA ? 0 : C::A_BYTES) + t * 1024);
+    dma16s((isA ? Ab : Wb) + ks * 128, isA ? offA[isA ? i : 0] : offB[isA ? 0 : i], lds);
   };
 
   f32x4 acc[TM][TN];
@@ -156,15 +134,15 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // fragment of 16-row group g (row0 = 16 g) of a stage image: this lane reads row row0 + fr, k-chunk fq
-  const int foff = (fr >> 1) * 128 + ((((fr & 1) << 2) | fq) ^ ((fr >> 1) & 7)) * 16;
-  auto frag = [&](int buf, bool isB, int g) {
-    return *reinterpret_cast<const tx8*>(smem + buf * C::STAGE + (isB ? C::A_BYTES : 0) + g * 1024 + foff);
+  // fragment of 16-row group g of a stage image, k-step ks (32 of the stage's 64): row 16 g + fr, chunk ks 4 + fq
+  const int foff0 = fr * 128 + ((0 + fq) ^ (fr & 7)) * 16, foff1 = fr * 128 + ((4 + fq) ^ (fr & 7)) * 16;
+  auto frag = [&](int buf, bool isB, int g, int ks) {
+    return *reinterpret_cast<const tx8*>(smem + buf * C::STAGE + (isB ? C::A_BYTES : 0) + g * 2048 + (ks ? foff1 : foff0));
   };
   tx8 fb[2][TN], fa[2];
-  auto read_b = [&](int buf, tx8* dst) {
+  auto read_b = [&](int buf, int ks) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) dst[j] = frag(buf, true, wn * TN + j);
+    for (int j = 0; j < TN; ++j) fb[ks][j] = frag(buf, true, wn * TN + j, ks);
   };
 
   const T* R = static_cast<const T*>(p.R);
@@ -175,7 +153,7 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = min(n0 + j * 16 + fq * 4, p.N - 4);
-      bj[j] = *reinterpret_cast<const f32x4*>(sbias + n);
+      bj[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + n) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -206,7 +184,7 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
   };
 
   // ---- the stage stream of this workgroup: tiles first, first + G, ...; nk stages each.  The DMA cursor (dtile,
-  // dks) runs NS stages ahead of the compute cursor; the stage it fills goes to ring slot dbuf.
+  // dks) fills ring slot dbuf.
   int dtile = first, dks = 0, dbuf = 0;
   auto advance = [&]() __attribute__((always_inline)) {
     dbuf = dbuf + 1 == NS ? 0 : dbuf + 1;
@@ -225,6 +203,7 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
       rows_tile = t;
     }
   };
+  auto pad_dma = [&]() __attribute__((always_inline)) { dma16(zero, __builtin_amdgcn_readfirstlane(lds0 + C::TRASH)); };
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s) {
     if (dtile < ntiles) {
@@ -234,46 +213,57 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
       advance();
     } else {
 #pragma unroll
-      for (int idx = 0; idx < LD; ++idx) dma16(zero, __builtin_amdgcn_readfirstlane(lds0 + C::TRASH));
+      for (int idx = 0; idx < LD; ++idx) pad_dma();
     }
   }
   // stage 0 landed (NS - 2 younger stages in flight) -> barrier -> its first fragments
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 2) * LD) : "memory");
   barrier();
   int buf = 0;
-  read_b(0, fb[0]);
-  fa[0] = frag(0, false, wm * TM);
+  read_b(0, 0);
+  fa[0] = frag(0, false, wm * TM, 0);
   // the stage whose DMA rides on the current stage's row groups: stage u + NS - 1 into slot (u - 1) % NS (the
   // prologue filled slots 0 .. NS - 2); past the end of the stream, padding DMA keeps every count exact
   int pks = dks, pbuf = dbuf, ptile = dtile;
   bool plive = dtile < ntiles;
   if (plive) advance();
   int stores = 0;        // mid-stage waits left with a tile's epilogue stores younger than the stage they need
-  constexpr int PER = (LD + TM - 2) / (TM - 1);   // refill instructions per row group
-  // one stage of the stream; CUR = which fb[] holds its B fragments (compile-time: a runtime index would put the
-  // fragment arrays in scratch)
-  auto stage = [&](auto CUR_) __attribute__((always_inline)) {
-    constexpr int CUR = decltype(CUR_)::value;
-    // row groups 0 .. TM - 2: the next A fragment read ahead, the refill DMA spread over them
+  constexpr int NG = 2 * TM;                          // (k-step, row block) groups of a stage
+  // refill schedule: FRONT instructions right behind the mid-stage barrier that frees the slot (with a 2-deep ring
+  // the stage has only until the next mid-stage wait to land), the rest PER per group from the next stage's start
+  constexpr int FRONT = NS == 2 ? (LD + 1) / 2 : 0;
+  constexpr int PER = 2;
+  static_assert(FRONT + PER * (NG - 1) >= LD, "refill schedule");
+  if constexpr (FRONT > 0) {             // the first pending stage's front part (no mid-stage barrier before it)
+    if (plive) ensure_rows(ptile);
 #pragma unroll
-    for (int i = 0; i < TM - 1; ++i) {
-      if (i == 0 && plive) ensure_rows(ptile);
+    for (int idx = 0; idx < FRONT; ++idx) {
+      if (plive) issue1(pks, pbuf, idx);
+      else pad_dma();
+    }
+  }
+  auto stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int g = 0; g < NG - 1; ++g) {
+      const int ks = g / TM, i = g % TM;
+      if (g == 0 && plive) ensure_rows(ptile);
 #pragma unroll
       for (int r = 0; r < PER; ++r) {
-        const int idx = i * PER + r;
+        const int idx = FRONT + g * PER + r;
         if (idx < LD) {
           if (plive) issue1(pks, pbuf, idx);
-          else dma16(zero, __builtin_amdgcn_readfirstlane(lds0 + C::TRASH));
+          else pad_dma();
         }
       }
-      fa[(i + 1) & 1] = frag(buf, false, wm * TM + i + 1);
+      if (g == TM - 2) read_b(buf, 1);                // k-step 1's B fragments under k-step 0's last row blocks
+      fa[(g + 1) & 1] = frag(buf, false, wm * TM + (g + 1) % TM, (g + 1) / TM);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[CUR][j], fa[i & 1], acc[i][j]);
+      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[ks][j], fa[g & 1], acc[i][j]);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // mid-stage: every DMA instruction of this stage's refill is out; the next stage (issued NS - 2 stages ago)
-    // must have landed — NS - 2 younger stages may stay in flight (a tile's epilogue stores in between: NWAIT_ST)
-    // — and every wave's reads of this stage are retired
+    // mid-stage: every DMA instruction of this stage's refill is out; the next stage must have landed — NS - 2
+    // younger stages may stay in flight (a tile's epilogue stores in between: NWAIT_ST) — and every wave's reads
+    // of this stage are retired
     if (stores > 0) {
       asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(C::NWAIT_ST) : "memory");
       --stores;
@@ -287,23 +277,27 @@ void gemm_wt(GemmArgs p, int ntn, int ntiles, int nk) {
     pbuf = dbuf;
     ptile = dtile;
     if (plive) advance();
-    // fragments of the next stage under the last row group's MFMAs (past the stream's end they read a stale slot:
-    // never used)
-    const int nbuf = buf + 1 == NS ? 0 : buf + 1;
-    read_b(nbuf, fb[CUR ^ 1]);
-    const tx8 fa_next = frag(nbuf, false, wm * TM);
+    if constexpr (FRONT > 0) {
+      if (plive) ensure_rows(ptile);
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[TM - 1][j] = mfma16x16x32(fb[CUR][j], fa[(TM - 1) & 1], acc[TM - 1][j]);
+      for (int idx = 0; idx < FRONT; ++idx) {
+        if (plive) issue1(pks, pbuf, idx);
+        else pad_dma();
+      }
+    }
+    // k-step-0 fragments of the next stage (fb[0] is free since this stage's k-step 0) under the last group's
+    // MFMAs; past the stream's end they read a stale slot, never used
+    const int nbuf = buf + 1 == NS ? 0 : buf + 1;
+    read_b(nbuf, 0);
+    const tx8 fa_next = frag(nbuf, false, wm * TM, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[TM - 1][j] = mfma16x16x32(fb[1][j], fa[(NG - 1) & 1], acc[TM - 1][j]);
     __builtin_amdgcn_sched_barrier(0);
     fa[0] = fa_next;
     buf = nbuf;
   };
-  // nk is even (host): stages alternate fb[0] / fb[1] and every tile starts on fb[0]
   for (int tile = first; tile < ntiles; tile += G) {
-    for (int ks = 0; ks < nk; ks += 2) {
-      stage(std::integral_constant<int, 0>{});
-      stage(std::integral_constant<int, 1>{});
-    }
+    for (int ks = 0; ks < nk; ++ks) stage();
     // (outside the K loop: inside it hipcc hoists the epilogue's per-tile addresses and keeps them live next to
     // the accumulators)
     epilogue(tile);
@@ -366,13 +360,12 @@ int gemm_wt_try(const GemmArgs& a, hipStream_t st, int cfg) {
   if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
   // 32-bit per-lane byte offsets of the DMA rows
   if ((long)a.M * a.lda * 2 + 256 >= (1L << 32) || (long)a.N * a.ldw * 2 + 256 >= (1L << 32)) return 1;
-  if (a.N > 4096) return 1;                       // the bias vector lives in LDS (Cfg::MAXN)
-  if (a.K % 64) return 1;                         // an even number of 32-deep stages per tile
+  if (a.K % 64) return 1;                         // whole 64-deep stages (no K tails)
   switch (cfg) {
-    case 0: return wt::launch_cfg<T, 8, 8, 4>(a, st);
-    case 3: return wt::launch_cfg<T, 8, 6, 4>(a, st);
-    case 1: return wt::launch_cfg<T, 8, 5, 4>(a, st);
-    case 2: return wt::launch_cfg<T, 8, 4, 5>(a, st);
+    case 0: return wt::launch_cfg<T, 8, 8, 2>(a, st);
+    case 1: return wt::launch_cfg<T, 8, 5, 3>(a, st);
+    case 2: return wt::launch_cfg<T, 8, 4, 3>(a, st);
+    case 3: return wt::launch_cfg<T, 8, 6, 2>(a, st);
     default: return 1;
   }
 }
