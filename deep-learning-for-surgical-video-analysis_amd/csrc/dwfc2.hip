@@ -253,6 +253,245 @@ static int launch(const void* H, const float* taps, const float* db, const void*
 }
 
 }  // namespace dwfc
+// ---- stage-3 form with the depthwise conv on the MATRIX cores (round 5) -------------
+// The LDS-tap form above is LDS-bound (per 64-token K-step it reads 9 halo chunks and 18 tap vectors from
+// LDS for every token it produces, ≈ 220 KB).  A register-window VALU form of the same production (taps as
+// DPP-fused v_fmac along image rows, measured 174 us vs 187 unfused at B = 256) is VALU-bound: 9 FMAs +
+// the GELU per element at two waves per SIMD, with the fc2 MFMAs in a separate phase.  Here the depthwise
+// 3x3 runs on MFMA as a block-diagonal implicit GEMM, so the VALU is left with the GELU only:
+//
+//   Gpre^T[c][tok] = sum_(t, c') Tap^T[c][(t, c')] * Hsh^T[(t, c')][tok],   Tap^T[c][(t, c')] = tap[t][c] [c == c']
+//
+// per 16-channel block: K = 9 taps x 16 channels = 144, padded to 5 MFMA k-steps (16x16x32); the A fragments
+// (one non-zero per lane) are built from the taps each K-step, the B fragments are shifted reads of the H
+// tile in LDS (the implicit-GEMM conv gather).  15/16 of those MFMA products are zeros, still cheaper per
+// useful MAC than the VALU (512 MAC / 16 cycles vs 16 FMA / 4 cycles per SIMD).
+//
+//  * tile = (frame, 4 image rows) x all N output channels, m-block = one image row: 16 slots, slot x16 =
+//    pixel x16 - 1 (slots 0 / 15 = the conv's zero padding; their outputs are never stored);
+//  * H tile per K-step (6 image rows = the 4 output rows +- 1, 16 slots, 64 channels; rows outside the frame
+//    and the padding slots from the zero block, 16-byte chunks XOR-swizzled by slot on the source address)
+//    LDS-DMA'd three K-steps ahead into a 3-deep ring;
+//  * wave w: the dwconv of channels 16 w .. 16 w + 15 for the 4 rows (20 MFMAs), GELU, G (16-bit, as the
+//    unfused dwconv stores it) into a [64 slot][64 channel] LDS tile; then fc2 over its N / 4 output columns
+//    (transposed MFMA: W2 fragment x G fragment, 40 MFMAs per K-step, a lane ends with 4 consecutive output
+//    channels of one token);
+//  * software pipeline, one barrier per K-step: iteration k runs the dwconv MFMAs of K-step k + 1, the fc2
+//    MFMAs of k (G(k) made one iteration earlier; the W2 fragments of k + 1 are loaded behind each half), the
+//    GELU of k + 1 (interleaved with those MFMAs by the scheduler), loads the taps of k + 2, DMAs H(k + 3) and
+//    waits for everything but that DMA.
+// Numerics: taps rounded to the 16-bit type (as autocast casts the conv weight), products exact and summed in
+// f32 from the bias, gelu_rl, G rounded to 16 bits; fc2 as the GEMM (f32, + b2, + residual, one rounding).
+namespace dwrw {
+
+template <int N_>
+struct Cfg {
+  static constexpr int N = N_, WI = 14, R = 4, NT = 256, BK = 64;
+  static constexpr int WNB = N / 64;                   // 16-column n-blocks per wave (fc2)
+  static constexpr int HROWS = R + 2, NHB = 3;
+  static constexpr int HBYTES = HROWS * 16 * 128;      // 12 KiB: 6 rows x 16 slots x 64 channels (16-bit)
+  static constexpr int HBLK = HBYTES / 1024;           // 1 KiB DMA blocks (12: 3 per wave)
+  static constexpr int GBYTES = R * 16 * 128;          // 8 KiB
+  static constexpr int H_OFF = 0, G_OFF = NHB * HBYTES, LDS = G_OFF + 2 * GBYTES;
+  static constexpr int TILES_PER_FRAME = (WI + R - 1) / R;
+  static_assert(N % 64 == 0 && HBLK == 12, "shape");
+};
+
+template <typename T, class C>
+__global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, const float* __restrict__ taps,
+                                                 const float* __restrict__ dbias, const T* __restrict__ W2,
+                                                 const float* __restrict__ b2, const T* __restrict__ R,
+                                                 T* __restrict__ Y, int ntiles, int K, int diag) {
+  typedef v8_t<T> tx8;
+  constexpr int WI = C::WI, WNB = C::WNB, RR = C::R;
+  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(dwfc::las_ptr)smem;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tile = dwfc::xcd_remap(blockIdx.x, gridDim.x);
+  if (tile >= ntiles) return;
+  const int frame = tile / C::TILES_PER_FRAME, y0 = (tile % C::TILES_PER_FRAME) * RR;
+  const int nk = K / C::BK;
+  const long fbase = (long)frame * WI * WI;            // first token of the frame
+
+  // ---- DMA of the H tile of K-step kt into ring slot hb: chunk q = 64 blk + lane (blk = wave + 4 j): row
+  // i = q / 128, slot px = (q / 8) % 16, LDS chunk cs = q % 8 holds global chunk cs ^ (px & 7)
+  const char* zero = reinterpret_cast<const char*>(dwfc::g_zero);
+  const char* hsrc[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int q = (wave + 4 * j) * 64 + lane;
+    const int i = q >> 7, px = (q >> 3) & 15, c = (q & 7) ^ (px & 7), y = y0 - 1 + i;
+    hsrc[j] = (px >= 1 && px <= WI && y >= 0 && y < WI)
+                  ? reinterpret_cast<const char*>(Hm + (fbase + (long)y * WI + (px - 1)) * K + c * 8)
+                  : nullptr;
+  }
+  auto dma_h = [&](int kt, int hb) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      dwfc::dma16(hsrc[j] ? hsrc[j] + kt * 128 : zero,
+                  __builtin_amdgcn_readfirstlane(lds0 + C::H_OFF + hb * C::HBYTES + (wave + 4 * j) * 1024));
+  };
+
+  // ---- dwconv on MFMA.  B fragment (kk, mb): lane (fr, fq) reads tap t = 2 kk + (fq >> 1) (t = 9: padding,
+  // any address) of token (row mb, slot fr): H at row mb + t / 3, slot fr + t % 3 - 1 (clamped: the padding
+  // slots' own outputs are garbage, never stored), channels 16 w + 8 (fq & 1) .. + 7
+  int hoff[5];
+#pragma unroll
+  for (int kk = 0; kk < 5; ++kk) {
+    const int t = min(2 * kk + (fq >> 1), 8), dy = t / 3, dx = t % 3;
+    const int sl = min(max(fr + dx - 1, 0), 15), c = 2 * wave + (fq & 1);
+    hoff[kk] = (dy * 16 + sl) * 128 + ((c ^ (sl & 7)) << 4);
+  }
+  // A fragment kk: row = channel fr of the block, k = 8 fq .. 8 fq + 7 = (tap 2 kk + (fq >> 1), channels
+  // 8 (fq & 1) .. + 7): one non-zero, tap[t][16 w + fr], at k-slot j = fr - 8 (fq & 1) when 0 <= j < 8
+  const int jsl = fr - 8 * (fq & 1);
+  const bool aon = jsl >= 0 && jsl < 8;
+  uint32_t amask[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) amask[d] = (aon && (jsl >> 1) == d) ? ~0u : 0u;
+  const int ash = (jsl & 1) * 16;
+  float tv[5];
+  float4 dbv;
+  auto load_taps = [&](int kt) {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const int t = min(2 * kk + (fq >> 1), 8);
+      tv[kk] = taps[(long)t * K + kt * 64 + 16 * wave + fr];
+    }
+    dbv = *reinterpret_cast<const float4*>(dbias + kt * 64 + 16 * wave + 4 * fq);
+  };
+  tx8 afr[5];
+  auto build_a = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const T tt = from_f<T>(2 * kk + (fq >> 1) < 9 ? tv[kk] : 0.f);
+      const uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, tt) << ash;
+      const uint4 u = {v & amask[0], v & amask[1], v & amask[2], v & amask[3]};
+      afr[kk] = __builtin_bit_cast(tx8, u);
+    }
+  };
+  f32x4 dacc[RR];
+  auto dwconv = [&](int hb) {
+    const char* hs = smem + C::H_OFF + hb * C::HBYTES;
+#pragma unroll
+    for (int mb = 0; mb < RR; ++mb) dacc[mb] = f32x4{dbv.x, dbv.y, dbv.z, dbv.w};
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk)
+#pragma unroll
+      for (int mb = 0; mb < RR; ++mb)
+        dacc[mb] = mfma16x16x32(afr[kk], *reinterpret_cast<const tx8*>(hs + hoff[kk] + mb * 2048), dacc[mb]);
+  };
+  // GELU of the dwconv outputs -> G tile gb: lane (fr, fq) of m-block mb = channels 16 w + 4 fq .. + 3, slot mb 16 + fr
+  auto gelu_store = [&](int gb) {
+#pragma unroll
+    for (int mb = 0; mb < RR; ++mb) {
+      T o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = from_f<T>((diag & 2) ? dacc[mb][r] : dwfc::gelu_rl(dacc[mb][r]));
+      const int s = mb * 16 + fr, cw = 16 * wave + 4 * fq;
+      *reinterpret_cast<uint2*>(smem + C::G_OFF + gb * C::GBYTES + s * 128 + ((((cw >> 3) ^ (s & 7)) << 4) | ((cw & 4) << 1))) =
+          *reinterpret_cast<const uint2*>(o);
+    }
+  };
+
+  // ---- fc2: wave's n-blocks n0w + 16 nb, W2 fragments of one K-step (2 x 32 channels)
+  const int n0w = wave * (C::N / 4);
+  tx8 w2f[2][WNB];
+  auto load_w2 = [&](int kt, int ks) {
+    if ((diag & 1) && kt > 0) kt = 0;                  // timing ablation: W2 of K-step 0 only (L1-resident)
+#pragma unroll
+    for (int nb = 0; nb < WNB; ++nb)
+      w2f[ks][nb] = *reinterpret_cast<const tx8*>(W2 + (long)(n0w + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
+  };
+  f32x4 acc[RR][WNB];
+#pragma unroll
+  for (int mb = 0; mb < RR; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto fc2_half = [&](int gb, int ks) {
+    const char* gs = smem + C::G_OFF + gb * C::GBYTES;
+#pragma unroll
+    for (int mb = 0; mb < RR; ++mb) {
+      const int row = mb * 16 + fr;
+      const tx8 g = *reinterpret_cast<const tx8*>(gs + row * 128 + (((ks * 4 + fq) ^ (row & 7)) << 4));
+#pragma unroll
+      for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = mfma16x16x32(w2f[ks][nb], g, acc[mb][nb]);
+    }
+  };
+
+  // ---- prologue: H(0..2) in the ring, G(0), taps(1), W2(0)
+  load_taps(0);
+  dma_h(0, 0);
+  dma_h(min(1, nk - 1), 1);
+  dma_h(min(2, nk - 1), 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  build_a();
+  dwconv(0);
+  gelu_store(0);
+  load_taps(min(1, nk - 1));
+  load_w2(0, 0);
+  load_w2(0, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // iteration kt < nk - 1: dwconv(kt + 1) || fc2(kt), GELU(kt + 1) -> G ring, taps(kt + 2), DMA H(kt + 3)
+  for (int kt = 0; kt + 1 < nk; ++kt) {
+    build_a();                                         // taps(kt + 1), loaded one iteration ago
+    dwconv((kt + 1) % 3);
+    fc2_half(kt & 1, 0);
+    load_w2(kt + 1, 0);
+    fc2_half(kt & 1, 1);
+    load_w2(kt + 1, 1);
+    gelu_store((kt + 1) & 1);
+    load_taps(min(kt + 2, nk - 1));
+    // H(kt + 3) into the slot dwconv(kt) read (before the previous barrier); clamped past the end (never read)
+    dma_h((diag & 4) ? 0 : min(kt + 3, nk - 1), kt % 3);   // diag 4: timing ablation, H of K-step 0 only
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // all but this DMA: H(kt + 2), W2(kt + 1), taps(kt + 2)
+    __syncthreads();
+  }
+  fc2_half((nk - 1) & 1, 0);
+  fc2_half((nk - 1) & 1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the clamped tail DMA (never read) retires
+
+  // ---- epilogue: lane (fr, fq) of block (mb, nb) = token (row y0 + mb, pixel fr - 1), channels n .. n + 3
+#pragma unroll
+  for (int mb = 0; mb < RR; ++mb) {
+    const int y = y0 + mb, x = fr - 1;
+    if (y >= WI || x < 0 || x >= WI) continue;
+    const long m = fbase + (long)y * WI + x;
+#pragma unroll
+    for (int nb = 0; nb < WNB; ++nb) {
+      const int n = n0w + nb * 16 + fq * 4;
+      const float4 bb = *reinterpret_cast<const float4*>(b2 + n);
+      float v[4] = {acc[mb][nb][0] + bb.x, acc[mb][nb][1] + bb.y, acc[mb][nb][2] + bb.z, acc[mb][nb][3] + bb.w};
+      if (R) {
+        const uint2 r = *reinterpret_cast<const uint2*>(R + m * C::N + n);
+        const f32x2 r01 = unpack2<T>(r.x), r23 = unpack2<T>(r.y);
+        v[0] += r01.x; v[1] += r01.y; v[2] += r23.x; v[3] += r23.y;
+      }
+      const T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
+      *reinterpret_cast<uint2*>(Y + m * C::N + n) = *reinterpret_cast<const uint2*>(o);
+    }
+  }
+}
+
+template <typename T, class C>
+static int launch(const void* H, const float* taps, const float* db, const void* W2, const float* b2, const void* R,
+                  void* Y, int B, int K, hipStream_t st) {
+  static const int diag = getenv("SVK_DWFC2_DIAG") ? atoi(getenv("SVK_DWFC2_DIAG")) : 0;   // timing ablations only
+  const long nt = (long)B * C::TILES_PER_FRAME;
+  if (nt > 0x7fffffffL || (long)B * C::WI * C::WI * K > 0x7fffffffL) return SVK_EUNSUPPORTED;
+  hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), 0, st, (const T*)H, taps, db, (const T*)W2, b2,
+                     (const T*)R, (T*)Y, (int)nt, K, diag);
+  static char name[64];
+  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d>>", type_name<T>(), C::N);
+  set_last_kernel(name);
+  return check_launch("dw_fc2_mx");
+}
+
+}  // namespace dwrw
 }  // namespace svk
 
 using namespace svk;
@@ -282,6 +521,8 @@ extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, co
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
     if (N == 512) return dwfc::launch<T, dwfc::Cfg<512, 7, 32>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
+    static const bool rw = !getenv("SVK_DWFC2_RW") || atoi(getenv("SVK_DWFC2_RW")) != 0;
+    if (rw) return dwrw::launch<T, dwrw::Cfg<320>>(H, taps, dbias, W2, b2, R, Y, B, K, st);
     return dwfc::launch<T, dwfc::Cfg<320, 14, 64>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
   });
 }

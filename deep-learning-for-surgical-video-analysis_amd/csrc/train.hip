@@ -242,31 +242,51 @@ __global__ __launch_bounds__(256) void colstats_part_kernel(const T* __restrict_
 }
 
 // out0[c] += sum_b ws[b][c], out1[c] += sum_b ws[nblk + b][c]; tot (optional) receives the two totals as well
-// ([2][C]).  Block = 64 columns x 4 lanes, lane rl sums partials rl, rl + 4, ... in order, the four lane sums
-// meet in LDS in a fixed order: the result does not depend on scheduling.
+// ([2][C]).  Block = 16 columns x 16 lanes; lane l owns partials l, l + 16, ... and keeps four accumulators
+// (partial index / 16 mod 4) so four loads are in flight, then the 16 x 4 lane sums meet in LDS in a fixed
+// tree order: the result does not depend on scheduling.  (Round 5 first had 64 columns x 4 lanes, one
+// accumulator: 256 dependent adds per lane at nblk = 1024, 37 us a launch in the train step.)
+constexpr int kFinCols = 16, kFinLanes = 16;
 __global__ __launch_bounds__(256) void colsum_final_kernel(const float* __restrict__ ws, int nblk, int C,
                                                            float* __restrict__ out0, float* __restrict__ out1,
                                                            float* __restrict__ tot) {
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int rl = threadIdx.x >> 6;
+  const int t = threadIdx.x % kFinCols, l = threadIdx.x / kFinCols;
+  const int c = blockIdx.x * kFinCols + t;
   const bool two = out1 || tot;
-  float a = 0.f, b = 0.f;
-  if (c < C)
-    for (int i = rl; i < nblk; i += 4) {
-      a += ws[(long)i * C + c];
-      if (two) b += ws[(long)(nblk + i) * C + c];
+  float a[4] = {0.f, 0.f, 0.f, 0.f}, b[4] = {0.f, 0.f, 0.f, 0.f};
+  if (c < C) {
+    int i = l;
+    for (; i + 3 * kFinLanes < nblk; i += 4 * kFinLanes) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += ws[(long)(i + u * kFinLanes) * C + c];
+      if (two)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) b[u] += ws[(long)(nblk + i + u * kFinLanes) * C + c];
     }
-  __shared__ float sa[4][64], sb[4][64];
-  sa[rl][threadIdx.x & 63] = a;
-  sb[rl][threadIdx.x & 63] = b;
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+      if (i + u * kFinLanes < nblk) {
+        a[u] += ws[(long)(i + u * kFinLanes) * C + c];
+        if (two) b[u] += ws[(long)(nblk + i + u * kFinLanes) * C + c];
+      }
+  }
+  __shared__ float sa[kFinLanes][kFinCols], sb[kFinLanes][kFinCols];
+  sa[l][t] = (a[0] + a[1]) + (a[2] + a[3]);
+  sb[l][t] = (b[0] + b[1]) + (b[2] + b[3]);
   __syncthreads();
-  if (rl == 0 && c < C) {
-    const int t = threadIdx.x & 63;
-    a = (sa[0][t] + sa[1][t]) + (sa[2][t] + sa[3][t]);
-    b = (sb[0][t] + sb[1][t]) + (sb[2][t] + sb[3][t]);
-    if (out0) out0[c] += a;
-    if (out1) out1[c] += b;
-    if (tot) { tot[c] = a; tot[C + c] = b; }
+#pragma unroll
+  for (int h = kFinLanes / 2; h >= 1; h >>= 1) {
+    if (l < h) {
+      sa[l][t] += sa[l + h][t];
+      sb[l][t] += sb[l + h][t];
+    }
+    __syncthreads();
+  }
+  if (l == 0 && c < C) {
+    const float x = sa[0][t], y = sb[0][t];
+    if (out0) out0[c] += x;
+    if (out1) out1[c] += y;
+    if (tot) { tot[c] = x; tot[C + c] = y; }
   }
 }
 
@@ -714,7 +734,7 @@ extern "C" int svk_colstats(int dtype, const void* X, long ldx, int M, int C, fl
   SVK_DISPATCH_DTYPE(dtype, T, {
     hipLaunchKernelGGL((colstats_part_kernel<T>), dim3(nb, (C + 63) / 64), dim3(256), 0, st, (const T*)X, ldx, M, C,
                        ws, sumsq ? 1 : 0);
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 63) / 64), dim3(256), 0, st, (const float*)ws, nb, C, sum,
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + kFinCols - 1) / kFinCols), dim3(256), 0, st, (const float*)ws, nb, C, sum,
                        sumsq, (float*)nullptr);
     return check_launch("colstats");
   });
@@ -746,7 +766,7 @@ extern "C" int svk_bn_bwd(int dtype, const void* X, const void* dY, const float*
     hipLaunchKernelGGL((bn_bwd_part_kernel<T>), dim3(nb, (C + 63) / 64), dim3(256), 0, st, (const T*)X, (const T*)dY,
                        sum, sumsq, gamma, beta, M, C, eps, relu, ws);
     // dbeta += sum dy', dgamma += sum dy'*xhat (exactly the two sums)
-    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + 63) / 64), dim3(256), 0, st, (const float*)ws, nb, C, dbeta,
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + kFinCols - 1) / kFinCols), dim3(256), 0, st, (const float*)ws, nb, C, dbeta,
                        dgamma, tot);
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T>), g1(n), dim3(256), 0, st, (const T*)X, (const T*)dY, sum, sumsq, gamma,
                        beta, (const float*)tot, (T*)dX, n, C, M, eps, relu);

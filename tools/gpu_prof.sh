@@ -25,6 +25,8 @@ cp $O/pmc_traffic.json $O/profiles_$R/pmc_traffic.json
 cp profiles/$R/pmc_mfma.json $O/pmc_mfma.json 2>/dev/null
 python tools/pmc_mfma.py $O/pmc_${W}_m/run_counter_collection.csv $O/pmc_mfma.json ${W}_${DT} 1 "${DOM:-gemm_pk<_Float16, PkCfg<128, 128}" "${DOMFLOP:-0}"
 cp $O/pmc_mfma.json $O/profiles_$R/pmc_mfma.json
+# this round's counters are the ones the bench line quotes (bench.py reads the newest profiles/rNN)
+mkdir -p profiles/$R && cp $O/pmc_traffic.json $O/pmc_mfma.json profiles/$R/
 mkdir -p $O/profiles_$R/pmc
 for p in f w m; do gzip -c $O/pmc_${W}_$p/run_counter_collection.csv > $O/profiles_$R/pmc/${W}_${DT}_$p.csv.gz; done
 step bench timeout -k 10 300 python bench.py --workload $W --dtype $DT --steps 20 --warmup 5 > $O/bench_${W}.log 2>&1
