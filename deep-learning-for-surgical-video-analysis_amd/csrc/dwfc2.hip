@@ -23,6 +23,7 @@
 // Numerics: the dwconv + GELU exactly as dwconv3x3_strip (f32 taps and accumulation, G rounded to 16 bits),
 // fc2 as the GEMM (f32 accumulation, bias then residual, one rounding).
 #include "svk_common.h"
+#include <type_traits>
 
 namespace svk {
 namespace dwfc {
@@ -294,14 +295,79 @@ struct Cfg {
   static constexpr int GBYTES = R * 16 * 128;          // 8 KiB
   static constexpr int H_OFF = 0, G_OFF = NHB * HBYTES, LDS = G_OFF + 2 * GBYTES;
   static constexpr int TILES_PER_FRAME = (WI + R - 1) / R;
+  // packed operands per K-step (svk_mixffn_dw_fc2_pack): A part [4 waves][6][64 lanes] x 16 B (5 dwconv A
+  // fragments + the lane's 4 dwconv biases), then W2 part [2 ks][4 waves][WNB][64 lanes] x 16 B (fc2 A
+  // fragments): every load of the K loop is one contiguous 1 KiB wave-instruction
+  static constexpr int APK = 4 * 6 * 64 * 16, WPK = 2 * 4 * WNB * 64 * 16, PK = APK + WPK;
   static_assert(N % 64 == 0 && HBLK == 12, "shape");
 };
 
+// packed operands: one thread per 16-byte chunk (A part, then W2 part, K-step-major)
 template <typename T, class C>
-__global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, const float* __restrict__ taps,
-                                                 const float* __restrict__ dbias, const T* __restrict__ W2,
+__global__ __launch_bounds__(256) void dwfc2_pack(const float* __restrict__ taps, const float* __restrict__ dbias,
+                                                  const T* __restrict__ W2, int K, uint4* __restrict__ out) {
+  const int nk = K / C::BK;
+  const long id = (long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= (long)nk * (C::PK / 16)) return;
+  const int kt = (int)(id / (C::PK / 16)), r = (int)(id % (C::PK / 16));
+  const int lane = r % 64, fr = lane & 15, fq = lane >> 4;
+  if (r < C::APK / 16) {
+    const int j = (r / 64) % 6, w = r / (64 * 6);
+    if (j == 5) {                                      // dwconv bias of channels 16 w + 4 fq .. + 3
+      const float* d = dbias + kt * 64 + 16 * w + 4 * fq;
+      out[id] = uint4{__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3])};
+      return;
+    }
+    // A fragment kk = j: row = channel 16 w + fr, k-slot 8 fq + e = (tap 2 kk + (fq >> 1), channel 8 (fq & 1) + e
+    // of the block): tap[t][16 w + fr] where 8 (fq & 1) + e == fr, 0 elsewhere (and for the padding tap t = 9)
+    const int t = 2 * j + (fq >> 1), e = fr - 8 * (fq & 1);
+    T v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = from_f<T>(0.f);
+    if (t < 9 && e >= 0 && e < 8) v[e] = from_f<T>(taps[(long)t * K + kt * 64 + 16 * w + fr]);
+    out[id] = *reinterpret_cast<const uint4*>(v);
+  } else {
+    const int rr = r - C::APK / 16, nb = (rr / 64) % C::WNB, w = (rr / (64 * C::WNB)) % 4, ks = rr / (64 * C::WNB * 4);
+    out[id] = *reinterpret_cast<const uint4*>(W2 + (long)(w * (C::N / 4) + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
+  }
+}
+
+// gelu_rl on four values in lockstep: each step is four independent instructions, so the dependent-issue
+// latency of the chain (rcp -> polynomial -> exp -> fma, ~10 deep) is covered inside the wave; hipcc, short
+// of registers, otherwise emits one element's whole chain at a time (issue stalls: SQ_WAIT_INST_ANY was 34 %)
+__device__ __forceinline__ f32x4 gelu4(f32x4 x) {
+  f32x4 ax, t, q, e, r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ax[i] = fabsf(x[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t[i] = fmaf(0.3275911f * 0.70710678118654752f, ax[i], 1.0f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t[i] = __builtin_amdgcn_rcpf(t[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = x[i] * x[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = fmaf(-0.5f * 1.061405429f, t[i], -0.5f * -1.453152027f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = e[i] * -0.72134752044448170f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = fmaf(q[i], t[i], -0.5f * 1.421413741f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = fmaf(q[i], t[i], -0.5f * -0.284496736f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = fmaf(q[i], t[i], -0.5f * 0.254829592f);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = ax[i] * t[i] * q[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r[i] = fmaf(r[i], e[i], fmaxf(x[i], 0.f));
+  return r;
+}
+
+template <typename T, class C>
+__global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, const char* __restrict__ pk,
                                                  const float* __restrict__ b2, const T* __restrict__ R,
-                                                 T* __restrict__ Y, int ntiles, int K, int diag) {
+                                                 T* __restrict__ Y, int ntiles, int K) {
   typedef v8_t<T> tx8;
   constexpr int WI = C::WI, WNB = C::WNB, RR = C::R;
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
@@ -344,39 +410,27 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
     const int sl = min(max(fr + dx - 1, 0), 15), c = 2 * wave + (fq & 1);
     hoff[kk] = (dy * 16 + sl) * 128 + ((c ^ (sl & 7)) << 4);
   }
-  // A fragment kk: row = channel fr of the block, k = 8 fq .. 8 fq + 7 = (tap 2 kk + (fq >> 1), channels
-  // 8 (fq & 1) .. + 7): one non-zero, tap[t][16 w + fr], at k-slot j = fr - 8 (fq & 1) when 0 <= j < 8
-  const int jsl = fr - 8 * (fq & 1);
-  const bool aon = jsl >= 0 && jsl < 8;
-  uint32_t amask[4];
-#pragma unroll
-  for (int d = 0; d < 4; ++d) amask[d] = (aon && (jsl >> 1) == d) ? ~0u : 0u;
-  const int ash = (jsl & 1) * 16;
-  float tv[5];
-  float4 dbv;
-  auto load_taps = [&](int kt) {
-#pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const int t = min(2 * kk + (fq >> 1), 8);
-      tv[kk] = taps[(long)t * K + kt * 64 + 16 * wave + fr];
-    }
-    dbv = *reinterpret_cast<const float4*>(dbias + kt * 64 + 16 * wave + 4 * fq);
-  };
+  // dwconv A fragments (one non-zero each, built by dwfc2_pack) and the lane's dwconv biases, one K-step
+  // at a time: loaded right after dwconv(k) has read them, for dwconv(k + 1) one iteration later
   tx8 afr[5];
-  auto build_a = [&]() {
+  f32x4 dbv;
+  const char* pkl = pk + lane * 16;
+  auto load_a = [&](int kt) {
+    const char* src = pkl + (long)kt * C::PK + wave * 6 * 1024;
 #pragma unroll
-    for (int kk = 0; kk < 5; ++kk) {
-      const T tt = from_f<T>(2 * kk + (fq >> 1) < 9 ? tv[kk] : 0.f);
-      const uint32_t v = (uint32_t)__builtin_bit_cast(uint16_t, tt) << ash;
-      const uint4 u = {v & amask[0], v & amask[1], v & amask[2], v & amask[3]};
-      afr[kk] = __builtin_bit_cast(tx8, u);
-    }
+    for (int kk = 0; kk < 5; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(afr[kk]) : "v"(src + kk * 1024) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dbv) : "v"(src + 5 * 1024) : "memory");
+  };
+  auto tie_a = [&]() {
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) asm volatile("" : "+v"(afr[kk]));
+    asm volatile("" : "+v"(dbv));
   };
   f32x4 dacc[RR];
   auto dwconv = [&](int hb) {
     const char* hs = smem + C::H_OFF + hb * C::HBYTES;
 #pragma unroll
-    for (int mb = 0; mb < RR; ++mb) dacc[mb] = f32x4{dbv.x, dbv.y, dbv.z, dbv.w};
+    for (int mb = 0; mb < RR; ++mb) dacc[mb] = dbv;
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk)
 #pragma unroll
@@ -387,9 +441,8 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
   auto gelu_store = [&](int gb) {
 #pragma unroll
     for (int mb = 0; mb < RR; ++mb) {
-      T o[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = from_f<T>((diag & 2) ? dacc[mb][r] : dwfc::gelu_rl(dacc[mb][r]));
+      const f32x4 gv = gelu4(dacc[mb]);
+      const T o[4] = {from_f<T>(gv[0]), from_f<T>(gv[1]), from_f<T>(gv[2]), from_f<T>(gv[3])};
       const int s = mb * 16 + fr, cw = 16 * wave + 4 * fq;
       *reinterpret_cast<uint2*>(smem + C::G_OFF + gb * C::GBYTES + s * 128 + ((((cw >> 3) ^ (s & 7)) << 4) | ((cw & 4) << 1))) =
           *reinterpret_cast<const uint2*>(o);
@@ -400,10 +453,16 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
   const int n0w = wave * (C::N / 4);
   tx8 w2f[2][WNB];
   auto load_w2 = [&](int kt, int ks) {
-    if ((diag & 1) && kt > 0) kt = 0;                  // timing ablation: W2 of K-step 0 only (L1-resident)
+    const char* src = pkl + (long)kt * C::PK + C::APK + (ks * 4 + wave) * WNB * 1024;
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb)
-      w2f[ks][nb] = *reinterpret_cast<const tx8*>(W2 + (long)(n0w + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(w2f[ks][nb]) : "v"(src + nb * 1024) : "memory");
+  };
+  auto tie_w2 = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < WNB; ++nb) asm volatile("" : "+v"(w2f[ks][nb]));
   };
   f32x4 acc[RR][WNB];
 #pragma unroll
@@ -421,34 +480,38 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
     }
   };
 
-  // ---- prologue: H(0..2) in the ring, G(0), taps(1), W2(0)
-  load_taps(0);
+  // ---- prologue: H(0..2) in the ring, A(0) -> G(0), A(1), W2(0)
+  load_a(0);
   dma_h(0, 0);
   dma_h(min(1, nk - 1), 1);
   dma_h(min(2, nk - 1), 2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tie_a();
   __syncthreads();
-  build_a();
   dwconv(0);
   gelu_store(0);
-  load_taps(min(1, nk - 1));
+  load_a(min(1, nk - 1));
   load_w2(0, 0);
   load_w2(0, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tie_a();
+  tie_w2();
   __syncthreads();
-  // iteration kt < nk - 1: dwconv(kt + 1) || fc2(kt), GELU(kt + 1) -> G ring, taps(kt + 2), DMA H(kt + 3)
+  // iteration kt < nk - 1: dwconv(kt + 1), then A(kt + 2) into the registers it read; fc2(kt) with W2(kt + 1)
+  // loaded behind each half; GELU(kt + 1) -> G ring; DMA H(kt + 3) into the slot dwconv(kt) read (before the
+  // previous barrier; clamped past the end: never read); the counted wait leaves only that DMA in flight
   for (int kt = 0; kt + 1 < nk; ++kt) {
-    build_a();                                         // taps(kt + 1), loaded one iteration ago
     dwconv((kt + 1) % 3);
+    load_a(min(kt + 2, nk - 1));
     fc2_half(kt & 1, 0);
     load_w2(kt + 1, 0);
     fc2_half(kt & 1, 1);
     load_w2(kt + 1, 1);
     gelu_store((kt + 1) & 1);
-    load_taps(min(kt + 2, nk - 1));
-    // H(kt + 3) into the slot dwconv(kt) read (before the previous barrier); clamped past the end (never read)
-    dma_h((diag & 4) ? 0 : min(kt + 3, nk - 1), kt % 3);   // diag 4: timing ablation, H of K-step 0 only
-    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // all but this DMA: H(kt + 2), W2(kt + 1), taps(kt + 2)
+    dma_h(min(kt + 3, nk - 1), kt % 3);
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // A(kt + 2) [6], W2(kt + 1) [2 WNB] retired; DMA [3] not
+    tie_a();
+    tie_w2();
     __syncthreads();
   }
   fc2_half((nk - 1) & 1, 0);
@@ -478,17 +541,23 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
 }
 
 template <typename T, class C>
-static int launch(const void* H, const float* taps, const float* db, const void* W2, const float* b2, const void* R,
-                  void* Y, int B, int K, hipStream_t st) {
-  static const int diag = getenv("SVK_DWFC2_DIAG") ? atoi(getenv("SVK_DWFC2_DIAG")) : 0;   // timing ablations only
+static int launch(const void* H, const void* pk, const float* b2, const void* R, void* Y, int B, int K, hipStream_t st) {
   const long nt = (long)B * C::TILES_PER_FRAME;
   if (nt > 0x7fffffffL || (long)B * C::WI * C::WI * K > 0x7fffffffL) return SVK_EUNSUPPORTED;
-  hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), 0, st, (const T*)H, taps, db, (const T*)W2, b2,
-                     (const T*)R, (T*)Y, (int)nt, K, diag);
+  hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), 0, st, (const T*)H, (const char*)pk, b2,
+                     (const T*)R, (T*)Y, (int)nt, K);
   static char name[64];
   if (!name[0]) snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d>>", type_name<T>(), C::N);
   set_last_kernel(name);
   return check_launch("dw_fc2_mx");
+}
+
+template <typename T, class C>
+static int pack(const float* taps, const float* db, const void* W2, int K, void* out, hipStream_t st) {
+  const long n = (long)(K / C::BK) * (C::PK / 16);
+  hipLaunchKernelGGL((dwfc2_pack<T, C>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, taps, db, (const T*)W2, K,
+                     (uint4*)out);
+  return check_launch("dw_fc2_pack");
 }
 
 }  // namespace dwrw
@@ -521,8 +590,39 @@ extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, co
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
     if (N == 512) return dwfc::launch<T, dwfc::Cfg<512, 7, 32>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
-    static const bool rw = !getenv("SVK_DWFC2_RW") || atoi(getenv("SVK_DWFC2_RW")) != 0;
-    if (rw) return dwrw::launch<T, dwrw::Cfg<320>>(H, taps, dbias, W2, b2, R, Y, B, K, st);
     return dwfc::launch<T, dwfc::Cfg<320, 14, 64>>(H, taps, dbias, W2, b2, R, Y, (int)M, K, st);
   });
+}
+
+// ---- the stage-3 form with the depthwise conv on MFMA: operands packed once per weight set -------------
+extern "C" long svk_mixffn_dw_fc2_packed_bytes(int dtype, int W, int N, int K) {
+  if (!(dtype == SVK_F16 || dtype == SVK_BF16) || W != 14 || N != 320 || K % 64 || K <= 0) return 0;
+  return (long)(K / 64) * dwrw::Cfg<320>::PK;
+}
+
+extern "C" int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float* dbias, const void* W2, int W, int N,
+                                      int K, void* packed, void* stream) {
+  if (!taps || !dbias || !W2 || !packed) { set_error("svk_mixffn_dw_fc2_pack: bad args"); return SVK_EINVAL; }
+  if (svk_mixffn_dw_fc2_packed_bytes(dtype, W, N, K) == 0) {
+    set_error("svk_mixffn_dw_fc2_pack: (dtype=%d, W=%d, N=%d, K=%d) has no packed form", dtype, W, N, K);
+    return SVK_EUNSUPPORTED;
+  }
+  if ((((uintptr_t)packed) | ((uintptr_t)W2)) & 15) { set_error("svk_mixffn_dw_fc2_pack: misaligned operand"); return SVK_EINVAL; }
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_H16(dtype, T, { return dwrw::pack<T, dwrw::Cfg<320>>(taps, dbias, W2, K, packed, st); });
+}
+
+extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const float* b2, const void* R,
+                                        void* Y, int B, int Himg, int Wimg, int K, int N, void* stream) {
+  if (B < 0 || Himg <= 0 || Wimg <= 0 || !H || !packed || !b2 || !Y) { set_error("svk_mixffn_dw_fc2_packed: bad args"); return SVK_EINVAL; }
+  if (Himg != Wimg || svk_mixffn_dw_fc2_packed_bytes(dtype, Wimg, N, K) == 0) {
+    set_error("svk_mixffn_dw_fc2_packed: (dtype=%d, %dx%d, N=%d, K=%d) has no packed form", dtype, Himg, Wimg, N, K);
+    return SVK_EUNSUPPORTED;
+  }
+  if ((((uintptr_t)H) | ((uintptr_t)packed) | ((uintptr_t)b2)) & 15 || (((uintptr_t)Y) | ((uintptr_t)R)) & 7) {
+    set_error("svk_mixffn_dw_fc2_packed: misaligned operand"); return SVK_EINVAL;
+  }
+  if (B == 0) return SVK_OK;
+  hipStream_t st = (hipStream_t)stream;
+  SVK_DISPATCH_H16(dtype, T, { return dwrw::launch<T, dwrw::Cfg<320>>(H, packed, b2, R, Y, B, K, st); });
 }

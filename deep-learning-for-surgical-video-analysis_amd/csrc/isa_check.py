@@ -15,7 +15,10 @@
    last K-step.  hipcc treats the destination VGPRs as written when the asm statement ends, so any
    compiler instruction touching them before that wait would read or clobber in-flight data.  Every
    VGPR-destination global_load in a gemm_pk kernel is followed, on EVERY control-flow path, by an
-   s_waitcnt with a vmcnt field before any instruction reads or writes its destination registers.
+   s_waitcnt with a vmcnt field before any instruction reads or writes its destination registers.  The same
+   holds for dwfc2_rw (round 5: its K-loop W2 / tap loads are asm too; a runtime index into a double
+   buffer of such registers once made hipcc copy them right after the load, the copy read in-flight data
+   and a reused address register was overwritten by the returning load — the GPU hung).
 Exit status 1 with a report on any violation."""
 import os
 import re
@@ -89,6 +92,7 @@ def check_packed(funcs):
 
 
 VMEM_RE = re.compile(r"(global_|buffer_|flat_|scratch_)")
+ASM_LOAD_KERNELS = ("gemm_pk", "dwfc2_rw")          # kernels whose global loads are issued from inline asm
 VMCNT_RE = re.compile(r"vmcnt\((\d+)\)")
 
 
@@ -99,7 +103,7 @@ def check_epilogue_loads(funcs):
     destination registers."""
     bad = []
     for f, ins in funcs.items():
-        if "gemm_pk" not in f:
+        if not any(t in f for t in ASM_LOAD_KERNELS):
             continue
         at = {a: k for k, (a, *_rest) in enumerate(ins)}
         for k, (addr, op, ops, _) in enumerate(ins):
@@ -151,7 +155,7 @@ def check_scratch(notes):
         if m:
             cur = m.group(1)
         m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count):\s+(\d+)", line)
-        if m and int(m.group(2)) > 0 and cur and ("gemm_pk" in cur or "gemm_pp" in cur):
+        if m and int(m.group(2)) > 0 and cur and any(t in cur for t in ASM_LOAD_KERNELS + ("gemm_pp",)):
             bad.append(f"{cur}: .{m.group(1)} {m.group(2)}")
     return bad
 
@@ -171,9 +175,10 @@ def main(objs):
         for msg in check_epilogue_loads(funcs):
             print(f"isa_check: {os.path.basename(obj)}: epilogue load register touched before its wait: {msg}")
             fails += 1
-        nload += sum(1 for f, ins in funcs.items() if "gemm_pk" in f for _, op, _, _ in ins
+        nload += sum(1 for f, ins in funcs.items() if any(t in f for t in ASM_LOAD_KERNELS) for _, op, _, _ in ins
                      if re.match(r"global_load_dword(x2|x4)?$", op))
-    print(f"isa_check: {len(objs)} objects, {nload} gemm_pk epilogue loads audited, {fails} violation(s)")
+    print(f"isa_check: {len(objs)} objects, {nload} asm-load kernel loads audited ({', '.join(ASM_LOAD_KERNELS)}), "
+          f"{fails} violation(s)")
     return 1 if fails else 0
 
 

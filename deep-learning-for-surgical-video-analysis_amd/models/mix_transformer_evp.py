@@ -72,7 +72,13 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def _pack(self, dt):
-        return dict(w1=lin_w(self.fc1, dt), b1=lin_b(self.fc1), w2=lin_w(self.fc2, dt), b2=lin_b(self.fc2))
+        p = dict(w1=lin_w(self.fc1, dt), b1=lin_b(self.fc1), w2=lin_w(self.fc2, dt), b2=lin_b(self.fc2))
+        if dt in ops.H16 and ops.DWFC2_MX and p["w2"].is_cuda:
+            # the stage-3 back half on the matrix cores (svk_mixffn_dw_fc2_packed): its operands packed once;
+            # None for the widths / shapes without that form
+            pd = self.dwconv._pack(dt)
+            p["dwfc_pk"] = ops.mixffn_dw_fc2_pack(pd["taps"], pd["b"], p["w2"], 14)
+        return p
 
     def forward(self, x, H, W, residual=None, ln=None):
         """``ln = (gamma, beta, eps)``: return LayerNorm(residual + mlp(x)) (the stage norm that follows the
@@ -101,12 +107,14 @@ class Mlp(nn.Module):
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")
             y = ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
-        elif (ops.DW_FC2 and x.dtype in ops.H16 and H == W and residual is not None
-              and ops.mixffn_dw_fc2_supported(x.dtype, W, self.fc2.out_features, hid)):
+        elif (x.dtype in ops.H16 and H == W and residual is not None
+              and ((W == 14 and p.get("dwfc_pk") is not None)
+                   or (ops.DW_FC2 and ops.mixffn_dw_fc2_supported(x.dtype, W, self.fc2.out_features, hid)))):
             # fc1 GEMM, then DWConv + GELU fused into fc2 (the GELU map never leaves the chip)
             h = ops.gemm(x, p["w1"], p["b1"])
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
-            y = ops.mixffn_dw_fc2(h.view(B, H, W, hid), pd["taps"], pd["b"], p["w2"], p["b2"], residual=residual)
+            y = ops.mixffn_dw_fc2(h.view(B, H, W, hid), pd["taps"], pd["b"], p["w2"], p["b2"], residual=residual,
+                                  packed=p.get("dwfc_pk") if W == 14 else None)
         else:
             h = ops.gemm(x, p["w1"], p["b1"])
             h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)

@@ -375,6 +375,7 @@ MIXFFN_RW = os.environ.get("SVK_MIXFFN_RW", "1") == "1"
 # 137.8 vs 99.6 us at B = 256, profiles/r04/dwfc2_bench.log): the per-tap LDS reads and masks of the G
 # production are latency-bound at 2 waves per SIMD
 DW_FC2 = os.environ.get("SVK_DW_FC2", "0") == "1"
+DWFC2_MX = os.environ.get("SVK_DWFC2_MX", "1") == "1"
 
 
 def mixffn_dw_fc2_supported(dtype, W, N, K):
@@ -382,10 +383,29 @@ def mixffn_dw_fc2_supported(dtype, W, N, K):
     return dtype in H16 and bool(_lib.load().svk_mixffn_dw_fc2_supported(dtype_code(dtype), int(W), int(N), int(K)))
 
 
-def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None):
+def mixffn_dw_fc2_pack(taps, dbias, w2, W):
+    """The packed operand buffer of the matrix-core stage-3 form (svk_mixffn_dw_fc2_pack), or None where the
+    map has no packed form.  Pack once per weight set (Mlp._pack does) and pass it to mixffn_dw_fc2."""
+    N, K = w2.shape
+    nbytes = _lib.load().svk_mixffn_dw_fc2_packed_bytes(dtype_code(w2.dtype), int(W), int(N), int(K))
+    if nbytes <= 0:
+        return None
+    for t, nm in ((taps, "taps"), (dbias, "dbias")):
+        _chk(t, nm, torch.float32)
+    _chk(w2, "w2")
+    if taps.shape != (9, K) or dbias.numel() != K or not (taps.is_contiguous() and w2.is_contiguous()):
+        raise _lib.SvkError("svk.mixffn_dw_fc2_pack: taps [9, K] / dbias [K] / w2 [N, K] contiguous")
+    out = torch.empty(nbytes, device=w2.device, dtype=torch.uint8)
+    _lib.call("svk_mixffn_dw_fc2_pack", dtype_code(w2.dtype), _p(taps), _p(dbias), _p(w2), int(W), int(N), int(K),
+              _p(out), _stream())
+    return out
+
+
+def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None):
     """fc2(GELU(dwconv3x3(h) + dbias)) + b2 (+ residual) with the GELU map kept on chip (svk_mixffn_dw_fc2):
     h [B, H, W, K] fc1 output (16-bit NHWC), taps [9, K] / dbias [K] f32 as DWConv packs them, w2 [N, K];
-    returns [B, H * W, N]."""
+    returns [B, H * W, N].  Where the map has the matrix-core form (stage 3: 14 x 14, N = 320) it runs that,
+    from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form."""
     if h.dtype not in H16:
         raise _lib.SvkError("svk.mixffn_dw_fc2: bf16 / f16 only")
     _chk(h, "h"); _chk(w2, "w2", h.dtype); _chk(residual, "residual", h.dtype)
@@ -401,9 +421,15 @@ def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None):
     if residual is not None and (residual.numel() != B * H * W * N or not residual.is_contiguous()):
         raise _lib.SvkError("svk.mixffn_dw_fc2: residual must be a contiguous [B, H*W, N] map")
     out = torch.empty(B, H * W, N, device=h.device, dtype=h.dtype)
+    if DWFC2_MX and packed is None:
+        packed = mixffn_dw_fc2_pack(taps, dbias, w2, W)
     t0 = _prof_begin()
-    _lib.call("svk_mixffn_dw_fc2", dtype_code(h.dtype), _p(h), _p(taps), _p(dbias), _p(w2), _p(b2), _p(residual),
-              _p(out), B, H, W, K, N, _stream())
+    if DWFC2_MX and packed is not None:
+        _lib.call("svk_mixffn_dw_fc2_packed", dtype_code(h.dtype), _p(h), _p(packed), _p(b2), _p(residual), _p(out),
+                  B, H, W, K, N, _stream())
+    else:
+        _lib.call("svk_mixffn_dw_fc2", dtype_code(h.dtype), _p(h), _p(taps), _p(dbias), _p(w2), _p(b2), _p(residual),
+                  _p(out), B, H, W, K, N, _stream())
     if t0 is not None:
         M = B * H * W
         _prof_end(t0, _last_kernel(), 2.0 * M * N * K + 2.0 * 9 * M * K,

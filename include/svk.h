@@ -145,6 +145,19 @@ int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K);
 int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2, const float* b2,
                       const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, void* stream);
 
+/* The stage-3 shape (14 x 14, N = 320, K % 64 == 0, 16-bit) with the depthwise conv on the matrix cores
+ * (csrc/dwfc2.hip, dwrw): the operands are packed once per weight set — svk_mixffn_dw_fc2_pack writes
+ * svk_mixffn_dw_fc2_packed_bytes(...) bytes (16-byte aligned): per 64-channel K-step the dwconv A fragments
+ * (taps rounded to the 16-bit type, block-diagonal), the dwconv biases and the W2 fragments, in load order —
+ * then svk_mixffn_dw_fc2_packed computes Y = GELU(dwconv3x3(H) + dbias) W2^T + b2 (+ R) from H and the packed
+ * buffer (same H / b2 / R / Y contract as svk_mixffn_dw_fc2).  packed_bytes is 0 where there is no packed form;
+ * the other two return SVK_EUNSUPPORTED there. */
+long svk_mixffn_dw_fc2_packed_bytes(int dtype, int W, int N, int K);
+int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float* dbias, const void* W2, int W, int N, int K,
+                           void* packed, void* stream);
+int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const float* b2, const void* R, void* Y,
+                             int B, int Himg, int Wimg, int K, int N, void* stream);
+
 /* MixFFN front half, G = act(dwconv3x3(XN W1^T + b1) + dbias) over NHWC maps (Mlp.fc1 -> DWConv -> GELU,
  * mix_transformer_evp.py:60-63, 24-30): the 4C-wide hidden map stays on chip (fc1 recomputed on one
  * halo row above / below each strip).  bf16, C in {32, 64, 128}, hidden % 64 == 0; W1 [hidden][C] bf16,

@@ -221,12 +221,16 @@ def test_conv2d_s2d_ln(cuda, dt, B, HB, CS, ln, C):
 
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,res", [(3, True), (1, False), (5, True)])
-@pytest.mark.parametrize("W,K,N", [(14, 1280, 320), (7, 2048, 512)])
-def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N):
+@pytest.mark.parametrize("W,K,N,mx", [(14, 1280, 320, True), (14, 1280, 320, False), (7, 2048, 512, False),
+                                      (14, 640, 320, True)])
+def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N, mx, monkeypatch):
     """dwconv3x3 + GELU fused into fc2 (svk_mixffn_dw_fc2; the stage-3 / stage-4 shapes 14 x 14, 1280 -> 320 and
-    7 x 7, 2048 -> 512) against the unfused svk path (dwconv3x3 + gemm: same roundings, expected within a few
-    16-bit ulps) and fp64.  Token counts that are not a multiple of the 64 / 32-token tile (masked rows)."""
+    7 x 7, 2048 -> 512; mx: the stage-3 form with the depthwise conv on MFMA from packed operands,
+    svk_mixffn_dw_fc2_packed, also at a shorter K) against the unfused svk path (dwconv3x3 + gemm: same
+    roundings but for the mx form's 16-bit taps, expected within a few 16-bit ulps) and fp64.  Token counts
+    that are not a multiple of the 64 / 32-token tile (masked rows)."""
     from svk import ops
+    monkeypatch.setattr(ops, "DWFC2_MX", mx)
     h = _rand(B, W, W, K, dt=dt, dev=cuda, seed=71)
     taps = _rand(9, K, dt=torch.float32, dev=cuda, scale=0.3, seed=72)
     db = _rand(K, dt=torch.float32, dev=cuda, scale=0.1, seed=73)
@@ -234,7 +238,10 @@ def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N):
     b2 = _rand(N, dt=torch.float32, dev=cuda, seed=75)
     r = _rand(B, W * W, N, dt=dt, dev=cuda, seed=76) if res else None
     got = ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r)
-    assert ops._last_kernel().startswith("dw_fc2"), ops._last_kernel()
+    assert ops._last_kernel().startswith("dw_fc2_mx" if mx else "dw_fc2<"), ops._last_kernel()
+    if mx:   # the pre-packed call gives the same bits
+        pk = ops.mixffn_dw_fc2_pack(taps, db, w2, W)
+        assert torch.equal(ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r, packed=pk), got)
     g = ops.dwconv3x3(h, taps, db, act="gelu")
     ref16 = ops.gemm(g.view(B, W * W, K), w2, b2, residual=r)
     d = (got.float() - ref16.float()).abs().max().item()

@@ -23,7 +23,8 @@ def main():
         w2 = (torch.randn(N, K, device=dev) * K ** -0.5).to(dt)
         b2 = torch.randn(N, device=dev)
         r = torch.randn(B, W * W, N, device=dev).to(dt)
-        f = lambda: ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r)
+        pk = ops.mixffn_dw_fc2_pack(taps, db, w2, W)
+        f = lambda: ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r, packed=pk)
         u = lambda: ops.gemm(ops.dwconv3x3(h, taps, db, act="gelu").view(B, W * W, K), w2, b2, residual=r)
         d = (f().float() - u().float()).abs().max().item()
         tf, tu = timeit(f, 20), timeit(u, 20)
