@@ -285,21 +285,28 @@ static int launch(const void* H, const float* taps, const float* db, const void*
 // f32 from the bias, gelu_rl, G rounded to 16 bits; fc2 as the GEMM (f32, + b2, + residual, one rounding).
 namespace dwrw {
 
-template <int N_>
+// Geometry.  A tile = (frame, R image rows) x all N outputs, 64 token slots = 4 MFMA m-blocks of 16.  The H
+// tile in LDS holds rows y0 - 1 .. in SW-slot rows: slot 0 is the conv's left zero padding and slot s the
+// pixel s - 1; the right padding is slot W + 1 when SW = W + 2 (14 x 14: SW = 16, one image row per m-block)
+// or the NEXT row's slot 0 when SW = W + 1 (7 x 7: SW = 8, two image rows per m-block; one extra zero row
+// below).  Token slot t <-> image row y0 + t / SW, slot t % SW.  Waves: NW = 4 (N = 320, 5 fc2 n-blocks
+// each) or 8 (N = 512, 4 each, one workgroup per CU); the dwconv of channel block cb = w % 4 of the K-step for
+// 16 / NW m-blocks per wave.
+template <int N_, int WI_>
 struct Cfg {
-  static constexpr int N = N_, WI = 14, R = 4, NT = 256, BK = 64;
-  static constexpr int WNB = N / 64;                   // 16-column n-blocks per wave (fc2)
-  static constexpr int HROWS = R + 2, NHB = 3;
-  static constexpr int HBYTES = HROWS * 16 * 128;      // 12 KiB: 6 rows x 16 slots x 64 channels (16-bit)
-  static constexpr int HBLK = HBYTES / 1024;           // 1 KiB DMA blocks (12: 3 per wave)
-  static constexpr int GBYTES = R * 16 * 128;          // 8 KiB
+  static constexpr int N = N_, WI = WI_, BK = 64;
+  static constexpr int SW = WI <= 7 ? 8 : 16, MBR = 16 / SW, R = 4 * MBR, XROW = SW == WI + 1 ? 1 : 0;
+  static constexpr int NW = N == 512 ? 8 : 4, NT = 64 * NW, WNB = N / (16 * NW), MPW = 16 / NW;
+  static constexpr int HROWS = R + 2 + XROW, HCH = HROWS * SW * 8;
+  static constexpr int DPW = (HCH + 64 * NW - 1) / (64 * NW);   // DMA wave-instructions per wave per K-step
+  static constexpr int HBYTES = DPW * NW * 1024, NHB = 3, GBYTES = 64 * 128;
   static constexpr int H_OFF = 0, G_OFF = NHB * HBYTES, LDS = G_OFF + 2 * GBYTES;
   static constexpr int TILES_PER_FRAME = (WI + R - 1) / R;
-  // packed operands per K-step (svk_mixffn_dw_fc2_pack): A part [4 waves][6][64 lanes] x 16 B (5 dwconv A
-  // fragments + the lane's 4 dwconv biases), then W2 part [2 ks][4 waves][WNB][64 lanes] x 16 B (fc2 A
+  // packed operands per K-step (svk_mixffn_dw_fc2_pack): A part [4 channel blocks][6][64 lanes] x 16 B (5 dwconv
+  // A fragments + the lane's 4 dwconv biases), then W2 part [2 ks][NW waves][WNB][64 lanes] x 16 B (fc2 A
   // fragments): every load of the K loop is one contiguous 1 KiB wave-instruction
-  static constexpr int APK = 4 * 6 * 64 * 16, WPK = 2 * 4 * WNB * 64 * 16, PK = APK + WPK;
-  static_assert(N % 64 == 0 && HBLK == 12, "shape");
+  static constexpr int APK = 4 * 6 * 64 * 16, WPK = 2 * NW * WNB * 64 * 16, PK = APK + WPK;
+  static_assert(N % (16 * NW) == 0 && SW * MBR == 16 && SW % 8 == 0 && HROWS * SW * 128 <= HBYTES, "shape");
 };
 
 // packed operands: one thread per 16-byte chunk (A part, then W2 part, K-step-major)
@@ -312,29 +319,29 @@ __global__ __launch_bounds__(256) void dwfc2_pack(const float* __restrict__ taps
   const int kt = (int)(id / (C::PK / 16)), r = (int)(id % (C::PK / 16));
   const int lane = r % 64, fr = lane & 15, fq = lane >> 4;
   if (r < C::APK / 16) {
-    const int j = (r / 64) % 6, w = r / (64 * 6);
-    if (j == 5) {                                      // dwconv bias of channels 16 w + 4 fq .. + 3
-      const float* d = dbias + kt * 64 + 16 * w + 4 * fq;
+    const int j = (r / 64) % 6, cb = r / (64 * 6);
+    if (j == 5) {                                      // dwconv bias of channels 16 cb + 4 fq .. + 3
+      const float* d = dbias + kt * 64 + 16 * cb + 4 * fq;
       out[id] = uint4{__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3])};
       return;
     }
-    // A fragment kk = j: row = channel 16 w + fr, k-slot 8 fq + e = (tap 2 kk + (fq >> 1), channel 8 (fq & 1) + e
-    // of the block): tap[t][16 w + fr] where 8 (fq & 1) + e == fr, 0 elsewhere (and for the padding tap t = 9)
+    // A fragment kk = j: row = channel 16 cb + fr, k-slot 8 fq + e = (tap 2 kk + (fq >> 1), channel 8 (fq & 1) + e
+    // of the block): tap[t][16 cb + fr] where 8 (fq & 1) + e == fr, 0 elsewhere (and for the padding tap t = 9)
     const int t = 2 * j + (fq >> 1), e = fr - 8 * (fq & 1);
     T v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = from_f<T>(0.f);
-    if (t < 9 && e >= 0 && e < 8) v[e] = from_f<T>(taps[(long)t * K + kt * 64 + 16 * w + fr]);
+    if (t < 9 && e >= 0 && e < 8) v[e] = from_f<T>(taps[(long)t * K + kt * 64 + 16 * cb + fr]);
     out[id] = *reinterpret_cast<const uint4*>(v);
   } else {
-    const int rr = r - C::APK / 16, nb = (rr / 64) % C::WNB, w = (rr / (64 * C::WNB)) % 4, ks = rr / (64 * C::WNB * 4);
-    out[id] = *reinterpret_cast<const uint4*>(W2 + (long)(w * (C::N / 4) + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
+    const int rr = r - C::APK / 16, nb = (rr / 64) % C::WNB, w = (rr / (64 * C::WNB)) % C::NW;
+    const int ks = rr / (64 * C::WNB * C::NW);
+    out[id] = *reinterpret_cast<const uint4*>(W2 + (long)(w * (C::N / C::NW) + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
   }
 }
 
-// gelu_rl on four values in lockstep: each step is four independent instructions, so the dependent-issue
-// latency of the chain (rcp -> polynomial -> exp -> fma, ~10 deep) is covered inside the wave; hipcc, short
-// of registers, otherwise emits one element's whole chain at a time (issue stalls: SQ_WAIT_INST_ANY was 34 %)
+// gelu_rl (dwfc::gelu_rl, bit-identical) on four values in lockstep, so four independent chains interleave
+// (measured no faster than the per-element form in this kernel, kept for the explicit schedule)
 __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
   f32x4 ax, t, q, e, r;
 #pragma unroll
@@ -365,50 +372,53 @@ __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
 }
 
 template <typename T, class C>
-__global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, const char* __restrict__ pk,
-                                                 const float* __restrict__ b2, const T* __restrict__ R,
-                                                 T* __restrict__ Y, int ntiles, int K) {
+__global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restrict__ Hm, const char* __restrict__ pk,
+                                                               const float* __restrict__ b2, const T* __restrict__ R,
+                                                               T* __restrict__ Y, int ntiles, int K) {
   typedef v8_t<T> tx8;
-  constexpr int WI = C::WI, WNB = C::WNB, RR = C::R;
+  constexpr int WI = C::WI, WNB = C::WNB, SW = C::SW, NW = C::NW, MPW = C::MPW, DPW = C::DPW;
   __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
   const uint32_t lds0 = (uint32_t)(uintptr_t)(dwfc::las_ptr)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
+  const int cb = wave & 3, mb0 = (wave >> 2) * MPW;    // this wave's dwconv: channel block, first m-block
   const int tile = dwfc::xcd_remap(blockIdx.x, gridDim.x);
   if (tile >= ntiles) return;
-  const int frame = tile / C::TILES_PER_FRAME, y0 = (tile % C::TILES_PER_FRAME) * RR;
+  const int frame = tile / C::TILES_PER_FRAME, y0 = (tile % C::TILES_PER_FRAME) * C::R;
   const int nk = K / C::BK;
   const long fbase = (long)frame * WI * WI;            // first token of the frame
 
-  // ---- DMA of the H tile of K-step kt into ring slot hb: chunk q = 64 blk + lane (blk = wave + 4 j): row
-  // i = q / 128, slot px = (q / 8) % 16, LDS chunk cs = q % 8 holds global chunk cs ^ (px & 7)
+  // ---- DMA of the H tile of K-step kt into ring slot hb: chunk q = 64 blk + lane (blk = wave + NW j): linear
+  // slot L = q / 8 (row L / SW, slot L % SW), LDS chunk cs = q % 8 holds global chunk cs ^ (L & 7)
   const char* zero = reinterpret_cast<const char*>(dwfc::g_zero);
-  const char* hsrc[3];
+  const char* hsrc[DPW];
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
-    const int q = (wave + 4 * j) * 64 + lane;
-    const int i = q >> 7, px = (q >> 3) & 15, c = (q & 7) ^ (px & 7), y = y0 - 1 + i;
-    hsrc[j] = (px >= 1 && px <= WI && y >= 0 && y < WI)
-                  ? reinterpret_cast<const char*>(Hm + (fbase + (long)y * WI + (px - 1)) * K + c * 8)
+  for (int j = 0; j < DPW; ++j) {
+    const int q = (wave + NW * j) * 64 + lane, L = q >> 3;
+    const int i = L / SW, sl = L % SW, c = (q & 7) ^ (L & 7), y = y0 - 1 + i;
+    hsrc[j] = (i < C::HROWS && sl >= 1 && sl <= WI && y >= 0 && y < WI)
+                  ? reinterpret_cast<const char*>(Hm + (fbase + (long)y * WI + (sl - 1)) * K + c * 8)
                   : nullptr;
   }
   auto dma_h = [&](int kt, int hb) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j)
+    for (int j = 0; j < DPW; ++j)
       dwfc::dma16(hsrc[j] ? hsrc[j] + kt * 128 : zero,
-                  __builtin_amdgcn_readfirstlane(lds0 + C::H_OFF + hb * C::HBYTES + (wave + 4 * j) * 1024));
+                  __builtin_amdgcn_readfirstlane(lds0 + C::H_OFF + hb * C::HBYTES + (wave + NW * j) * 1024));
   };
 
   // ---- dwconv on MFMA.  B fragment (kk, mb): lane (fr, fq) reads tap t = 2 kk + (fq >> 1) (t = 9: padding,
-  // any address) of token (row mb, slot fr): H at row mb + t / 3, slot fr + t % 3 - 1 (clamped: the padding
-  // slots' own outputs are garbage, never stored), channels 16 w + 8 (fq & 1) .. + 7
+  // any address) of token slot 16 mb + fr = (tile row rt, slot s): H at row rt + t / 3, slot s + t % 3 - 1,
+  // i.e. linear slot L = 16 mb + (token row's first slot) + ..., channels 16 cb + 8 (fq & 1) .. + 7.  Padding
+  // lanes' own outputs are garbage, never stored; their reads stay inside the workgroup's LDS
   int hoff[5];
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
     const int t = min(2 * kk + (fq >> 1), 8), dy = t / 3, dx = t % 3;
-    const int sl = min(max(fr + dx - 1, 0), 15), c = 2 * wave + (fq & 1);
-    hoff[kk] = (dy * 16 + sl) * 128 + ((c ^ (sl & 7)) << 4);
+    const int rt = fr / SW, s = fr % SW;
+    const int L = max((rt + dy) * SW + s + dx - 1, 0), c = 2 * cb + (fq & 1);
+    hoff[kk] = L * 128 + ((c ^ (L & 7)) << 4);
   }
   // dwconv A fragments (one non-zero each, built by dwfc2_pack) and the lane's dwconv biases, one K-step
   // at a time: loaded right after dwconv(k) has read them, for dwconv(k + 1) one iteration later
@@ -416,7 +426,7 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
   f32x4 dbv;
   const char* pkl = pk + lane * 16;
   auto load_a = [&](int kt) {
-    const char* src = pkl + (long)kt * C::PK + wave * 6 * 1024;
+    const char* src = pkl + (long)kt * C::PK + cb * 6 * 1024;
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(afr[kk]) : "v"(src + kk * 1024) : "memory");
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dbv) : "v"(src + 5 * 1024) : "memory");
@@ -426,34 +436,34 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
     for (int kk = 0; kk < 5; ++kk) asm volatile("" : "+v"(afr[kk]));
     asm volatile("" : "+v"(dbv));
   };
-  f32x4 dacc[RR];
+  f32x4 dacc[MPW];
   auto dwconv = [&](int hb) {
-    const char* hs = smem + C::H_OFF + hb * C::HBYTES;
+    const char* hs = smem + C::H_OFF + hb * C::HBYTES + mb0 * 2048;
 #pragma unroll
-    for (int mb = 0; mb < RR; ++mb) dacc[mb] = dbv;
+    for (int m = 0; m < MPW; ++m) dacc[m] = dbv;
 #pragma unroll
     for (int kk = 0; kk < 5; ++kk)
 #pragma unroll
-      for (int mb = 0; mb < RR; ++mb)
-        dacc[mb] = mfma16x16x32(afr[kk], *reinterpret_cast<const tx8*>(hs + hoff[kk] + mb * 2048), dacc[mb]);
+      for (int m = 0; m < MPW; ++m)
+        dacc[m] = mfma16x16x32(afr[kk], *reinterpret_cast<const tx8*>(hs + hoff[kk] + m * 2048), dacc[m]);
   };
-  // GELU of the dwconv outputs -> G tile gb: lane (fr, fq) of m-block mb = channels 16 w + 4 fq .. + 3, slot mb 16 + fr
+  // GELU of the dwconv outputs -> G tile gb: lane (fr, fq) of m-block mb = channels 16 cb + 4 fq .. + 3, slot 16 mb + fr
   auto gelu_store = [&](int gb) {
 #pragma unroll
-    for (int mb = 0; mb < RR; ++mb) {
-      const f32x4 gv = gelu4(dacc[mb]);
+    for (int m = 0; m < MPW; ++m) {
+      const f32x4 gv = gelu4(dacc[m]);
       const T o[4] = {from_f<T>(gv[0]), from_f<T>(gv[1]), from_f<T>(gv[2]), from_f<T>(gv[3])};
-      const int s = mb * 16 + fr, cw = 16 * wave + 4 * fq;
+      const int s = (mb0 + m) * 16 + fr, cw = 16 * cb + 4 * fq;
       *reinterpret_cast<uint2*>(smem + C::G_OFF + gb * C::GBYTES + s * 128 + ((((cw >> 3) ^ (s & 7)) << 4) | ((cw & 4) << 1))) =
           *reinterpret_cast<const uint2*>(o);
     }
   };
 
-  // ---- fc2: wave's n-blocks n0w + 16 nb, W2 fragments of one K-step (2 x 32 channels)
-  const int n0w = wave * (C::N / 4);
+  // ---- fc2: wave's n-blocks n0w + 16 nb over the 4 m-blocks, W2 fragments of one K-step (2 x 32 channels)
+  const int n0w = wave * (C::N / NW);
   tx8 w2f[2][WNB];
   auto load_w2 = [&](int kt, int ks) {
-    const char* src = pkl + (long)kt * C::PK + C::APK + (ks * 4 + wave) * WNB * 1024;
+    const char* src = pkl + (long)kt * C::PK + C::APK + (ks * NW + wave) * WNB * 1024;
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb)
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(w2f[ks][nb]) : "v"(src + nb * 1024) : "memory");
@@ -464,15 +474,15 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
 #pragma unroll
       for (int nb = 0; nb < WNB; ++nb) asm volatile("" : "+v"(w2f[ks][nb]));
   };
-  f32x4 acc[RR][WNB];
+  f32x4 acc[4][WNB];
 #pragma unroll
-  for (int mb = 0; mb < RR; ++mb)
+  for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto fc2_half = [&](int gb, int ks) {
     const char* gs = smem + C::G_OFF + gb * C::GBYTES;
 #pragma unroll
-    for (int mb = 0; mb < RR; ++mb) {
+    for (int mb = 0; mb < 4; ++mb) {
       const int row = mb * 16 + fr;
       const tx8 g = *reinterpret_cast<const tx8*>(gs + row * 128 + (((ks * 4 + fq) ^ (row & 7)) << 4));
 #pragma unroll
@@ -509,7 +519,8 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
     load_w2(kt + 1, 1);
     gelu_store((kt + 1) & 1);
     dma_h(min(kt + 3, nk - 1), kt % 3);
-    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // A(kt + 2) [6], W2(kt + 1) [2 WNB] retired; DMA [3] not
+    // A(kt + 2) [6] and W2(kt + 1) [2 WNB] retired; the DMA [DPW] not
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
     tie_a();
     tie_w2();
     __syncthreads();
@@ -518,10 +529,10 @@ __global__ __launch_bounds__(256, 2) void dwfc2_rw(const T* __restrict__ Hm, con
   fc2_half((nk - 1) & 1, 1);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");    // the clamped tail DMA (never read) retires
 
-  // ---- epilogue: lane (fr, fq) of block (mb, nb) = token (row y0 + mb, pixel fr - 1), channels n .. n + 3
+  // ---- epilogue: lane (fr, fq) of block (mb, nb) = token slot 16 mb + fr, channels n .. n + 3
 #pragma unroll
-  for (int mb = 0; mb < RR; ++mb) {
-    const int y = y0 + mb, x = fr - 1;
+  for (int mb = 0; mb < 4; ++mb) {
+    const int t = mb * 16 + fr, y = y0 + t / SW, x = t % SW - 1;
     if (y >= WI || x < 0 || x >= WI) continue;
     const long m = fbase + (long)y * WI + x;
 #pragma unroll
@@ -547,7 +558,7 @@ static int launch(const void* H, const void* pk, const float* b2, const void* R,
   hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), 0, st, (const T*)H, (const char*)pk, b2,
                      (const T*)R, (T*)Y, (int)nt, K);
   static char name[64];
-  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d>>", type_name<T>(), C::N);
+  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d, %d>>", type_name<T>(), C::N, C::WI);
   set_last_kernel(name);
   return check_launch("dw_fc2_mx");
 }
@@ -596,8 +607,10 @@ extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, co
 
 // ---- the stage-3 form with the depthwise conv on MFMA: operands packed once per weight set -------------
 extern "C" long svk_mixffn_dw_fc2_packed_bytes(int dtype, int W, int N, int K) {
-  if (!(dtype == SVK_F16 || dtype == SVK_BF16) || W != 14 || N != 320 || K % 64 || K <= 0) return 0;
-  return (long)(K / 64) * dwrw::Cfg<320>::PK;
+  if (!(dtype == SVK_F16 || dtype == SVK_BF16) || K % 64 || K <= 0) return 0;
+  if (W == 14 && N == 320) return (long)(K / 64) * dwrw::Cfg<320, 14>::PK;
+  if (W == 7 && N == 512) return (long)(K / 64) * dwrw::Cfg<512, 7>::PK;
+  return 0;
 }
 
 extern "C" int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float* dbias, const void* W2, int W, int N,
@@ -609,7 +622,10 @@ extern "C" int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float*
   }
   if ((((uintptr_t)packed) | ((uintptr_t)W2)) & 15) { set_error("svk_mixffn_dw_fc2_pack: misaligned operand"); return SVK_EINVAL; }
   hipStream_t st = (hipStream_t)stream;
-  SVK_DISPATCH_H16(dtype, T, { return dwrw::pack<T, dwrw::Cfg<320>>(taps, dbias, W2, K, packed, st); });
+  SVK_DISPATCH_H16(dtype, T, {
+    if (W == 7) return dwrw::pack<T, dwrw::Cfg<512, 7>>(taps, dbias, W2, K, packed, st);
+    return dwrw::pack<T, dwrw::Cfg<320, 14>>(taps, dbias, W2, K, packed, st);
+  });
 }
 
 extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const float* b2, const void* R,
@@ -624,5 +640,8 @@ extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* pa
   }
   if (B == 0) return SVK_OK;
   hipStream_t st = (hipStream_t)stream;
-  SVK_DISPATCH_H16(dtype, T, { return dwrw::launch<T, dwrw::Cfg<320>>(H, packed, b2, R, Y, B, K, st); });
+  SVK_DISPATCH_H16(dtype, T, {
+    if (Wimg == 7) return dwrw::launch<T, dwrw::Cfg<512, 7>>(H, packed, b2, R, Y, B, K, st);
+    return dwrw::launch<T, dwrw::Cfg<320, 14>>(H, packed, b2, R, Y, B, K, st);
+  });
 }

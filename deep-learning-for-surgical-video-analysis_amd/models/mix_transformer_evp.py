@@ -74,10 +74,11 @@ class Mlp(nn.Module):
     def _pack(self, dt):
         p = dict(w1=lin_w(self.fc1, dt), b1=lin_b(self.fc1), w2=lin_w(self.fc2, dt), b2=lin_b(self.fc2))
         if dt in ops.H16 and ops.DWFC2_MX and p["w2"].is_cuda:
-            # the stage-3 back half on the matrix cores (svk_mixffn_dw_fc2_packed): its operands packed once;
-            # None for the widths / shapes without that form
+            # the stage-3 / stage-4 back half on the matrix cores (svk_mixffn_dw_fc2_packed): operands packed once
+            # per map width that has that form (14 x 14 with N = 320, 7 x 7 with N = 512)
             pd = self.dwconv._pack(dt)
-            p["dwfc_pk"] = ops.mixffn_dw_fc2_pack(pd["taps"], pd["b"], p["w2"], 14)
+            pks = {w: ops.mixffn_dw_fc2_pack(pd["taps"], pd["b"], p["w2"], w) for w in (14, 7)}
+            p["dwfc_pk"] = {w: v for w, v in pks.items() if v is not None}
         return p
 
     def forward(self, x, H, W, residual=None, ln=None):
@@ -108,13 +109,13 @@ class Mlp(nn.Module):
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")
             y = ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
         elif (x.dtype in ops.H16 and H == W and residual is not None
-              and ((W == 14 and p.get("dwfc_pk") is not None)
+              and (W in p.get("dwfc_pk", {})
                    or (ops.DW_FC2 and ops.mixffn_dw_fc2_supported(x.dtype, W, self.fc2.out_features, hid)))):
             # fc1 GEMM, then DWConv + GELU fused into fc2 (the GELU map never leaves the chip)
             h = ops.gemm(x, p["w1"], p["b1"])
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             y = ops.mixffn_dw_fc2(h.view(B, H, W, hid), pd["taps"], pd["b"], p["w2"], p["b2"], residual=residual,
-                                  packed=p.get("dwfc_pk") if W == 14 else None)
+                                  packed=p.get("dwfc_pk", {}).get(W))
         else:
             h = ops.gemm(x, p["w1"], p["b1"])
             h = self.dwconv(h, H, W, act="gelu")           # DWConv + GELU in one pass (Mlp.forward :61-63)

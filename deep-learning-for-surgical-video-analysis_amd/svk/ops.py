@@ -404,7 +404,8 @@ def mixffn_dw_fc2_pack(taps, dbias, w2, W):
 def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None):
     """fc2(GELU(dwconv3x3(h) + dbias)) + b2 (+ residual) with the GELU map kept on chip (svk_mixffn_dw_fc2):
     h [B, H, W, K] fc1 output (16-bit NHWC), taps [9, K] / dbias [K] f32 as DWConv packs them, w2 [N, K];
-    returns [B, H * W, N].  Where the map has the matrix-core form (stage 3: 14 x 14, N = 320) it runs that,
+    returns [B, H * W, N].  Where the map has the matrix-core form (14 x 14 with N = 320, 7 x 7 with N = 512)
+    it runs that,
     from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form."""
     if h.dtype not in H16:
         raise _lib.SvkError("svk.mixffn_dw_fc2: bf16 / f16 only")

@@ -145,7 +145,8 @@ int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K);
 int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2, const float* b2,
                       const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, void* stream);
 
-/* The stage-3 shape (14 x 14, N = 320, K % 64 == 0, 16-bit) with the depthwise conv on the matrix cores
+/* The stage-3 / stage-4 shapes (14 x 14 with N = 320, 7 x 7 with N = 512; K % 64 == 0, 16-bit) with the
+ * depthwise conv on the matrix cores
  * (csrc/dwfc2.hip, dwrw): the operands are packed once per weight set — svk_mixffn_dw_fc2_pack writes
  * svk_mixffn_dw_fc2_packed_bytes(...) bytes (16-byte aligned): per 64-channel K-step the dwconv A fragments
  * (taps rounded to the 16-bit type, block-diagonal), the dwconv biases and the W2 fragments, in load order —

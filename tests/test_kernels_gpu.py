@@ -221,12 +221,12 @@ def test_conv2d_s2d_ln(cuda, dt, B, HB, CS, ln, C):
 
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,res", [(3, True), (1, False), (5, True)])
-@pytest.mark.parametrize("W,K,N,mx", [(14, 1280, 320, True), (14, 1280, 320, False), (7, 2048, 512, False),
-                                      (14, 640, 320, True)])
+@pytest.mark.parametrize("W,K,N,mx", [(14, 1280, 320, True), (14, 1280, 320, False), (7, 2048, 512, True),
+                                      (7, 2048, 512, False), (14, 640, 320, True), (7, 1024, 512, True)])
 def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N, mx, monkeypatch):
     """dwconv3x3 + GELU fused into fc2 (svk_mixffn_dw_fc2; the stage-3 / stage-4 shapes 14 x 14, 1280 -> 320 and
-    7 x 7, 2048 -> 512; mx: the stage-3 form with the depthwise conv on MFMA from packed operands,
-    svk_mixffn_dw_fc2_packed, also at a shorter K) against the unfused svk path (dwconv3x3 + gemm: same
+    7 x 7, 2048 -> 512; mx: the form with the depthwise conv on MFMA from packed operands,
+    svk_mixffn_dw_fc2_packed, also at shorter K) against the unfused svk path (dwconv3x3 + gemm: same
     roundings but for the mx form's 16-bit taps, expected within a few 16-bit ulps) and fp64.  Token counts
     that are not a multiple of the 64 / 32-token tile (masked rows)."""
     from svk import ops
