@@ -587,6 +587,8 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
       case 10: return launch_pk_k<T, PkCfg<128, 64, 2, 2, 2>, 1>(a, st, !big);
       case 20: return launch_pk_k<T, PkCfg<64, 128, 2, 2, 2>, 1>(a, st, !big);
       case 30: return launch_pk_k<T, PkCfg<64, 64, 2, 2, 2>, 1>(a, st, !big);
+      // (128 x 160 for the N = 320 patch embed: 74.5 vs 88 us in isolation, profiles/r05/conv_sweep.txt, but the
+      // conv instantiation spills 2 VGPRs — rejected by isa_check: scratch beside counted DMA waits)
       default: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 1>(a, st, !reg_epi);
     }
   }

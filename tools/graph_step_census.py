@@ -64,6 +64,17 @@ def analyse(args):
         foreign = collections.Counter(r["Kernel_Name"][:90] for r in st if "svk" not in r["Kernel_Name"])
         print(f"step {k}: {len(st)} launches, span {(e1 - s0) / 1e6:.3f} ms, sum of kernel times {busy / 1e6:.3f} ms, "
               f"non-svk: {dict(foreign) if foreign else 'none'}")
+    if args.by_kernel and steps:   # per-kernel time per replayed step (all replays but the first)
+        use = steps[1:] or steps
+        agg, cnt = collections.Counter(), collections.Counter()
+        for st in use:
+            for r in st:
+                agg[r["Kernel_Name"][:100]] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+                cnt[r["Kernel_Name"][:100]] += 1
+        tot = sum(agg.values()) / len(use) / 1e3
+        print(f"per replayed step: {sum(cnt.values()) / len(use):.1f} launches, kernel time {tot:.1f} us")
+        for k, v in agg.most_common():
+            print(f"{v / len(use) / 1e3:9.1f} us {cnt[k] / len(use):6.1f}x  {k}")
     if args.seq and steps:   # the last step's launch sequence: start offset, duration (us), queue, kernel
         st = steps[-1]
         s0 = int(st[0]["Start_Timestamp"])
@@ -80,6 +91,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--replays", type=int, default=6)
     ap.add_argument("--seq", default="", help="analyse: write the last step's launch sequence here")
+    ap.add_argument("--by-kernel", action="store_true", help="analyse: per-kernel time per replayed step")
     args = ap.parse_args()
     (run if args.mode == "run" else analyse)(args)
 
