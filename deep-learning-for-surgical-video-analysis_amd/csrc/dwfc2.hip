@@ -285,28 +285,33 @@ static int launch(const void* H, const float* taps, const float* db, const void*
 // f32 from the bias, gelu_rl, G rounded to 16 bits; fc2 as the GEMM (f32, + b2, + residual, one rounding).
 namespace dwrw {
 
-// Geometry.  A tile = (frame, R image rows) x all N outputs, 64 token slots = 4 MFMA m-blocks of 16.  The H
-// tile in LDS holds rows y0 - 1 .. in SW-slot rows: slot 0 is the conv's left zero padding and slot s the
-// pixel s - 1; the right padding is slot W + 1 when SW = W + 2 (14 x 14: SW = 16, one image row per m-block)
-// or the NEXT row's slot 0 when SW = W + 1 (7 x 7: SW = 8, two image rows per m-block; one extra zero row
-// below).  Token slot t <-> image row y0 + t / SW, slot t % SW.  Waves: NW = 4 (N = 320, 5 fc2 n-blocks
-// each) or 8 (N = 512, 4 each, one workgroup per CU); the dwconv of channel block cb = w % 4 of the K-step for
-// 16 / NW m-blocks per wave.
+// Geometry.  A tile = (frame, R image rows) x all N outputs, 16 NMB token slots = NMB MFMA m-blocks of 16.  The
+// H tile in LDS holds rows y0 - 1 .. in SW-slot rows: slot 0 is the conv's left zero padding and slot s the
+// pixel s - 1; the right padding is slot W + 1 when SW >= W + 2 (14 x 14: SW = 16, one image row per m-block;
+// 28 x 28: SW = 32, half a row per m-block, slots 30 / 31 unused zeros) or the NEXT row's slot 0 when SW = W + 1
+// (7 x 7: SW = 8, two image rows per m-block; one extra zero row below).  Token slot t <-> image row
+// y0 + t / SW, slot t % SW, so the tap (dy, dx) of slot t is linear slot t + dy SW + dx - 1.  Waves: NW = 4
+// (N = 320: 5 fc2 n-blocks each) or 8 (N = 512: 4 each; N = 128: 1 each, 8 m-blocks), the dwconv of channel
+// block cb = w % 4 of the K-step for MPW = 4 NMB / NW m-blocks per wave.
 template <int N_, int WI_>
 struct Cfg {
   static constexpr int N = N_, WI = WI_, BK = 64;
-  static constexpr int SW = WI <= 7 ? 8 : 16, MBR = 16 / SW, R = 4 * MBR, XROW = SW == WI + 1 ? 1 : 0;
-  static constexpr int NW = N == 512 ? 8 : 4, NT = 64 * NW, WNB = N / (16 * NW), MPW = 16 / NW;
+  static constexpr int SW = WI <= 7 ? 8 : (WI <= 14 ? 16 : 32);
+  static constexpr int NMB = N == 128 ? 8 : 4, R = 16 * NMB / SW, XROW = SW == WI + 1 ? 1 : 0;
+  static constexpr int NW = N == 320 ? 4 : 8, NT = 64 * NW, WNB = N / (16 * NW), MPW = 4 * NMB / NW;
   static constexpr int HROWS = R + 2 + XROW, HCH = HROWS * SW * 8;
   static constexpr int DPW = (HCH + 64 * NW - 1) / (64 * NW);   // DMA wave-instructions per wave per K-step
-  static constexpr int HBYTES = DPW * NW * 1024, NHB = 3, GBYTES = 64 * 128;
-  static constexpr int H_OFF = 0, G_OFF = NHB * HBYTES, LDS = G_OFF + 2 * GBYTES;
+  // H ring slot: one 128-byte front pad (linear slot -1: the left tap of the tile's first token, a padding
+  // lane whose output is never stored) + the DMA'd tile; 1 KiB of slack keeps the slots 1 KiB-aligned
+  static constexpr int HBYTES = DPW * NW * 1024, HSTRIDE = HBYTES + 1024, NHB = 3, GBYTES = NMB * 16 * 128;
+  static constexpr int H_OFF = 0, G_OFF = NHB * HSTRIDE, LDS = G_OFF + 2 * GBYTES;
   static constexpr int TILES_PER_FRAME = (WI + R - 1) / R;
   // packed operands per K-step (svk_mixffn_dw_fc2_pack): A part [4 channel blocks][6][64 lanes] x 16 B (5 dwconv
   // A fragments + the lane's 4 dwconv biases), then W2 part [2 ks][NW waves][WNB][64 lanes] x 16 B (fc2 A
   // fragments): every load of the K loop is one contiguous 1 KiB wave-instruction
   static constexpr int APK = 4 * 6 * 64 * 16, WPK = 2 * NW * WNB * 64 * 16, PK = APK + WPK;
-  static_assert(N % (16 * NW) == 0 && SW * MBR == 16 && SW % 8 == 0 && HROWS * SW * 128 <= HBYTES, "shape");
+  static_assert(N % (16 * NW) == 0 && R * SW == 16 * NMB && SW % 8 == 0 && HROWS * SW * 128 <= HBYTES &&
+                SW >= WI + 1 && WNB >= 1 && MPW >= 1, "shape");
 };
 
 // packed operands: one thread per 16-byte chunk (A part, then W2 part, K-step-major)
@@ -377,7 +382,9 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
                                                                T* __restrict__ Y, int ntiles, int K) {
   typedef v8_t<T> tx8;
   constexpr int WI = C::WI, WNB = C::WNB, SW = C::SW, NW = C::NW, MPW = C::MPW, DPW = C::DPW;
-  __shared__ __attribute__((aligned(1024))) char smem[C::LDS];
+  // dynamic LDS (C::LDS bytes, up to 107 KiB for 28 x 28), sized through hipFuncAttributeMaxDynamicSharedMemorySize
+  extern __shared__ __attribute__((aligned(16))) uint4 smem_dwrw[];
+  char* const smem = reinterpret_cast<char*>(smem_dwrw);
   const uint32_t lds0 = (uint32_t)(uintptr_t)(dwfc::las_ptr)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -405,20 +412,21 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
 #pragma unroll
     for (int j = 0; j < DPW; ++j)
       dwfc::dma16(hsrc[j] ? hsrc[j] + kt * 128 : zero,
-                  __builtin_amdgcn_readfirstlane(lds0 + C::H_OFF + hb * C::HBYTES + (wave + NW * j) * 1024));
+                  __builtin_amdgcn_readfirstlane(lds0 + C::H_OFF + hb * C::HSTRIDE + 128 + (wave + NW * j) * 1024));
   };
 
   // ---- dwconv on MFMA.  B fragment (kk, mb): lane (fr, fq) reads tap t = 2 kk + (fq >> 1) (t = 9: padding,
-  // any address) of token slot 16 mb + fr = (tile row rt, slot s): H at row rt + t / 3, slot s + t % 3 - 1,
-  // i.e. linear slot L = 16 mb + (token row's first slot) + ..., channels 16 cb + 8 (fq & 1) .. + 7.  Padding
-  // lanes' own outputs are garbage, never stored; their reads stay inside the workgroup's LDS
+  // any address) of token slot u = 16 mb + fr: linear slot L = u + (t / 3) SW + t % 3 - 1 of the H tile, channels
+  // 16 cb + 8 (fq & 1) .. + 7.  Padding lanes' own outputs are garbage, never stored; their reads stay inside
+  // the workgroup's LDS.  (Round 5: clamping L at 0 instead of the front pad read the wrong left neighbour for
+  // a 28 x 28 tile's m-block 1, whose first token is a real pixel.)
   int hoff[5];
 #pragma unroll
   for (int kk = 0; kk < 5; ++kk) {
     const int t = min(2 * kk + (fq >> 1), 8), dy = t / 3, dx = t % 3;
-    const int rt = fr / SW, s = fr % SW;
-    const int L = max((rt + dy) * SW + s + dx - 1, 0), c = 2 * cb + (fq & 1);
-    hoff[kk] = L * 128 + ((c ^ (L & 7)) << 4);
+    // m-block 0 (+ 16 slots per m-block); L = -1 only for the tile's first token (a padding lane): the front pad
+    const int L = fr + dy * SW + dx - 1, c = 2 * cb + (fq & 1);
+    hoff[kk] = (L + 1) * 128 + ((c ^ (L & 7)) << 4);
   }
   // dwconv A fragments (one non-zero each, built by dwfc2_pack) and the lane's dwconv biases, one K-step
   // at a time: loaded right after dwconv(k) has read them, for dwconv(k + 1) one iteration later
@@ -438,7 +446,7 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   };
   f32x4 dacc[MPW];
   auto dwconv = [&](int hb) {
-    const char* hs = smem + C::H_OFF + hb * C::HBYTES + mb0 * 2048;
+    const char* hs = smem + C::H_OFF + hb * C::HSTRIDE + mb0 * 2048;
 #pragma unroll
     for (int m = 0; m < MPW; ++m) dacc[m] = dbv;
 #pragma unroll
@@ -474,15 +482,16 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
 #pragma unroll
       for (int nb = 0; nb < WNB; ++nb) asm volatile("" : "+v"(w2f[ks][nb]));
   };
-  f32x4 acc[4][WNB];
+  constexpr int NMB = C::NMB;
+  f32x4 acc[NMB][WNB];
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb)
+  for (int mb = 0; mb < NMB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto fc2_half = [&](int gb, int ks) {
     const char* gs = smem + C::G_OFF + gb * C::GBYTES;
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb) {
+    for (int mb = 0; mb < NMB; ++mb) {
       const int row = mb * 16 + fr;
       const tx8 g = *reinterpret_cast<const tx8*>(gs + row * 128 + (((ks * 4 + fq) ^ (row & 7)) << 4));
 #pragma unroll
@@ -531,7 +540,7 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
 
   // ---- epilogue: lane (fr, fq) of block (mb, nb) = token slot 16 mb + fr, channels n .. n + 3
 #pragma unroll
-  for (int mb = 0; mb < 4; ++mb) {
+  for (int mb = 0; mb < NMB; ++mb) {
     const int t = mb * 16 + fr, y = y0 + t / SW, x = t % SW - 1;
     if (y >= WI || x < 0 || x >= WI) continue;
     const long m = fbase + (long)y * WI + x;
@@ -555,7 +564,13 @@ template <typename T, class C>
 static int launch(const void* H, const void* pk, const float* b2, const void* R, void* Y, int B, int K, hipStream_t st) {
   const long nt = (long)B * C::TILES_PER_FRAME;
   if (nt > 0x7fffffffL || (long)B * C::WI * C::WI * K > 0x7fffffffL) return SVK_EUNSUPPORTED;
-  hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), 0, st, (const T*)H, (const char*)pk, b2,
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dwfc2_rw<T, C>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              C::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H, (const char*)pk, b2,
                      (const T*)R, (T*)Y, (int)nt, K);
   static char name[64];
   if (!name[0]) snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d, %d>>", type_name<T>(), C::N, C::WI);
@@ -610,6 +625,7 @@ extern "C" long svk_mixffn_dw_fc2_packed_bytes(int dtype, int W, int N, int K) {
   if (!(dtype == SVK_F16 || dtype == SVK_BF16) || K % 64 || K <= 0) return 0;
   if (W == 14 && N == 320) return (long)(K / 64) * dwrw::Cfg<320, 14>::PK;
   if (W == 7 && N == 512) return (long)(K / 64) * dwrw::Cfg<512, 7>::PK;
+  if (W == 28 && N == 128) return (long)(K / 64) * dwrw::Cfg<128, 28>::PK;
   return 0;
 }
 
@@ -624,6 +640,7 @@ extern "C" int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float*
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
     if (W == 7) return dwrw::pack<T, dwrw::Cfg<512, 7>>(taps, dbias, W2, K, packed, st);
+    if (W == 28) return dwrw::pack<T, dwrw::Cfg<128, 28>>(taps, dbias, W2, K, packed, st);
     return dwrw::pack<T, dwrw::Cfg<320, 14>>(taps, dbias, W2, K, packed, st);
   });
 }
@@ -642,6 +659,7 @@ extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* pa
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
     if (Wimg == 7) return dwrw::launch<T, dwrw::Cfg<512, 7>>(H, packed, b2, R, Y, B, K, st);
+    if (Wimg == 28) return dwrw::launch<T, dwrw::Cfg<128, 28>>(H, packed, b2, R, Y, B, K, st);
     return dwrw::launch<T, dwrw::Cfg<320, 14>>(H, packed, b2, R, Y, B, K, st);
   });
 }

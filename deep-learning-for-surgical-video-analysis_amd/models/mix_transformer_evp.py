@@ -29,6 +29,14 @@ from ._common import pair, compute_dtype, check_inference, to_nhwc, DropPath
 from .segformer_head import SegFormerHead
 
 
+def _lin_pack(lin, dt):
+    """A Linear's packed forms: the weight in dt, the f32 bias, and (16-bit, N in {320, 512}) the gemm_ln
+    fragments (None elsewhere).  One builder for every get_packed call on the module (the cache keys on the
+    parameters, not on the builder)."""
+    w = lin_w(lin, dt)
+    return dict(w=w, b=lin_b(lin), gln=ops.gemm_ln_pack(w))
+
+
 def _ln_params(norm):
     return norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous()
 
@@ -77,7 +85,7 @@ class Mlp(nn.Module):
             # the stage-3 / stage-4 back half on the matrix cores (svk_mixffn_dw_fc2_packed): operands packed once
             # per map width that has that form (14 x 14 with N = 320, 7 x 7 with N = 512)
             pd = self.dwconv._pack(dt)
-            pks = {w: ops.mixffn_dw_fc2_pack(pd["taps"], pd["b"], p["w2"], w) for w in (14, 7)}
+            pks = {w: ops.mixffn_dw_fc2_pack(pd["taps"], pd["b"], p["w2"], w) for w in ops.DWFC2_MX_WIDTHS}
             p["dwfc_pk"] = {w: v for w, v in pks.items() if v is not None}
         return p
 
@@ -103,14 +111,14 @@ class Mlp(nn.Module):
             return y.view(B, N, C)
         # measured: wins where the hidden map is largest (stages 1-2, C <= 128); at C = 320 / 512 the
         # recomputed halo fc1 work outweighs the saved traffic
-        if ops.FC1_DWCONV and x.dtype in ops.H16 and C in ops.FC1_DWCONV_C and hid % 64 == 0:
+        mx = x.dtype in ops.H16 and H == W and residual is not None and W in p.get("dwfc_pk", {})
+        if ops.FC1_DWCONV and x.dtype in ops.H16 and C in ops.FC1_DWCONV_C and hid % 64 == 0 and not mx:
             # fc1 -> DWConv -> GELU in one kernel, the hidden map kept on chip (Mlp.forward :60-63)
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
             g = ops.mixffn_fc1_dwconv(x.contiguous().view(B, H, W, C), p["w1"], p["b1"], pd["taps"], pd["b"], act="gelu")
             y = ops.gemm(g.view(B, N, hid), p["w2"], p["b2"], residual=residual)
-        elif (x.dtype in ops.H16 and H == W and residual is not None
-              and (W in p.get("dwfc_pk", {})
-                   or (ops.DW_FC2 and ops.mixffn_dw_fc2_supported(x.dtype, W, self.fc2.out_features, hid)))):
+        elif mx or (ops.DW_FC2 and x.dtype in ops.H16 and H == W and residual is not None
+                    and ops.mixffn_dw_fc2_supported(x.dtype, W, self.fc2.out_features, hid)):
             # fc1 GEMM, then DWConv + GELU fused into fc2 (the GELU map never leaves the chip)
             h = ops.gemm(x, p["w1"], p["b1"])
             pd = get_packed(self.dwconv, x.dtype, self.dwconv._pack)
@@ -152,6 +160,7 @@ class Attention(nn.Module):
             p["wsr"] = conv_w(self.sr.weight, dt)
             p["bsr"] = self.sr.bias.detach().float().contiguous()
             p["gn"], p["bn"] = _ln_params(self.norm)
+        p["wp_gln"] = ops.gemm_ln_pack(p["wp"])      # proj + residual + norm2 in one kernel (stages 3-4, 16-bit)
         return p
 
     @get_local("attn")
@@ -170,6 +179,25 @@ class Attention(nn.Module):
         kv = ops.gemm(xs, p["wkv"], p["bkv"])                                # [B, Nk, 2C]: k | v
         o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], self.num_heads, self.scale)
         return ops.gemm(o, p["wp"], p["bp"], residual=residual)
+
+    def forward_ln(self, x, H, W, residual, ln):
+        """(residual + attn(x), LayerNorm(residual + attn(x))) with proj, the residual add and the norm in one
+        kernel (svk_gemm_ln: N in {320, 512}); None where not covered."""
+        p = get_packed(self, x.dtype, self._pack)
+        if p.get("wp_gln") is None or residual is None:
+            return None
+        B, N, C = x.shape
+        x = x.contiguous()
+        q = ops.gemm(x, p["wq"], p["bq"])
+        if self.sr_ratio > 1:
+            r = self.sr_ratio
+            xs = ops.conv2d_ln_nhwc(x.view(B, H, W, C), p["wsr"], r, r, 0, p["bsr"], p["gn"], p["bn"], self.norm.eps)
+            xs = xs.view(B, -1, C)
+        else:
+            xs = x
+        kv = ops.gemm(xs, p["wkv"], p["bkv"])
+        o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], self.num_heads, self.scale)
+        return ops.gemm_ln(o, p["wp_gln"], C, p["bp"], residual.contiguous(), ln[0], ln[1], ln[2])
 
     def block_fusable(self, x, H, W):
         """True when svk_attn_block covers this layer: 16-bit, 64-channel heads with C in {64, 128} (MiT
@@ -219,8 +247,12 @@ class Block(nn.Module):
         if self.attn.block_fusable(x, H, W):
             x, h = self.attn.forward_block(h, H, W, x, (p["g2"], p["b2"], self.norm2.eps))
             return self.mlp(h, H, W, residual=x, ln=ln)
-        x = self.attn(h, H, W, residual=x)
-        h = ops.layernorm(x, p["g2"], p["b2"], self.norm2.eps)
+        fused = self.attn.forward_ln(h, H, W, x, (p["g2"], p["b2"], self.norm2.eps))
+        if fused is not None:            # proj + residual + norm2 in one kernel (stages 3-4)
+            x, h = fused
+        else:
+            x = self.attn(h, H, W, residual=x)
+            h = ops.layernorm(x, p["g2"], p["b2"], self.norm2.eps)
         return self.mlp(h, H, W, residual=x, ln=ln)
 
 
@@ -415,9 +447,25 @@ class PromptGenerator(nn.Module):
         sh = getattr(self, f"shared_mlp{block_num}")
         dt = x.dtype
         pl = get_packed(lw, dt, lambda d: dict(w=lin_w(lw, d), b=lin_b(lw)))
-        ps = get_packed(sh, dt, lambda d: dict(w=lin_w(sh, d), b=lin_b(sh)))
+        ps = get_packed(sh, dt, lambda d: _lin_pack(sh, d))
         feat = ops.gemm(summed, pl["w"], pl["b"], act="gelu")
         return ops.gemm(feat, ps["w"], ps["b"], residual=x)
+
+    def get_prompt_gln(self, x, prompt, block_num, depth_num, norm):
+        """(get_prompt(...), norm(get_prompt(...))) with the shared MLP, the residual add and the norm in one
+        kernel (svk_gemm_ln, stages 3-4 widths at 16 bits); None when not covered."""
+        summed = getattr(prompt, "summed", None)
+        if summed is None or x.dtype not in ops.H16:
+            return None
+        sh = getattr(self, f"shared_mlp{block_num}")
+        ps = get_packed(sh, x.dtype, lambda d: _lin_pack(sh, d))
+        if ps.get("gln") is None:
+            return None
+        lw = getattr(self, f"lightweight_mlp{block_num}_{depth_num}")[0]
+        pl = get_packed(lw, x.dtype, lambda d: dict(w=lin_w(lw, d), b=lin_b(lw)))
+        pn = get_packed(norm, x.dtype, lambda d, n=norm: _ln_params(n))
+        feat = ops.gemm(summed, pl["w"], pl["b"], act="gelu")
+        return ops.gemm_ln(feat, ps["gln"], x.shape[-1], ps["b"], x.contiguous(), pn[0], pn[1], norm.eps)
 
     def get_prompt_ln(self, x, prompt, block_num, depth_num, norm):
         """(get_prompt(...), norm(get_prompt(...))) in one kernel for the stages 1-3 widths at 16 bits
@@ -431,7 +479,7 @@ class PromptGenerator(nn.Module):
         sh = getattr(self, f"shared_mlp{block_num}")
         dt = x.dtype
         pl = get_packed(lw, dt, lambda d: dict(w=lin_w(lw, d), b=lin_b(lw)))
-        ps = get_packed(sh, dt, lambda d: dict(w=lin_w(sh, d), b=lin_b(sh)))
+        ps = get_packed(sh, dt, lambda d: _lin_pack(sh, d))
         pn = get_packed(norm, dt, lambda d, n=norm: _ln_params(n))
         return ops.prompt_ln(x.contiguous(), summed.contiguous(), pl["w"], pl["b"], ps["w"], ps["b"], pn[0], pn[1],
                              norm.eps)
@@ -596,9 +644,10 @@ class MixVisionTransformerEVP(nn.Module):
                 m.svk_dtype = dt
 
     # -- forward --------------------------------------------------------------------------------------
-    def _stages(self, x, y, hcs=None, hc_ready=None):
+    def _stages(self, x, y, hcs=None, hc_ready=None, emb0=None):
         """Token-level forward_features: returns [(tokens [B, H*W, C], H, W)] for the 4 stages.  ``hcs``:
-        handcrafted prompt maps computed elsewhere (a side stream), usable once ``hc_ready`` (an event)."""
+        handcrafted prompt maps computed elsewhere (a side stream), usable once ``hc_ready`` (an event);
+        ``emb0``: patch_embed1's output when the caller already has it."""
         dt = compute_dtype(self)
         self._propagate_dtype(dt)
         x = x.reshape(-1, 3, x.shape[-2], x.shape[-1])
@@ -608,7 +657,10 @@ class MixVisionTransformerEVP(nn.Module):
         outs = []
         for s in range(4):
             pe = getattr(self, f"patch_embed{s + 1}")
-            t, H, W = pe.embed_image(x) if s == 0 else pe.embed_nhwc(h)
+            if s == 0:
+                t, H, W = emb0 if emb0 is not None else pe.embed_image(x)
+            else:
+                t, H, W = pe.embed_nhwc(h)
             if hc_ready is not None:      # one event, or one per stage (the stage-s map is all stage s needs)
                 ev = hc_ready[s] if isinstance(hc_ready, (list, tuple)) else (hc_ready if s == 0 else None)
                 if ev is not None:
@@ -621,6 +673,8 @@ class MixVisionTransformerEVP(nn.Module):
                 # the stage norm (:370-412) rides on the last block's MixFFN epilogue
                 ln = (pn[0], pn[1], norm.eps) if i == len(blocks) - 1 else None
                 fused = self.prompt_generator.get_prompt_ln(t, prompt, s + 1, i, blk.norm1)
+                if fused is None:              # stages 3-4: shared MLP + residual + norm1 in one GEMM kernel
+                    fused = self.prompt_generator.get_prompt_gln(t, prompt, s + 1, i, blk.norm1)
                 if fused is not None:          # prompt add + norm1 in one kernel (stages 1-2)
                     t = blk(fused[0], H, W, ln=ln, h=fused[1])
                 else:
@@ -659,7 +713,15 @@ class MixVisionTransformerEVP(nn.Module):
             # cross-attention
             main = torch.cuda.current_stream(flow.device)
             side = _side_stream(flow.device)
-            side.wait_stream(main)
+            fork = torch.cuda.Event()
+            fork.record(main)
+            if EARLY_STEM:
+                # the main stream's stage-1 stem is enqueued BEFORE the side branch: a replayed graph dispatches
+                # its nodes in capture order, and with the side cascade first the main stream's first kernel
+                # started ~175 us into the step (profiles/r05/graph_step_sequence.txt); the side branch still
+                # depends only on the fork point, not on the stem
+                emb0 = self.patch_embed1.embed_image(x.reshape(-1, 3, x.shape[-2], x.shape[-1]))
+            side.wait_event(fork)
             with torch.cuda.stream(side):
                 if PROMPT_STAGE_EVENTS:     # stage 1 starts once the first handcrafted map exists
                     hc_ready = [torch.cuda.Event() for _ in range(4)]
@@ -669,7 +731,7 @@ class MixVisionTransformerEVP(nn.Module):
                     hc_ready = torch.cuda.Event()
                     hc_ready.record(side)
                 f3, f4 = self.flow_encoder(flow)
-            outs = self._stages(x, y, hcs=tuple(hcs), hc_ready=hc_ready)
+            outs = self._stages(x, y, hcs=tuple(hcs), hc_ready=hc_ready, emb0=emb0 if EARLY_STEM else None)
         else:
             outs = self._stages(x, y)
         if flow is not None:
@@ -688,6 +750,7 @@ class MixVisionTransformerEVP(nn.Module):
 
 FLOW_STREAM = os.environ.get("SVK_FLOW_STREAM", "1") == "1"
 PROMPT_STAGE_EVENTS = os.environ.get("SVK_PROMPT_STAGE_EVENTS", "1") == "1"
+EARLY_STEM = os.environ.get("SVK_EARLY_STEM", "1") == "1"
 _SIDE = {}
 
 

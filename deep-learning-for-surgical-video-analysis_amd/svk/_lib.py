@@ -71,6 +71,8 @@ SIGNATURES = {
     "svk_mixffn_rw": [c_int, P, P, P, P, P, P, P, P, P, P, P, P, c_float, c_int, c_int, c_int, c_int, P],
     "svk_mixffn_dw_fc2": [c_int, P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_mixffn_dw_fc2_pack": [c_int, P, P, P, c_int, c_int, c_int, P, P],
+    "svk_gemm_ln_pack": [c_int, P, c_int, c_int, P, P],
+    "svk_gemm_ln": [c_int, P, c_int, c_int, P, P, P, P, P, c_float, P, P, c_int, P],
     "svk_mixffn_dw_fc2_packed": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_conv2d_s2d_ln": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
@@ -109,6 +111,7 @@ SIGNATURES = {
 STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")
 LONG_FUNCS = {"svk_attention_bwd_workspace": [c_int, c_int, c_int, c_int, c_int, c_int],
               "svk_mixffn_dw_fc2_packed_bytes": [c_int, c_int, c_int, c_int],
+              "svk_gemm_ln_packed_bytes": [c_int, c_int, c_int],
               "svk_conv2d_ln_workspace": [c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_workspace": [c_int, c_int, c_int, c_int, c_int],
               "svk_mamba_scan_bwd_workspace": [c_int, c_int, c_int, c_int],

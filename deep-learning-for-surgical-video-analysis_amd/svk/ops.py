@@ -237,6 +237,50 @@ def layernorm(x, gamma, beta, eps, out=None):
     return out
 
 
+# off by default until it beats the unfused pair (first form: direct global A-fragment loads, one step of
+# prefetch — 63 us against 32 + 16 for proj + LayerNorm; step 32.5k vs 34.0k, profiles/r05/gemm_ln_mx28_ab.txt)
+GEMM_LN = os.environ.get("SVK_GEMM_LN", "0") == "1"
+
+
+def gemm_ln_pack(w):
+    """Packed weight fragments for gemm_ln (svk_gemm_ln_pack), or None where (dtype, N, K) has no gemm_ln
+    instantiation (N in {320, 512}, 16-bit, K % 8 == 0).  Pack once per weight set."""
+    if not GEMM_LN or w.dtype not in H16 or not w.is_cuda:
+        return None
+    N, K = w.shape
+    nbytes = _lib.load().svk_gemm_ln_packed_bytes(dtype_code(w.dtype), int(N), int(K))
+    if nbytes <= 0:
+        return None
+    _chk(w, "w")
+    if not w.is_contiguous():
+        raise _lib.SvkError("svk.gemm_ln_pack: w must be contiguous [N, K]")
+    out = torch.empty(nbytes, device=w.device, dtype=torch.uint8)
+    _lib.call("svk_gemm_ln_pack", dtype_code(w.dtype), _p(w), int(N), int(K), _p(out), _stream())
+    return out
+
+
+def gemm_ln(a, packed, n, bias, residual, gamma, beta, eps):
+    """(x, h): x = a @ w.T + bias (+ residual), h = LayerNorm(x) over the full row (svk_gemm_ln: one kernel,
+    the row statistics inside the workgroup); w from gemm_ln_pack.  a [..., K] 16-bit, n = N."""
+    _chk(a, "a"); _chk(bias, "bias", torch.float32); _chk(residual, "residual", a.dtype)
+    _chk(gamma, "gamma", torch.float32); _chk(beta, "beta", torch.float32)
+    M, K, lda = _rows(a, "a")
+    if lda != K:
+        raise _lib.SvkError("svk.gemm_ln: a must be row-contiguous")
+    shape = tuple(a.shape[:-1]) + (n,)
+    if residual is not None and (tuple(residual.shape) != shape or not residual.is_contiguous()):
+        raise _lib.SvkError("svk.gemm_ln: residual must be a contiguous [..., N] map")
+    x = torch.empty(shape, device=a.device, dtype=a.dtype)
+    h = torch.empty(shape, device=a.device, dtype=a.dtype)
+    t0 = _prof_begin()
+    _lib.call("svk_gemm_ln", dtype_code(a.dtype), _p(a), M, K, _p(packed), _p(bias), _p(residual), _p(gamma), _p(beta),
+              float(eps), _p(x), _p(h), int(n), _stream())
+    if t0 is not None:
+        _prof_end(t0, _last_kernel(), 2.0 * M * n * K, (M * K + n * K + M * n * (3 if residual is not None else 2)) * 2,
+                  (M, n, K, "gemm_ln"))
+    return x, h
+
+
 def attention(q, k, v, heads, scale, out=None):
     """q [B, Nq, heads*hd], k/v [B, Nk, heads*hd] (any row/batch strides, unit column stride)."""
     for t, nm in ((q, "q"), (k, "k"), (v, "v")):
@@ -376,6 +420,11 @@ MIXFFN_RW = os.environ.get("SVK_MIXFFN_RW", "1") == "1"
 # production are latency-bound at 2 waves per SIMD
 DW_FC2 = os.environ.get("SVK_DW_FC2", "0") == "1"
 DWFC2_MX = os.environ.get("SVK_DWFC2_MX", "1") == "1"
+# map widths whose MixFFN back half the model runs in the matrix-core form (14: stage 3, 7: stage 4).  28 (stage 2)
+# is instantiated but off: its fc1 then needs a GEMM of its own, and fc1 GEMM + dw_fc2_mx (196 us) loses to the
+# register-window fc1dw_rw (fc1 + dwconv, 135 us) + fc2 GEMM (68 us): step 32.6k vs 34.2k frames/s same-box
+# (profiles/r05/gemm_ln_mx28_ab.txt)
+DWFC2_MX_WIDTHS = tuple(int(v) for v in os.environ.get("SVK_DWFC2_MX_WIDTHS", "14,7").split(",") if v)
 
 
 def mixffn_dw_fc2_supported(dtype, W, N, K):
@@ -404,8 +453,8 @@ def mixffn_dw_fc2_pack(taps, dbias, w2, W):
 def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None):
     """fc2(GELU(dwconv3x3(h) + dbias)) + b2 (+ residual) with the GELU map kept on chip (svk_mixffn_dw_fc2):
     h [B, H, W, K] fc1 output (16-bit NHWC), taps [9, K] / dbias [K] f32 as DWConv packs them, w2 [N, K];
-    returns [B, H * W, N].  Where the map has the matrix-core form (14 x 14 with N = 320, 7 x 7 with N = 512)
-    it runs that,
+    returns [B, H * W, N].  Where the map has the matrix-core form (14 x 14 with N = 320, 7 x 7 with N = 512,
+    28 x 28 with N = 128) it runs that,
     from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form."""
     if h.dtype not in H16:
         raise _lib.SvkError("svk.mixffn_dw_fc2: bf16 / f16 only")

@@ -145,7 +145,8 @@ int svk_mixffn_dw_fc2_supported(int dtype, int W, int N, int K);
 int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* dbias, const void* W2, const float* b2,
                       const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, void* stream);
 
-/* The stage-3 / stage-4 shapes (14 x 14 with N = 320, 7 x 7 with N = 512; K % 64 == 0, 16-bit) with the
+/* The stage-2 / 3 / 4 shapes (28 x 28 with N = 128, 14 x 14 with N = 320, 7 x 7 with N = 512; K % 64 == 0,
+ * 16-bit) with the
  * depthwise conv on the matrix cores
  * (csrc/dwfc2.hip, dwrw): the operands are packed once per weight set — svk_mixffn_dw_fc2_pack writes
  * svk_mixffn_dw_fc2_packed_bytes(...) bytes (16-byte aligned): per 64-channel K-step the dwconv A fragments
@@ -158,6 +159,18 @@ int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float* dbias, con
                            void* packed, void* stream);
 int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const float* b2, const void* R, void* Y,
                              int B, int Himg, int Wimg, int K, int N, void* stream);
+
+/* GEMM + bias + residual + LayerNorm over the full output row in one kernel (csrc/gemm_ln.hip): X = A W^T + bias
+ * (+ R) rounded to the 16-bit type, H = LayerNorm(X; gamma, beta, eps) — Block's x + proj(...) followed by norm2,
+ * or the prompt adapter's x + shared_mlp(...) followed by norm1 (mix_transformer_evp.py:167-171, 776-815; replaces
+ * svk_gemm + svk_layernorm).  16-bit, N in {320, 512}, K % 8 == 0.  W is consumed PACKED: svk_gemm_ln_pack writes
+ * svk_gemm_ln_packed_bytes(dtype, N, K) bytes (0 where not instantiated) from W [N][K]; then svk_gemm_ln reads A
+ * [M][K] (row-contiguous), the packed buffer, bias [N] / gamma [N] / beta [N] f32 (bias may be NULL), R / X / H
+ * [M][N] (R and X may be NULL).  A, packed, bias, gamma, beta 16-byte aligned; R, X, H 8-byte. */
+long svk_gemm_ln_packed_bytes(int dtype, int N, int K);
+int svk_gemm_ln_pack(int dtype, const void* W, int N, int K, void* packed, void* stream);
+int svk_gemm_ln(int dtype, const void* A, int M, int K, const void* packed, const float* bias, const void* R,
+                const float* gamma, const float* beta, float eps, void* X, void* H, int N, void* stream);
 
 /* MixFFN front half, G = act(dwconv3x3(XN W1^T + b1) + dbias) over NHWC maps (Mlp.fc1 -> DWConv -> GELU,
  * mix_transformer_evp.py:60-63, 24-30): the 4C-wide hidden map stays on chip (fc1 recomputed on one

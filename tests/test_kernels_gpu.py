@@ -222,7 +222,8 @@ def test_conv2d_s2d_ln(cuda, dt, B, HB, CS, ln, C):
 @pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("B,res", [(3, True), (1, False), (5, True)])
 @pytest.mark.parametrize("W,K,N,mx", [(14, 1280, 320, True), (14, 1280, 320, False), (7, 2048, 512, True),
-                                      (7, 2048, 512, False), (14, 640, 320, True), (7, 1024, 512, True)])
+                                      (7, 2048, 512, False), (14, 640, 320, True), (7, 1024, 512, True),
+                                      (28, 512, 128, True)])
 def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N, mx, monkeypatch):
     """dwconv3x3 + GELU fused into fc2 (svk_mixffn_dw_fc2; the stage-3 / stage-4 shapes 14 x 14, 1280 -> 320 and
     7 x 7, 2048 -> 512; mx: the form with the depthwise conv on MFMA from packed operands,
@@ -253,6 +254,36 @@ def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N, mx, monkeypatch):
     if res:
         ref = ref + r.double().cpu()
     _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("M,N,K,res,bias", [(50176, 320, 320, True, True), (12544, 512, 512, True, True),
+                                            (1000, 320, 80, True, True), (77, 512, 128, True, False),
+                                            (130, 320, 40, False, True)])
+def test_gemm_ln(cuda, dt, M, N, K, res, bias):
+    """svk_gemm_ln (proj / shared-MLP GEMM + bias + residual + LayerNorm over the full row, packed weights)
+    against the unfused svk path (gemm, then layernorm of its rounded output: X bit-identical up to the MFMA
+    summation order, H within a few 16-bit ulps) and fp64; ragged M, K tails (80, 40: zero-filled fragments)."""
+    from svk import ops
+    a = _rand(M, K, dt=dt, dev=cuda, seed=81)
+    w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=82)
+    b = _rand(N, dt=torch.float32, dev=cuda, scale=0.1, seed=83) if bias else None
+    r = _rand(M, N, dt=dt, dev=cuda, seed=84) if res else None
+    g = 1 + _rand(N, dt=torch.float32, dev=cuda, scale=0.1, seed=85)
+    bt = _rand(N, dt=torch.float32, dev=cuda, scale=0.1, seed=86)
+    pk = ops.gemm_ln_pack(w)
+    assert pk is not None
+    x, h = ops.gemm_ln(a, pk, N, b, r, g, bt, 1e-6)
+    assert ops._last_kernel().startswith("gemm_ln"), ops._last_kernel()
+    x16 = ops.gemm(a, w, b, residual=r)
+    h16 = ops.layernorm(x16, g, bt, 1e-6)
+    ulp = 2 ** -8 if dt == torch.bfloat16 else 2 ** -11
+    assert (x.float() - x16.float()).abs().max().item() <= 2 * ulp * max(1.0, x16.float().abs().max().item())
+    assert (h.float() - h16.float()).abs().max().item() <= 4 * ulp * max(1.0, h16.float().abs().max().item())
+    xd = a.double().cpu() @ w.double().cpu().t() + (b.double().cpu() if bias else 0) + (r.double().cpu() if res else 0)
+    hd = F.layer_norm(xd, (N,), g.double().cpu(), bt.double().cpu(), 1e-6)
+    _close(x, xd, dt)
+    _close(h, hd, dt)
 
 
 @pytest.mark.parametrize("lds,rows", [(1, 1), (1, 3), (1, 8), (2, -1)])

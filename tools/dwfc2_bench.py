@@ -15,7 +15,7 @@ from pk_cfg_sweep import timeit  # noqa: E402
 def main():
     dev = torch.device("cuda:0")
     for dt, (W, K, N) in ((torch.float16, (14, 1280, 320)), (torch.bfloat16, (14, 1280, 320)),
-                          (torch.float16, (7, 2048, 512))):
+                          (torch.float16, (7, 2048, 512)), (torch.float16, (28, 512, 128))):
         B = 256
         h = torch.randn(B, W, W, K, device=dev).to(dt)
         taps = torch.randn(9, K, device=dev) * 0.3
