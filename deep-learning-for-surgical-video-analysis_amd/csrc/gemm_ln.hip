@@ -11,9 +11,9 @@
 //  * 4 waves split N (N / 4 columns each), every wave covers the BM rows; transposed MFMA (W fragment x A
 //    fragment, 16x16x32), a lane ends with 4 consecutive columns of one row;
 //  * W comes from a PACKED buffer (svk_gemm_ln_pack: per 32-wide k-step, per wave and n-block, the 64 lanes'
-//    16-byte fragments in load order — one contiguous 1 KiB wave-instruction each, L2-resident), A fragments
-//    straight from global memory (16 bytes per lane; the four waves' repeats of a row hit L1); a K tail is
-//    zero-filled on both sides, so any K % 8 == 0 works (the adapter's K = C / 4 = 80);
+//    16-byte fragments in load order — one contiguous 1 KiB wave-instruction each, L2-resident); the A tile is
+//    LDS-DMA'd (see the K loop below); a K tail is zero-filled on both sides, so any K % 8 == 0 works (the
+//    adapter's K = C / 4 = 80);
 //  * epilogue: + bias + residual in f32, rounded to 16 bits (X, as the unfused GEMM stores it), row sums
 //    over the lane's columns -> 4 lanes of a row (xor 16 / 32) -> the 4 waves through LDS; mean, then the
 //    centred sum of squares the same way (two passes, as layernorm_vec), H = (x - mean) rstd gamma + beta.
@@ -45,57 +45,132 @@ __global__ __launch_bounds__(256) void gemm_ln_pack(const T* __restrict__ W, int
   out[id] = v;
 }
 
+static __device__ __attribute__((aligned(16))) uint4 g_zero_ln[4];   // DMA source of A's K tail / rows past M
+typedef __attribute__((address_space(3))) void* las_ptr;
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+}
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// K loop (round 5, second form): the A tile (BM rows x 64 k, 16-byte chunks XOR-swizzled by row on the
+// source address) LDS-DMA'd three K-steps ahead into a 3-deep ring, the W fragments (packed, one contiguous
+// 1 KiB wave-instruction each) double-buffered in registers two K-steps ahead, all from inline asm so hipcc's
+// waitcnt pass never drains the ring; one counted wait + barrier per K-step.  (The first form loaded the A
+// fragments straight from global memory with one step of prefetch: 63 us for the stage-3 proj against 48 for
+// GEMM + LayerNorm.)
 template <typename T, class C>
 __global__ __launch_bounds__(256, 2) void gemm_ln(const T* __restrict__ A, int M, int K, const char* __restrict__ pk,
                                                  const float* __restrict__ bias, const T* __restrict__ R,
                                                  const float* __restrict__ gamma, const float* __restrict__ beta,
                                                  float eps, T* __restrict__ X, T* __restrict__ Hn) {
   typedef v8_t<T> tx8;
-  constexpr int MB = C::MB, NBW = C::NBW, N = C::N;
-  __shared__ float red[2][4][C::BM];                   // per-wave row partials: sums, then centred squares
+  constexpr int MB = C::MB, NBW = C::NBW, N = C::N, BM = C::BM;
+  constexpr int ABYTES = BM * 128, DPW = BM * 8 / 256;     // A tile per K-step; DMA wave-instructions per wave
+  // the output rows are staged through LDS (row stride 2 N + 16 bytes: the 8-byte fragment-layout writes of a
+  // wave's 16 rows hit 16 distinct bank pairs) and leave as 16-byte row-contiguous stores — the fragment layout's
+  // own 8-byte stores (16 rows x 32 bytes per instruction) made the first forms 1.3x slower than GEMM + LN.  The
+  // stage overlays the A ring: it is written after the row-sum barrier, which every wave reaches after the
+  // vmcnt(0) that retires its last (clamped) ring DMA
+  constexpr int SROW = 2 * N + 16;
+  constexpr int SMEM = 3 * ABYTES > BM * SROW ? 3 * ABYTES : BM * SROW;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+  __shared__ float red[2][4][BM];                      // per-wave row partials: sums, then centred squares
+  char* const stage = smem;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(las_ptr)smem;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int m0 = blockIdx.x * C::BM, n0w = wave * (N / 4);
-  const int nks = (K + 31) / 32;
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * BM, n0w = wave * (N / 4);
+  const int nk = (K + 63) / 64;
 
-  const T* arow[MB];
+  // ---- A DMA: chunk q = 64 (wave + 4 j) + lane: row q / 8, LDS chunk q % 8 holds global chunk (q % 8) ^ (row & 7)
+  const char* zero = reinterpret_cast<const char*>(g_zero_ln);
+  const char* asrc[DPW];
+  int acol[DPW];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb) arow[mb] = A + (long)min(m0 + 16 * mb + fr, M - 1) * K + 8 * fq;
+  for (int j = 0; j < DPW; ++j) {
+    const int q = (wave + 4 * j) * 64 + lane, row = q >> 3, c = (q & 7) ^ (row & 7);
+    asrc[j] = m0 + row < M ? reinterpret_cast<const char*>(A + (long)(m0 + row) * K + c * 8) : nullptr;
+    acol[j] = c * 8;
+  }
+  auto dma_a = [&](int kt, int slot) {
+#pragma unroll
+    for (int j = 0; j < DPW; ++j)
+      dma16(asrc[j] && kt * 64 + acol[j] < K ? asrc[j] + kt * 128 : zero,
+            __builtin_amdgcn_readfirstlane(lds0 + slot * ABYTES + (wave + 4 * j) * 1024));
+  };
+  // ---- W fragments (two register sets, static indices: the loop is unrolled by two)
   const char* pkl = pk + (wave * NBW * 64 + lane) * 16;
-  auto load = [&](int ks, tx8 (&af)[MB], tx8 (&wf)[NBW]) __attribute__((always_inline)) {
-    const bool kin = 32 * ks + 8 * fq < K;
+  tx8 wf0[2][NBW], wf1[2][NBW];                        // the two sets: [ks][nb]
+  auto load_w = [&](int kt, tx8 (&w)[2][NBW]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      tx8 v = *reinterpret_cast<const tx8*>(arow[mb] + (kin ? 32 * ks : 0));
-      if (!kin) v = tx8{};
-      af[mb] = v;
-    }
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int nb = 0; nb < NBW; ++nb) wf[nb] = *reinterpret_cast<const tx8*>(pkl + (long)ks * C::PKS + nb * 1024);
+      for (int nb = 0; nb < NBW; ++nb)
+        asm volatile("global_load_dwordx4 %0, %1, off"
+                     : "=v"(w[ks][nb]) : "v"(pkl + (long)(2 * kt + ks) * C::PKS + nb * 1024) : "memory");
+  };
+  auto tie_w = [&](tx8 (&w)[2][NBW]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) asm volatile("" : "+v"(w[ks][nb]));
   };
   f32x4 acc[MB][NBW];
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const tx8 (&af)[MB], const tx8 (&wf)[NBW]) __attribute__((always_inline)) {
+  auto mma = [&](int slot, const tx8 (&w)[2][NBW]) __attribute__((always_inline)) {
+    const char* as = smem + slot * ABYTES;
 #pragma unroll
-    for (int mb = 0; mb < MB; ++mb)
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = mfma16x16x32(wf[nb], af[mb], acc[mb][nb]);
+      for (int mb = 0; mb < MB; ++mb) {
+        const int row = mb * 16 + fr;
+        const tx8 a = *reinterpret_cast<const tx8*>(as + row * 128 + (((ks * 4 + fq) ^ (row & 7)) << 4));
+#pragma unroll
+        for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = mfma16x16x32(w[ks][nb], a, acc[mb][nb]);
+      }
   };
-  // k loop, two register sets (static indices: the loop is unrolled by two), the next step's loads in flight
-  tx8 a0[MB], w0[NBW], a1[MB], w1[NBW];
-  load(0, a0, w0);
-  int ks = 0;
-  for (; ks + 2 <= nks; ks += 2) {
-    load(ks + 1, a1, w1);
-    mma(a0, w0);
-    if (ks + 2 < nks) load(ks + 2, a0, w0);
-    mma(a1, w1);
+  // prologue: A(0..2) in the ring, W(0) / W(1) in the two sets
+  dma_a(0, 0);
+  dma_a(min(1, nk - 1), 1);
+  dma_a(min(2, nk - 1), 2);
+  load_w(0, wf0);
+  load_w(min(1, nk - 1), wf1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tie_w(wf0);
+  tie_w(wf1);
+  __syncthreads();
+  // iteration kt: MFMAs of K-step kt (A slot kt % 3, W set kt & 1), then W(kt + 2) into that set and the DMA
+  // of A(kt + 3) into that slot; the counted wait leaves those in flight (W(kt + 1) and A(kt + 1) retired)
+  auto iter = [&](int kt, tx8 (&w)[2][NBW], tx8 (&wn)[2][NBW]) __attribute__((always_inline)) {
+    mma(kt % 3, w);
+    load_w(min(kt + 2, nk - 1), w);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of slot kt % 3 are done
+    __syncthreads();                                    // everybody's: the slot may be refilled
+    dma_a(min(kt + 3, nk - 1), kt % 3);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NBW + DPW) : "memory");
+    tie_w(wn);
+    __syncthreads();                                    // A(kt + 1) visible to every wave
+  };
+  int kt = 0;
+  for (; kt + 2 <= nk; kt += 2) {
+    iter(kt, wf0, wf1);
+    iter(kt + 1, wf1, wf0);
   }
-  if (ks < nks) mma(a0, w0);
+  if (kt < nk) iter(kt, wf0, wf1);
+  // the clamped tail loads / DMA (never used) retire; the ties keep hipcc from handing their registers to other
+  // values while those loads are still in flight (an asm load whose output is never read is dead to the compiler)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  tie_w(wf0);
+  tie_w(wf1);
 
   // ---- epilogue: lane (fr, fq) of (mb, nb) = row m0 + 16 mb + fr, columns n0w + 16 nb + 4 fq .. + 3
   float v[MB][NBW][4];
@@ -151,26 +226,49 @@ __global__ __launch_bounds__(256, 2) void gemm_ln(const T* __restrict__ A, int M
       }
   }
   row_reduce(q, 1);
+  // X (rounded) into the stage, then the rows leave 16 bytes per lane; H the same way through the same buffer
+  auto stage_put = [&](int mb, int nb, const T (&o)[4]) __attribute__((always_inline)) {
+    *reinterpret_cast<uint2*>(stage + (16 * mb + fr) * SROW + (n0w + 16 * nb + 4 * fq) * 2) = *reinterpret_cast<const uint2*>(o);
+  };
+  auto stage_store = [&](T* dst) __attribute__((always_inline)) {
+    constexpr int CPR = N / 8, NCH = BM * CPR;        // 16-byte chunks per row / per tile
+#pragma unroll
+    for (int it = 0; it < (NCH + 255) / 256; ++it) {
+      const int c = tid + 256 * it, row = c / CPR, cc = c % CPR;
+      if (c < NCH && m0 + row < M)
+        *reinterpret_cast<uint4*>(dst + (long)(m0 + row) * N + cc * 8) = *reinterpret_cast<const uint4*>(stage + row * SROW + cc * 16);
+    }
+  };
+  if (X) {
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb) {
+        T xo[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xo[e] = from_f<T>(v[mb][nb][e]);
+        stage_put(mb, nb, xo);
+      }
+    __syncthreads();
+    stage_store(X);
+    __syncthreads();                                   // the stage is rewritten with H next
+  }
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
-    const int m = m0 + 16 * mb + fr;
-    if (m >= M) continue;
     const float rstd = 1.0f / sqrtf(q[mb] * (1.0f / N) + eps);
 #pragma unroll
     for (int nb = 0; nb < NBW; ++nb) {
       const int n = n0w + 16 * nb + 4 * fq;
       const float4 g = *reinterpret_cast<const float4*>(gamma + n), b = *reinterpret_cast<const float4*>(beta + n);
       const float gg[4] = {g.x, g.y, g.z, g.w}, bv[4] = {b.x, b.y, b.z, b.w};
-      T xo[4], ho[4];
+      T ho[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        xo[e] = from_f<T>(v[mb][nb][e]);
-        ho[e] = from_f<T>((v[mb][nb][e] - mean[mb]) * rstd * gg[e] + bv[e]);
-      }
-      if (X) *reinterpret_cast<uint2*>(X + (long)m * N + n) = *reinterpret_cast<const uint2*>(xo);
-      *reinterpret_cast<uint2*>(Hn + (long)m * N + n) = *reinterpret_cast<const uint2*>(ho);
+      for (int e = 0; e < 4; ++e) ho[e] = from_f<T>((v[mb][nb][e] - mean[mb]) * rstd * gg[e] + bv[e]);
+      stage_put(mb, nb, ho);
     }
   }
+  __syncthreads();
+  stage_store(Hn);
 }
 
 template <typename T, class C>

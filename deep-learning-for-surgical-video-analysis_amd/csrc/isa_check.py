@@ -92,7 +92,7 @@ def check_packed(funcs):
 
 
 VMEM_RE = re.compile(r"(global_|buffer_|flat_|scratch_)")
-ASM_LOAD_KERNELS = ("gemm_pk", "dwfc2_rw")          # kernels whose global loads are issued from inline asm
+ASM_LOAD_KERNELS = ("gemm_pk", "dwfc2_rw", "gemm_ln")          # kernels whose global loads are issued from inline asm
 VMCNT_RE = re.compile(r"vmcnt\((\d+)\)")
 
 

@@ -237,8 +237,11 @@ def layernorm(x, gamma, beta, eps, out=None):
     return out
 
 
-# off by default until it beats the unfused pair (first form: direct global A-fragment loads, one step of
-# prefetch — 63 us against 32 + 16 for proj + LayerNorm; step 32.5k vs 34.0k, profiles/r05/gemm_ln_mx28_ab.txt)
+# off by default: it does not beat the unfused pair yet (second form, A LDS-DMA ring + staged row stores: stage-3
+# proj + norm2 52 us vs 35 + 15, shared MLP + norm1 47 vs 24 + 16; step 34.8k vs 35.7k same-box,
+# profiles/r05/gemm_ln_v2.txt) — it is one tile per workgroup, where gemm_pk is persistent and overlaps a tile's
+# epilogue with the next tile's loads; turning it on cuts the replayed step from 192 to 174 launches
+# (profiles/r05/gemm_ln_mx28_ab.txt)
 GEMM_LN = os.environ.get("SVK_GEMM_LN", "0") == "1"
 
 

@@ -260,11 +260,12 @@ def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N, mx, monkeypatch):
 @pytest.mark.parametrize("M,N,K,res,bias", [(50176, 320, 320, True, True), (12544, 512, 512, True, True),
                                             (1000, 320, 80, True, True), (77, 512, 128, True, False),
                                             (130, 320, 40, False, True)])
-def test_gemm_ln(cuda, dt, M, N, K, res, bias):
+def test_gemm_ln(cuda, dt, M, N, K, res, bias, monkeypatch):
     """svk_gemm_ln (proj / shared-MLP GEMM + bias + residual + LayerNorm over the full row, packed weights)
     against the unfused svk path (gemm, then layernorm of its rounded output: X bit-identical up to the MFMA
     summation order, H within a few 16-bit ulps) and fp64; ragged M, K tails (80, 40: zero-filled fragments)."""
     from svk import ops
+    monkeypatch.setattr(ops, "GEMM_LN", True)
     a = _rand(M, K, dt=dt, dev=cuda, seed=81)
     w = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=82)
     b = _rand(N, dt=torch.float32, dev=cuda, scale=0.1, seed=83) if bias else None
