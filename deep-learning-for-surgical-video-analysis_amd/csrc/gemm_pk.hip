@@ -92,6 +92,20 @@ __device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_dst) {
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
 }
+// the same from an SGPR base + 32-bit per-lane VGPR offset (dense operands without a K tail, round 5): the
+// per-lane offsets are computed once per tile and the K-step advance is a scalar add on the base, so a DMA costs
+// no vector address arithmetic (the 64-bit form spent ~8 VALU per DMA instruction on it: gemm_pk issued 6.6 VALU
+// per MFMA, 27 us of VALU per SIMD in the 76 us stage-3 fc1, profiles/r05/gemm_fc1_pmc.txt)
+__device__ __forceinline__ void dma16s(const char* sbase, uint32_t voff, uint32_t lds_dst) {
+  const uint64_t b = reinterpret_cast<uint64_t>(sbase);
+  // (readfirstlane returns int: widen through uint32_t — a sign-extended low word would corrupt the high one)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  sbase = reinterpret_cast<const char*>(((uint64_t)hi << 32) | (uint64_t)lo);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(voff), "s"(sbase), "s"(lds_dst) : "memory");
+}
 __device__ __forceinline__ void barrier_mem() { asm volatile("s_barrier" ::: "memory"); }
 // Epilogue operand loads hidden from hipcc's waitcnt pass (see epi_load): completion is covered by the
 // counted wait of the tile's last step.
@@ -137,6 +151,10 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int dia
   // this thread's DMA lane covers 16-byte chunk q = (wave * LD + i) * 64 + lane of the stage image
   // ASRC == 1: im2col rows of this thread's A slots (output pixel -> first input tap), per tile
   int crb[Cfg::A_LD], ciy[Cfg::A_LD], cix[Cfg::A_LD];
+  // dense, no K tail: per-lane byte offsets of this thread's A / W chunks within the current issue tile
+  // (32-bit: the host routes operands of 4 GiB or more to the KTAIL instantiation)
+  constexpr bool SOFF = ASRC == 0 && !KTAIL && !SPLIT && Cfg::BM * Cfg::BN <= 128 * 128;   // (bigger tiles: no registers left)
+  uint32_t offA[SOFF ? Cfg::A_LD : 1], offB[SOFF ? Cfg::B_LD : 1];
   // live == false: past the workgroup's last (tile, K-step) — the same instructions run (branch-free
   // around the DMA issue) with every source replaced by the zero block
   auto issue = [&](int unit, int kt, int buf, bool live) {
@@ -170,6 +188,31 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int dia
         const char* src = ok && live ? reinterpret_cast<const char*>(A + crb[i] + ((long)iy * p.Wd + ix) * p.Cin + ci) : zero;
         dma16(src, __builtin_amdgcn_readfirstlane(sa + (wave * Cfg::A_LD + i) * 1024));
       }
+    } else if constexpr (SOFF) {
+      // a new tile's first K-step: the per-lane offsets; past the last unit (live == false) the last live tile's
+      // offsets stay and the DMA re-reads its K-step 0 into a stage nobody reads any more (in bounds, no select)
+      if (live && kt == 0) {
+#pragma unroll
+        for (int i = 0; i < Cfg::A_LD; ++i) {
+          const int q = (wave * Cfg::A_LD + i) * 64 + lane;
+          const int r = q >> 3, c = (q & 7) ^ (r & 7);
+          offA[i] = (uint32_t)min(m0 + r, p.M - 1) * (uint32_t)(p.lda * 2) + c * 16;
+        }
+#pragma unroll
+        for (int i = 0; i < Cfg::B_LD; ++i) {
+          const int q = (wave * Cfg::B_LD + i) * 64 + lane;
+          const int r = q >> 3, c = (q & 7) ^ (r & 7);
+          offB[i] = (uint32_t)min(n0 + r, p.N - 1) * (uint32_t)(p.ldw * 2) + c * 16;
+        }
+      }
+      const long kb = live ? (long)k0 * 2 : 0;
+#pragma unroll
+      for (int i = 0; i < Cfg::A_LD; ++i)
+        dma16s(reinterpret_cast<const char*>(A) + kb, offA[i], sa + (wave * Cfg::A_LD + i) * 1024);
+#pragma unroll
+      for (int i = 0; i < Cfg::B_LD; ++i)
+        dma16s(reinterpret_cast<const char*>(Wt) + kb, offB[i], sb + (wave * Cfg::B_LD + i) * 1024);
+      return;
     } else {
 #pragma unroll
       for (int i = 0; i < Cfg::A_LD; ++i) {
@@ -475,7 +518,10 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   if (g_tune[TUNE_PK_ELDS] >= 0) elds = g_tune[TUNE_PK_ELDS];
   // the staged epilogue swizzles 16-byte chunks within a power-of-two row of chunks, in one stage buffer
   elds = elds && Cfg::ELDS_FITS && (Cfg::BN & (Cfg::BN - 1)) == 0 && a.N % 8 == 0 && a.ldc % 8 == 0 && al16(a.C);
-  const bool tail = a.K % 64 != 0, ext = a.rscale || a.U;
+  // (the K-tail instantiation also takes operands whose byte offsets do not fit 32 bits: the dense no-tail path
+  // addresses its DMA as SGPR base + 32-bit lane offset)
+  const bool big = ASRC == 0 && ((long)a.M * a.lda * 2 >= 0xffffffffL || (long)a.N * a.ldw * 2 >= 0xffffffffL);
+  const bool tail = a.K % 64 != 0 || big, ext = a.rscale || a.U;
   // the extended (training) epilogue holds two more operand sets: with 8 waves or 3 stages it spills, so
   // it runs on the 4-wave two-stage 128 x 128 tile
   constexpr bool EXT_OK = Cfg::NT == 256 && Cfg::NSTAGE == 2 && Cfg::BM * Cfg::BN <= 128 * 128;
