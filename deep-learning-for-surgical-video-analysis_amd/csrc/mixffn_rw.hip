@@ -334,6 +334,291 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
   }
 }
 
+// ---- second form of the whole stage-1 MixFFN: the depthwise taps as f16-pair dot products.
+// The hidden window is kept as f16 PAIRS of vertically adjacent rows, P_y[c] = (h[y][c], h[y+1][c]) in one
+// VGPR per channel, so output row y is, per channel and horizontal offset dx,
+//   dot2(P_{y-1}, (t[0][dx], t[1][dx])) + dot2(P_y, (0, t[2][dx]))
+// — six v_dot2c_f32_f16 (horizontal shift through the DPP source, as taps3) instead of nine v_fmac_f32, a
+// 2-row window of 32 VGPRs instead of 48 f32, and 96 tap dwords per row from LDS instead of 144.  The new
+// row's pair P_{y+1} = (hi(P_y), f16(fc1)) replaces P_{y-1} once its n-tile's dwconv has read it.  The
+// products of the f16 hidden values and f16 taps are exact in f32 (the conv of the reference's autocast
+// in f16 with f32 accumulation); only the summation order differs from the f32-FMA form.
+template <int C_, int W_, int R_, int OCC_>
+struct DCfg {
+  static constexpr int C = C_, W = W_, R = R_, OCC = OCC_;
+  static constexpr int HID = 4 * C, NW = HID / 64, NT = 64 * NW;
+  static constexpr int KS = C / 32, NC2 = C / 16, XT = (W + 13) / 14;
+  static constexpr int TPW = 16 / NW, LPT = 64 / TPW;
+  static constexpr int SROW = C + 4, SLAB = 16 * SROW;
+  static constexpr int TBLK = 112;                  // tap block (wave, n-tile, fq): [4 ch][6] f16 pairs, dwb [4] f32
+  static constexpr int LDS_TP = HID * 4;             // b1 (f32) | tap blocks | b2, gamma, beta | slabs
+  static constexpr int LDS_EP = LDS_TP + NW * 16 * TBLK;
+  static constexpr int LDS_T = LDS_EP + 3 * C * 4;
+  static constexpr int LDS = LDS_T + 2 * NW * SLAB * 4;
+  static_assert(C % 32 == 0 && NW >= 1 && NW <= 4 && LPT * 4 == C && R % 2 == 0, "shape");
+};
+
+// acc0/1 (channels c0, c1) += the 3x3 taps: p = P_{y-1}, q = P_y pairs; t = [c0: T01 dx0..2, T2 dx0..2,
+// c1: the same], T01 = (t[0][dx], t[1][dx]), T2 = (0, t[2][dx]).  The four centre products go first: they
+// give the DPP reads the two wait states a VALU write of p / q needs.
+__device__ __forceinline__ void taps_d2(float& a0, float& a1, uint32_t p0, uint32_t p1, uint32_t q0, uint32_t q1,
+                                        const uint32_t (&t)[12]) {
+  asm("v_dot2c_f32_f16 %0, %2, %7\n\t"
+      "v_dot2c_f32_f16 %1, %3, %13\n\t"
+      "v_dot2c_f32_f16 %0, %4, %10\n\t"
+      "v_dot2c_f32_f16 %1, %5, %16\n\t"
+      "v_dot2c_f32_f16_dpp %0, %2, %6 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %1, %3, %12 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %0, %4, %9 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %1, %5, %15 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %0, %2, %8 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %1, %3, %14 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %0, %4, %11 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+      "v_dot2c_f32_f16_dpp %1, %5, %17 row_shl:1 row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(a0), "+v"(a1)
+      : "v"(p0), "v"(p1), "v"(q0), "v"(q1), "v"(t[0]), "v"(t[1]), "v"(t[2]), "v"(t[3]), "v"(t[4]), "v"(t[5]),
+        "v"(t[6]), "v"(t[7]), "v"(t[8]), "v"(t[9]), "v"(t[10]), "v"(t[11]));
+}
+
+__device__ __forceinline__ uint32_t hpair(uint32_t lo_from_hi, float v) {   // (hi half of lo_from_hi, f16(v))
+  return __builtin_bit_cast(uint32_t, h2{__builtin_bit_cast(h2, lo_from_hi).y, (f16)v});
+}
+
+template <class K>
+__global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rwd(const f16* __restrict__ XN, const f16* __restrict__ X,
+                                                       const f16* __restrict__ W1, const float* __restrict__ b1,
+                                                       const float* __restrict__ taps, const float* __restrict__ dwb,
+                                                       const f16* __restrict__ W2, const float* __restrict__ b2,
+                                                       f16* __restrict__ Y, f16* __restrict__ Yn,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float eps, int H, int nstrip, int total) {
+  constexpr int C = K::C, W = K::W, R = K::R, HID = K::HID, KS = K::KS, NC2 = K::NC2, NW = K::NW;
+  extern __shared__ __attribute__((aligned(16))) uint4 smem4[];
+  char* const smem = reinterpret_cast<char*>(smem4);
+  float* const slab0 = reinterpret_cast<float*>(smem + K::LDS_T);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+
+  // ---- prologue (as mixffn_rw; the tap blocks hold f16 pairs): block blk = (w * 4 + j) * 4 + fq holds
+  // channels 4 blk + i: dwords 6 i + s, s < 3: (t[0][s], t[1][s]), s >= 3: (0, t[2][s - 3]); then dwb [4] f32
+  for (int e = tid; e < HID; e += K::NT) reinterpret_cast<float*>(smem)[e] = b1[e];
+  for (int e = tid; e < NW * 16 * 28; e += K::NT) {
+    const int blk = e / 28, r = e % 28;
+    uint32_t v;
+    if (r < 24) {
+      const int i = r / 6, s = r % 6, dx = s % 3, ch = 4 * blk + i;
+      const f16 lo = s < 3 ? (f16)taps[dx * HID + ch] : (f16)0.f;
+      const f16 hi = s < 3 ? (f16)taps[(3 + dx) * HID + ch] : (f16)taps[(6 + dx) * HID + ch];
+      v = __builtin_bit_cast(uint32_t, h2{lo, hi});
+    } else {
+      v = __float_as_uint(dwb[4 * blk + r - 24]);
+    }
+    reinterpret_cast<uint32_t*>(smem + K::LDS_TP + blk * K::TBLK)[r] = v;
+  }
+  f16x8 w1f[4][KS], w2f[2][NC2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+      w1f[j][ks] = *reinterpret_cast<const f16x8*>(W1 + (long)(64 * w + 16 * j + fr) * C + 32 * ks + 8 * fq);
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int c = 0; c < NC2; ++c) {
+      const f16* src = W2 + (long)(16 * c + fr) * HID + 64 * w + 32 * q + 4 * fq;
+      const f16x4 lo = *reinterpret_cast<const f16x4*>(src), hi = *reinterpret_cast<const f16x4*>(src + 16);
+      w2f[q][c] = f16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  float* const sEp = reinterpret_cast<float*>(smem + K::LDS_EP);
+  for (int e = tid; e < 3 * C; e += K::NT)
+    sEp[e] = e < C ? b2[e] : (gamma ? (e < 2 * C ? gamma[e - C] : beta[e - 2 * C]) : (e < 2 * C ? 1.f : 0.f));
+  const int et = K::TPW * w + lane / K::LPT, ec = lane % K::LPT;
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  const float* b1l = reinterpret_cast<const float*>(smem) + 64 * w + 4 * fq;
+  const char* tpb = smem + K::LDS_TP + (w * 16 + fq) * K::TBLK;   // + j * 4 * TBLK
+  const int G = gridDim.x;
+  int buf = 0;
+  for (int u = xcd_remap(blockIdx.x, G); u < total; u += G) {
+    const int xt = u % K::XT, rest = u / K::XT, sidx = rest % nstrip, b = rest / nstrip;
+    const int y0 = sidx * R, x0 = 14 * xt;
+    const int tx = x0 - 1 + fr;
+    const bool xok = tx >= 0 && tx < W;
+    const f16* XNb = XN + (long)b * H * W * C + (long)min(max(tx, 0), W - 1) * C + 8 * fq;
+    auto load_x = [&](int yy, f16x8 (&xf)[KS]) __attribute__((always_inline)) {
+      const f16* src = XNb + (long)min(max(yy, 0), H - 1) * W * C;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) xf[ks] = *reinterpret_cast<const f16x8*>(src + 32 * ks);
+    };
+    auto fc1_mma = [&](const f16x8 (&xf)[KS], f32x4 (&a)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = *reinterpret_cast<const f32x4*>(b1l + 16 * j);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) a[j] = mfma16x16x32(w1f[j][ks], xf[ks], a[j]);
+      }
+    };
+    const bool edge = x0 == 0 || x0 + 15 > W;
+    // hidden row yy of n-tile j as f32 values zeroed outside the image: a wave-uniform branch (the empty
+    // volatile asm keeps hipcc from if-converting it into two selects per value on every row), one select
+    // per value on the edge tiles and the rows beyond the map
+    auto fc1_val = [&](int yy, const f32x4& a, float (&hv)[4]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) hv[c] = a[c];
+      if (edge || yy < 0 || yy >= H) {
+        asm volatile("");
+        const bool ok = xok && yy >= 0 && yy < H;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) hv[c] = ok ? hv[c] : 0.f;
+      }
+    };
+    uint32_t P[2][4][4];          // the two pair rows; at row r: P_{y-1} in slot r % 2, P_y in slot (r + 1) % 2
+    {
+      f16x8 xa[KS], xb[KS], xc[KS];
+      f32x4 a[4];
+      load_x(y0 - 1, xa);
+      load_x(y0, xb);
+      load_x(y0 + 1, xc);
+      fc1_mma(xa, a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float hv[4];
+        fc1_val(y0 - 1, a[j], hv);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) P[1][j][c] = hpair(0u, hv[c]);          // (0, h[y0-1])
+      }
+      fc1_mma(xb, a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float hv[4];
+        fc1_val(y0, a[j], hv);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) P[0][j][c] = hpair(P[1][j][c], hv[c]);   // (h[y0-1], h[y0])
+      }
+      fc1_mma(xc, a);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float hv[4];
+        fc1_val(y0 + 1, a[j], hv);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) P[1][j][c] = hpair(P[0][j][c], hv[c]);   // (h[y0], h[y0+1])
+      }
+    }
+    f16x8 xn[KS];
+    load_x(y0 + 2, xn);
+    const int etx = x0 - 1 + et;
+    const bool eok = et >= 1 && et <= 14 && etx < W;
+    const long eoff0 = ((long)b * H * W + min(max(etx, 0), W - 1)) * C + 4 * ec;
+    auto epilogue = [&](int yy, uint2 res, int bb) __attribute__((always_inline)) {
+      float4 v = *reinterpret_cast<const float4*>(slab0 + bb * NW * K::SLAB + et * K::SROW + 4 * ec);
+#pragma unroll
+      for (int ww = 1; ww < NW; ++ww) {
+        const float4 o = *reinterpret_cast<const float4*>(slab0 + (bb * NW + ww) * K::SLAB + et * K::SROW + 4 * ec);
+        v.x += o.x; v.y += o.y; v.z += o.z; v.w += o.w;
+      }
+      const f32x2 r01 = unpack2<f16>(res.x), r23 = unpack2<f16>(res.y);
+      const float4 eb2 = *reinterpret_cast<const float4*>(sEp + 4 * ec);
+      const f16 o0 = (f16)(v.x + eb2.x + r01.x), o1 = (f16)(v.y + eb2.y + r01.y);
+      const f16 o2 = (f16)(v.z + eb2.z + r23.x), o3 = (f16)(v.w + eb2.w + r23.y);
+      const bool st = eok && yy < H;
+      const long oo = eoff0 + (long)yy * W * C;
+      if (Y && st) *reinterpret_cast<f16x4*>(Y + oo) = f16x4{o0, o1, o2, o3};
+      if (gamma) {
+        const float f0 = o0, f1 = o1, f2 = o2, f3 = o3;
+        float sm = f0 + f1 + f2 + f3;
+#pragma unroll
+        for (int m = K::LPT / 2; m >= 1; m >>= 1) sm += __shfl_xor(sm, m, 64);
+        const float mean = sm * (1.0f / C);
+        const float d0 = f0 - mean, d1 = f1 - mean, d2 = f2 - mean, d3 = f3 - mean;
+        float q = d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
+#pragma unroll
+        for (int m = K::LPT / 2; m >= 1; m >>= 1) q += __shfl_xor(q, m, 64);
+        const float rstd = 1.0f / sqrtf(q * (1.0f / C) + eps);
+        const float4 egam = *reinterpret_cast<const float4*>(sEp + C + 4 * ec);
+        const float4 ebet = *reinterpret_cast<const float4*>(sEp + 2 * C + 4 * ec);
+        if (st)
+          *reinterpret_cast<f16x4*>(Yn + oo) = f16x4{(f16)(d0 * rstd * egam.x + ebet.x), (f16)(d1 * rstd * egam.y + ebet.y),
+                                                     (f16)(d2 * rstd * egam.z + ebet.z), (f16)(d3 * rstd * egam.w + ebet.w)};
+      }
+    };
+    // taps of n-tile j, channel half hf (channels 2 hf, 2 hf + 1): 12 dwords
+    auto tload = [&](int jh, uint32_t (&t)[12]) __attribute__((always_inline)) {
+      const uint4* src = reinterpret_cast<const uint4*>(tpb + (jh >> 1) * 4 * K::TBLK + (jh & 1) * 48);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const uint4 v = src[i];
+        t[4 * i] = v.x; t[4 * i + 1] = v.y; t[4 * i + 2] = v.z; t[4 * i + 3] = v.w;
+      }
+    };
+    uint2 res_prev = {0u, 0u};
+    f32x4 a2[NC2];
+    // one row (software-pipelined as mixffn_rw): the fc1 MFMAs of hidden row y + 2 and the X row of y + 3;
+    // the previous row's fc2 sums to the slab (their MFMAs retired a whole dwconv ago) and its epilogue
+    // behind the barrier that publishes them; then per n-tile the taps, the new pair row, GELU and (every
+    // second n-tile) a k-step of fc2
+    auto row = [&](int r, auto ROT_) __attribute__((always_inline)) {
+      constexpr int S0 = decltype(ROT_)::value, S1 = S0 ^ 1;   // P_{y-1} in slot S0, P_y in S1
+      const int y = y0 + r;
+      const uint2 res = *reinterpret_cast<const uint2*>(X + eoff0 + (long)min(y, H - 1) * W * C);
+      f32x4 a1[4];
+      fc1_mma(xn, a1);
+      load_x(y + 3, xn);
+      __builtin_amdgcn_sched_barrier(0);
+      uint32_t tq[2][12];
+      tload(0, tq[0]);
+      if (r > 0) {
+        float* sl = slab0 + ((buf ^ 1) * NW + w) * K::SLAB;
+#pragma unroll
+        for (int c = 0; c < NC2; ++c) *reinterpret_cast<f32x4*>(sl + fr * K::SROW + 16 * c + 4 * fq) = a2[c];
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        epilogue(y - 1, res_prev, buf ^ 1);
+      }
+      f16x8 g[2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 db = *reinterpret_cast<const float4*>(tpb + j * 4 * K::TBLK + 96);
+        float acc[4] = {db.x, db.y, db.z, db.w};
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const int jh = 2 * j + hf;
+          if (jh + 1 < 8) tload(jh + 1, tq[(jh + 1) & 1]);
+          taps_d2(acc[2 * hf], acc[2 * hf + 1], P[S0][j][2 * hf], P[S0][j][2 * hf + 1], P[S1][j][2 * hf],
+                  P[S1][j][2 * hf + 1], tq[jh & 1]);
+        }
+        // n-tile j of the new pair row P_{y+1} = (h[y+1], h[y+2]) into the slot of P_{y-1}, which this
+        // n-tile's taps have just read
+        {
+          float hv[4];
+          fc1_val(y + 2, a1[j], hv);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) P[S0][j][c] = hpair(P[S1][j][c], hv[c]);
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)gelu_rw(acc[c]);
+        if (j & 1) {   // a complete 32-channel k-step of fc2
+#pragma unroll
+          for (int c = 0; c < NC2; ++c)
+            a2[c] = mfma16x16x32(w2f[j >> 1][c], g[j >> 1], j == 1 ? f32x4{0.f, 0.f, 0.f, 0.f} : a2[c]);
+        }
+      }
+      res_prev = res;
+      buf ^= 1;
+    };
+    for (int r = 0; r < R; r += 2) {
+      row(r, std::integral_constant<int, 0>{});
+      row(r + 1, std::integral_constant<int, 1>{});
+    }
+    {
+      float* sl = slab0 + ((buf ^ 1) * NW + w) * K::SLAB;
+#pragma unroll
+      for (int c = 0; c < NC2; ++c) *reinterpret_cast<f32x4*>(sl + fr * K::SROW + 16 * c + 4 * fq) = a2[c];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    epilogue(y0 + R - 1, res_prev, buf ^ 1);
+  }
+}
+
 // ---- MixFFN front half in the same register-window form: G = GELU(dwconv3x3(fc1(XN))) written to HBM
 // (stage 2, C = 128, hidden 512: the whole-MixFFN form would need 128 weight VGPRs per wave).  A wave owns
 // 64 hidden channels of a (frame, 14-column x-tile, R-row strip); a workgroup = 4 waves = 256 channels
@@ -479,7 +764,7 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
   }
 }
 
-template <class K>
+template <class K, bool D2 = false>
 static int launch(const void* XN, const void* X, const void* W1, const float* b1, const float* taps, const float* dwb,
                   const void* W2, const float* b2, void* Y, void* Yn, const float* gamma, const float* beta, float eps,
                   int B, int H, hipStream_t st) {
@@ -490,19 +775,25 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mixffn_rw<K>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              K::LDS);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(&mixffn_rw<K>), K::NT, K::LDS);
+    const void* fn;
+    if constexpr (D2) fn = reinterpret_cast<const void*>(&mixffn_rwd<K>);
+    else fn = reinterpret_cast<const void*>(&mixffn_rw<K>);
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, K::LDS);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, K::NT, K::LDS);
     slots = std::max(1, cus) * std::max(1, per);
     if (getenv("SVK_RW_VERBOSE")) fprintf(stderr, "mixffn_rw: %d CUs x %d workgroups, LDS %d B\n", cus, per, K::LDS);
   }
   if (total > 0x7fffffffL) { set_error("svk_mixffn_rw: too many strips"); return SVK_EINVAL; }
   static const int force = getenv("SVK_RW_GRID") ? atoi(getenv("SVK_RW_GRID")) : 0;   // debugging: grid size
   const int grid = (int)std::min<long>(total, force > 0 ? force : slots);
-  hipLaunchKernelGGL((mixffn_rw<K>), dim3(grid), dim3(K::NT), K::LDS, st, (const f16*)XN, (const f16*)X, (const f16*)W1,
-                     b1, taps, dwb, (const f16*)W2, b2, (f16*)Y, (f16*)Yn, gamma, beta, eps, H, nstrip, (int)total);
+  if constexpr (D2)
+    hipLaunchKernelGGL((mixffn_rwd<K>), dim3(grid), dim3(K::NT), K::LDS, st, (const f16*)XN, (const f16*)X, (const f16*)W1,
+                       b1, taps, dwb, (const f16*)W2, b2, (f16*)Y, (f16*)Yn, gamma, beta, eps, H, nstrip, (int)total);
+  else
+    hipLaunchKernelGGL((mixffn_rw<K>), dim3(grid), dim3(K::NT), K::LDS, st, (const f16*)XN, (const f16*)X, (const f16*)W1,
+                       b1, taps, dwb, (const f16*)W2, b2, (f16*)Y, (f16*)Yn, gamma, beta, eps, H, nstrip, (int)total);
   static char name[64];
-  if (!name[0]) snprintf(name, sizeof(name), "mixffn_rw<Cfg<%d, %d, %d>>", K::C, K::W, K::R);
+  if (!name[0]) snprintf(name, sizeof(name), "%s<Cfg<%d, %d, %d>>", D2 ? "mixffn_rwd" : "mixffn_rw", K::C, K::W, K::R);
   set_last_kernel(name);
   return check_launch("mixffn_rw");
 }
@@ -574,5 +865,8 @@ extern "C" int svk_mixffn_rw(int dtype, const void* XN, const void* X, const voi
   // strips of 28 rows (two per 56-row frame): measured 335 us vs 341 (14 rows), 342 (8 rows) at B = 256
   if (var == 1) return ffnrw::launch<ffnrw::Cfg<64, 56, 14, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
   if (var == 2) return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2, false>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
-  return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  // 3: the f32-FMA tap form (mixffn_rw); default: the f16-pair dot-product taps (mixffn_rwd), 310 vs 319 us
+  // (profiles/r05/mixffn_rwd.txt; its 3-waves-per-SIMD build spills and ran 440 us)
+  if (var == 3) return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  return ffnrw::launch<ffnrw::DCfg<64, 56, 28, 2>, true>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
 }

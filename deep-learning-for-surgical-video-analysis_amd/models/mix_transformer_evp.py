@@ -161,13 +161,23 @@ class Attention(nn.Module):
             p["bsr"] = self.sr.bias.detach().float().contiguous()
             p["gn"], p["bn"] = _ln_params(self.norm)
         p["wp_gln"] = ops.gemm_ln_pack(p["wp"])      # proj + residual + norm2 in one kernel (stages 3-4, 16-bit)
+        if self.sr_ratio == 1 and ops.MERGED_QKV:
+            # no sequence reduction (the last stage): q and kv read the same tokens, so one GEMM with the
+            # weights stacked [Wq; Wkv] produces q | k | v (one launch instead of two, and one wider GEMM)
+            bq, bkv = p["bq"], p["bkv"]
+            if (bq is None) != (bkv is None):
+                bq = torch.zeros(self.dim, device=p["wq"].device) if bq is None else bq
+                bkv = torch.zeros(2 * self.dim, device=p["wq"].device) if bkv is None else bkv
+            p["wqkv"] = torch.cat([p["wq"], p["wkv"]], 0).contiguous()
+            p["bqkv"] = None if bq is None else torch.cat([bq, bkv]).contiguous()
         return p
 
-    @get_local("attn")
-    def forward(self, x, H, W, residual=None):
+    def _qkv(self, x, p, H, W):
+        """(q, k, v) views [B, N(k), C] of x's projections (Attention.forward :94-112)."""
         B, N, C = x.shape
-        p = get_packed(self, x.dtype, self._pack)
-        x = x.contiguous()
+        if "wqkv" in p:
+            qkv = ops.gemm(x, p["wqkv"], p["bqkv"])                           # [B, N, 3C]: q | k | v
+            return qkv[:, :, :C], qkv[:, :, C:2 * C], qkv[:, :, 2 * C:]
         q = ops.gemm(x, p["wq"], p["bq"])
         if self.sr_ratio > 1:
             r = self.sr_ratio
@@ -177,7 +187,14 @@ class Attention(nn.Module):
         else:
             xs = x
         kv = ops.gemm(xs, p["wkv"], p["bkv"])                                # [B, Nk, 2C]: k | v
-        o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], self.num_heads, self.scale)
+        return q, kv[:, :, :C], kv[:, :, C:]
+
+    @get_local("attn")
+    def forward(self, x, H, W, residual=None):
+        p = get_packed(self, x.dtype, self._pack)
+        x = x.contiguous()
+        q, k, v = self._qkv(x, p, H, W)
+        o = ops.attention(q, k, v, self.num_heads, self.scale)
         return ops.gemm(o, p["wp"], p["bp"], residual=residual)
 
     def forward_ln(self, x, H, W, residual, ln):
@@ -186,17 +203,10 @@ class Attention(nn.Module):
         p = get_packed(self, x.dtype, self._pack)
         if p.get("wp_gln") is None or residual is None:
             return None
-        B, N, C = x.shape
+        C = x.shape[2]
         x = x.contiguous()
-        q = ops.gemm(x, p["wq"], p["bq"])
-        if self.sr_ratio > 1:
-            r = self.sr_ratio
-            xs = ops.conv2d_ln_nhwc(x.view(B, H, W, C), p["wsr"], r, r, 0, p["bsr"], p["gn"], p["bn"], self.norm.eps)
-            xs = xs.view(B, -1, C)
-        else:
-            xs = x
-        kv = ops.gemm(xs, p["wkv"], p["bkv"])
-        o = ops.attention(q, kv[:, :, :C], kv[:, :, C:], self.num_heads, self.scale)
+        q, k, v = self._qkv(x, p, H, W)
+        o = ops.attention(q, k, v, self.num_heads, self.scale)
         return ops.gemm_ln(o, p["wp_gln"], C, p["bp"], residual.contiguous(), ln[0], ln[1], ln[2])
 
     def block_fusable(self, x, H, W):

@@ -242,13 +242,22 @@ def layernorm(x, gamma, beta, eps, out=None):
 # profiles/r05/gemm_ln_v2.txt) — it is one tile per workgroup, where gemm_pk is persistent and overlaps a tile's
 # epilogue with the next tile's loads; turning it on cuts the replayed step from 192 to 174 launches
 # (profiles/r05/gemm_ln_mx28_ab.txt)
-GEMM_LN = os.environ.get("SVK_GEMM_LN", "0") == "1"
+# "auto" (default): only where the fused kernel measured faster than GEMM + LayerNorm — the stage-4 prompt
+# shared MLP + norm1 (N = 512, K = 128: 21.6 vs 24.8 us; the N = 320 and K = 512 shapes lose,
+# profiles/r05/gemm_ln_v2.txt); "1": every instantiated shape; "0": off
+GEMM_LN = os.environ.get("SVK_GEMM_LN", "auto")
+
+
+def _gemm_ln_on(N, K):
+    if GEMM_LN is True or GEMM_LN == "1":
+        return True
+    return GEMM_LN == "auto" and N == 512 and K <= 128
 
 
 def gemm_ln_pack(w):
     """Packed weight fragments for gemm_ln (svk_gemm_ln_pack), or None where (dtype, N, K) has no gemm_ln
     instantiation (N in {320, 512}, 16-bit, K % 8 == 0).  Pack once per weight set."""
-    if not GEMM_LN or w.dtype not in H16 or not w.is_cuda:
+    if w.dtype not in H16 or not w.is_cuda or not _gemm_ln_on(*w.shape):
         return None
     N, K = w.shape
     nbytes = _lib.load().svk_gemm_ln_packed_bytes(dtype_code(w.dtype), int(N), int(K))
@@ -310,6 +319,8 @@ def mixffn_supported(W, C):
 
 
 FUSED_ATTN_BLOCK = os.environ.get("SVK_FUSED_ATTN_BLOCK", "1") == "1"
+# stage 4 (no sequence reduction): q and kv as one GEMM over the stacked weights
+MERGED_QKV = os.environ.get("SVK_MERGED_QKV", "1") == "1"
 FUSED_PROMPT_LN = os.environ.get("SVK_FUSED_PROMPT_LN", "1") == "1"
 # C = 320 (stage 3) is available but off: at 256 VGPRs and 130 KB of LDS it runs one wave per SIMD and
 # cost 11 % of the whole step in a same-box A/B
