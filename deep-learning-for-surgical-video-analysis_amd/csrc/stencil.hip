@@ -744,6 +744,51 @@ __global__ void resize_bilinear_kernel(const T* __restrict__ X, long ldx, T* __r
   Y[((long)b * OH * OW + (long)oy * OW + ox) * ldy + c] = from_f<T>(v);
 }
 
+// ---- the head's four pyramid resizes in one launch (segformer_head.py:150-158: c4..c1 resized to the
+// c4 grid and concatenated along channels): a thread owns 8 channels of one output pixel of one level,
+// 16-byte loads of the four source pixels and one 16-byte store into the concatenated row; the blend is
+// resize_bilinear_kernel's expression, so the values are bit-identical to four resize_bilinear calls
+struct RsLevels {
+  const void* X[4];
+  long ldx[4];
+  int H[4], W[4], coff[5];   // coff[l]..coff[l+1]: level l's channels in the output row
+};
+
+template <typename T>
+__global__ void resize_multi_kernel(RsLevels L, int nl, T* __restrict__ Y, long ldy, int B, int OH, int OW) {
+  const int nq = L.coff[nl] / 8;
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)B * OH * OW * nq;
+  if (idx >= total) return;
+  const int q = (int)(idx % nq);
+  const long pix = idx / nq;
+  const int ox = (int)(pix % OW);
+  const long t = pix / OW;
+  const int oy = (int)(t % OH);
+  const int b = (int)(t / OH);
+  const int c0 = 8 * q;
+  int l = 0;
+#pragma unroll
+  for (int i = 1; i < 4; ++i) l += (i < nl && c0 >= L.coff[i]) ? 1 : 0;
+  const int H = L.H[l], W = L.W[l], c = c0 - L.coff[l];
+  const long ldx = L.ldx[l];
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  src_index(oy, H, OH, y0, y1, ly0, ly1);
+  src_index(ox, W, OW, x0, x1, lx0, lx1);
+  const T* base = static_cast<const T*>(L.X[l]) + (long)b * H * W * ldx + c;
+  typedef T v8 __attribute__((ext_vector_type(8)));
+  const v8 a = *reinterpret_cast<const v8*>(base + ((long)y0 * W + x0) * ldx);
+  const v8 bb = *reinterpret_cast<const v8*>(base + ((long)y0 * W + x1) * ldx);
+  const v8 cc = *reinterpret_cast<const v8*>(base + ((long)y1 * W + x0) * ldx);
+  const v8 d = *reinterpret_cast<const v8*>(base + ((long)y1 * W + x1) * ldx);
+  v8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    o[e] = from_f<T>(ly0 * (lx0 * to_f(a[e]) + lx1 * to_f(bb[e])) + ly1 * (lx0 * to_f(cc[e]) + lx1 * to_f(d[e])));
+  *reinterpret_cast<v8*>(Y + ((long)b * OH * OW + (long)oy * OW + ox) * ldy + c0) = o;
+}
+
 // ---- causal window unfold (adapter_transformer.py:336-343) ---------------------------------
 template <typename T>
 __global__ void window_unfold_kernel(const T* __restrict__ X, long ldx, const float* __restrict__ pos, T* __restrict__ Y,
@@ -1187,6 +1232,37 @@ extern "C" int svk_resize_bilinear(int dtype, const void* X, long ldx, void* Y, 
     hipLaunchKernelGGL((resize_bilinear_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, (const T*)X, ldx, (T*)Y,
                        ldy, B, H, W, C, OH, OW);
     return check_launch("resize_bilinear");
+  });
+}
+
+extern "C" int svk_resize_bilinear_multi(int dtype, int nl, const void* const* X, const long* ldx, const int* H,
+                                         const int* W, const int* C, void* Y, long ldy, int B, int OH, int OW,
+                                         void* stream) {
+  if (nl < 1 || nl > 4 || B < 0 || OH <= 0 || OW <= 0 || !X || !ldx || !H || !W || !C || !Y ||
+      (dtype != SVK_F16 && dtype != SVK_BF16)) {
+    set_error("svk_resize_bilinear_multi: bad args (1-4 levels, 16-bit)"); return SVK_EINVAL;
+  }
+  RsLevels L{};
+  L.coff[0] = 0;
+  for (int l = 0; l < nl; ++l) {
+    if (!X[l] || H[l] <= 0 || W[l] <= 0 || C[l] <= 0 || C[l] % 8 || ldx[l] < C[l] || ldx[l] % 8 ||
+        ((uintptr_t)X[l] & 15)) {
+      set_error("svk_resize_bilinear_multi: level %d needs C %% 8 == 0, ldx %% 8 == 0, 16-byte aligned", l);
+      return SVK_EINVAL;
+    }
+    L.X[l] = X[l]; L.ldx[l] = ldx[l]; L.H[l] = H[l]; L.W[l] = W[l];
+    L.coff[l + 1] = L.coff[l] + C[l];
+  }
+  if (ldy < L.coff[nl] || ldy % 8 || ((uintptr_t)Y & 15)) {
+    set_error("svk_resize_bilinear_multi: ldy must cover the levels' channels, ldy %% 8 == 0, Y 16-byte aligned");
+    return SVK_EINVAL;
+  }
+  if (B == 0) return SVK_OK;
+  const long n = (long)B * OH * OW * (L.coff[nl] / 8);
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((resize_multi_kernel<T>), grid1d(n), dim3(256), 0, (hipStream_t)stream, L, nl, (T*)Y, ldy, B,
+                       OH, OW);
+    return check_launch("resize_bilinear_multi");
   });
 }
 

@@ -105,11 +105,15 @@ class SegFormerHead(nn.Module):
         B = t4.shape[0]
         ctot = sum(t.shape[-1] for t, _, _ in outs)
         r = torch.empty(B, H4 * W4, ctot, device=t4.device, dtype=t4.dtype)
-        off = 0
-        for t, H, W in ((t4, H4, W4), (t3, H3, W3), (t2, H2, W2), (t1, H1, W1)):   # torch.cat order (:158)
-            C = t.shape[-1]
-            ops.resize_bilinear(t, H, W, H4, W4, out=r[:, :, off:off + C])
-            off += C
+        levels = ((t4, H4, W4), (t3, H3, W3), (t2, H2, W2), (t1, H1, W1))   # torch.cat order (:158)
+        if ops.RESIZE_MULTI and r.dtype in ops.H16 and all(t.shape[-1] % 8 == 0 for t, _, _ in levels):
+            ops.resize_bilinear_multi(levels, H4, W4, r)                         # the four resizes, one launch
+        else:
+            off = 0
+            for t, H, W in levels:
+                C = t.shape[-1]
+                ops.resize_bilinear(t, H, W, H4, W4, out=r[:, :, off:off + C])
+                off += C
         y = ops.gemm(r.view(B * H4 * W4, ctot), p["w"], p["b"], act="relu")
         x = ops.mean_rows(y, H4 * W4)                                            # [B, 2048] f32
         if return_features:

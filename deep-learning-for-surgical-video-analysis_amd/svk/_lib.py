@@ -32,6 +32,7 @@ SIGNATURES = {
     "svk_nchw_to_s2d": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_gauss5x5_s2d": [c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P],
     "svk_resize_bilinear": [c_int, P, c_long, P, c_long, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_resize_bilinear_multi": [c_int, c_int, P, P, P, P, P, P, c_long, c_int, c_int, c_int, P],
     "svk_mean_rows": [c_int, P, c_long, P, c_int, c_int, c_int, P],
     "svk_softmax_rows": [P, c_long, P, c_long, c_int, c_int, P],
     "svk_mstcn_layer": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, P],

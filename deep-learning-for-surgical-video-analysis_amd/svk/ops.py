@@ -6,6 +6,7 @@ launches on the current stream.  There is deliberately no CPU path: a CPU tensor
 is an error.
 """
 import collections
+import ctypes
 import os
 
 import torch
@@ -691,6 +692,28 @@ def resize_bilinear(x, H, W, OH, OW, out=None):
         out = torch.empty(B, OH * OW, C, device=x.device, dtype=x.dtype)
     _lib.call("svk_resize_bilinear", dtype_code(x.dtype), _p(x), x.stride(-2), _p(out), out.stride(-2), B, H, W, C,
               OH, OW, _stream())
+    return out
+
+
+RESIZE_MULTI = os.environ.get("SVK_RESIZE_MULTI", "1") == "1"
+
+
+def resize_bilinear_multi(levels, OH, OW, out):
+    """levels: [(x [B, H*W, C] 16-bit, H, W)] (1-4, C % 8 == 0, unit channel stride) resized to OH x OW and
+    written side by side along channels into out [B, OH*OW, >= sum C] (svk_resize_bilinear_multi, one
+    launch; bit-identical to one resize_bilinear per level)."""
+    n = len(levels)
+    X = (ctypes.c_void_p * n)(*[_p(t) for t, _, _ in levels])
+    ld = (ctypes.c_long * n)(*[t.stride(-2) for t, _, _ in levels])
+    Hs = (ctypes.c_int * n)(*[h for _, h, _ in levels])
+    Ws = (ctypes.c_int * n)(*[w for _, _, w in levels])
+    Cs = (ctypes.c_int * n)(*[t.shape[-1] for t, _, _ in levels])
+    for t, _, _ in levels:
+        _chk(t, "x", out.dtype)
+        if t.stride(-1) != 1:
+            raise _lib.SvkError("svk.resize_bilinear_multi: unit channel stride required")
+    _lib.call("svk_resize_bilinear_multi", dtype_code(out.dtype), n, X, ld, Hs, Ws, Cs, _p(out), out.stride(-2),
+              out.shape[0], OH, OW, _stream())
     return out
 
 

@@ -215,6 +215,13 @@ int svk_gauss5x5_reflect(int dtype_out, const float* X, void* Y, int B, int C, i
 int svk_resize_bilinear(int dtype, const void* X, long ldx, void* Y, long ldy, int B, int H, int W,
                         int C, int OH, int OW, void* stream);
 
+/* The head's pyramid resizes in one launch: nl (1-4) 16-bit levels X[l] ([B, H[l]*W[l], C[l]], row stride
+ * ldx[l], C[l] % 8 == 0) each resized as svk_resize_bilinear to OH x OW and written side by side (level l at
+ * channel offset C[0] + ... + C[l-1]) into Y [B, OH*OW, ldy].  Bit-identical to nl svk_resize_bilinear calls;
+ * replaces SegFormerHead's four resize() calls before the channel concat (segformer_head.py:150-158). */
+int svk_resize_bilinear_multi(int dtype, int nl, const void* const* X, const long* ldx, const int* H,
+                              const int* W, const int* C, void* Y, long ldy, int B, int OH, int OW, void* stream);
+
 /* Y[b, c] = mean_r X[b*R + r, c] (f32 out).  Replaces AdaptiveAvgPool2d + flatten
  * (segformer_head.py:167-169). */
 int svk_mean_rows(int dtype, const void* X, long ldx, float* Y, int B, int R, int C, void* stream);

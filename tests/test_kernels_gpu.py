@@ -530,6 +530,31 @@ def test_resize_bilinear(cuda, dt, H, OH):
     assert float(out[:, :, :C].abs().max()) == 0
 
 
+@pytest.mark.parametrize("dt", [d for d in DTS if d != torch.float32])
+@pytest.mark.parametrize("OH", [7, 4])
+def test_resize_bilinear_multi(cuda, dt, OH):
+    """The head's four resizes in one launch (svk_resize_bilinear_multi) equal four resize_bilinear calls
+    bit for bit, each level at its channel offset of the concatenated row (row stride beyond the levels,
+    one level a strided view)."""
+    from svk import ops
+    dims = [(7, 40), (14, 32), (28, 16), (56, 8)]
+    srcs = []
+    for i, (H, C) in enumerate(dims):
+        t = _rand(3, H * H, 2 * C if i == 1 else C, dt=dt, dev=cuda, seed=60 + i)
+        srcs.append((t[:, :, :C] if i == 1 else t, H, H))
+    ctot = sum(C for _, C in dims)
+    got = torch.full((3, OH * OH, ctot + 8), 7.0, device=cuda, dtype=dt)
+    ops.resize_bilinear_multi(srcs, OH, OH, got)
+    ref = torch.full_like(got, 7.0)
+    off = 0
+    for t, H, W in srcs:
+        C = t.shape[-1]
+        ops.resize_bilinear(t, H, W, OH, OH, out=ref[:, :, off:off + C])
+        off += C
+    torch.cuda.synchronize()
+    assert torch.equal(got.cpu(), ref.cpu())
+
+
 @pytest.mark.parametrize("dt", DTS)
 def test_mean_rows(cuda, dt):
     from svk import ops

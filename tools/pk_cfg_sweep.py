@@ -15,9 +15,10 @@ SHAPES = [  # (M, N, K, residual, what)
     (12544, 640, 320, False, "s3 kv"), (12544, 2048, 512, False, "s4 fc1"), (12544, 512, 2048, True, "s4 fc2"),
     (12544, 512, 512, True, "s4 q/proj"), (12544, 1024, 512, False, "s4 kv"), (12544, 2048, 1024, False, "head"),
     (200704, 512, 128, False, "s2 fc1"), (200704, 128, 512, True, "s2 fc2"), (200704, 128, 128, True, "s2 q/proj"),
-    (802816, 64, 64, True, "s1 q/proj"),
+    (802816, 64, 64, True, "s1 q/proj"), (50176, 320, 80, True, "s3 prompt"), (50176, 80, 80, False, "s3 plight"),
+    (12544, 1536, 512, False, "s4 qkv"),
 ]
-CFGS = [(-1, "auto"), (10, "128x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair"), (90, "wt256"), (91, "wt160"), (92, "wt128"), (93, "wt192")]
+CFGS = [(-1, "auto"), (10, "128x64"), (20, "64x128"), (30, "64x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"), (71, "ppPair"), (90, "wt256"), (91, "wt160"), (92, "wt128"), (93, "wt192")]
 
 
 def timeit(fn, reps):
@@ -60,7 +61,8 @@ def main():
                 ref = y
             err = float((y.float() - ref.float()).abs().max())
             ms = timeit(lambda: ops.gemm(a, w, b, residual=r, out=out), args.reps)
-            row.append(f"{name} {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF d={err:.1e}"
+            gbs = 2 * (M * K + N * K + M * N * (2 if res else 1)) / ms / 1e6
+            row.append(f"{name} {ms * 1e3:7.1f}us {2 * M * N * K / ms / 1e9:6.0f}TF {gbs:5.0f}GB/s d={err:.1e}"
                        + ("" if cfg < 70 or kname.startswith(("gemm_pp", "gemm_wt"))
                              else " (fallback)"))
         lib.svk_tune(b"pk_cfg", -1)
