@@ -376,7 +376,9 @@ __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
   return r;
 }
 
-template <typename T, class C>
+// GELU = false: the activation is the identity — the data gradient of a frozen MixFFN's DWConv + fc1
+// (svk/train.py: dX = (dwconv3x3ᵀ dU) W1, the transposed depthwise conv being the conv with flipped taps)
+template <typename T, class C, bool GELU = true>
 __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restrict__ Hm, const char* __restrict__ pk,
                                                                const float* __restrict__ b2, const T* __restrict__ R,
                                                                T* __restrict__ Y, int ntiles, int K) {
@@ -459,7 +461,7 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   auto gelu_store = [&](int gb) {
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
-      const f32x4 gv = gelu4(dacc[m]);
+      const f32x4 gv = GELU ? gelu4(dacc[m]) : dacc[m];
       const T o[4] = {from_f<T>(gv[0]), from_f<T>(gv[1]), from_f<T>(gv[2]), from_f<T>(gv[3])};
       const int s = (mb0 + m) * 16 + fr, cw = 16 * cb + 4 * fq;
       *reinterpret_cast<uint2*>(smem + C::G_OFF + gb * C::GBYTES + s * 128 + ((((cw >> 3) ^ (s & 7)) << 4) | ((cw & 4) << 1))) =
@@ -560,20 +562,21 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   }
 }
 
-template <typename T, class C>
+template <typename T, class C, bool GELU = true>
 static int launch(const void* H, const void* pk, const float* b2, const void* R, void* Y, int B, int K, hipStream_t st) {
   const long nt = (long)B * C::TILES_PER_FRAME;
   if (nt > 0x7fffffffL || (long)B * C::WI * C::WI * K > 0x7fffffffL) return SVK_EUNSUPPORTED;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dwfc2_rw<T, C>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              C::LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dwfc2_rw<T, C, GELU>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((dwfc2_rw<T, C>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H, (const char*)pk, b2,
-                     (const T*)R, (T*)Y, (int)nt, K);
+  hipLaunchKernelGGL((dwfc2_rw<T, C, GELU>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H, (const char*)pk,
+                     b2, (const T*)R, (T*)Y, (int)nt, K);
   static char name[64];
-  if (!name[0]) snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d, %d>>", type_name<T>(), C::N, C::WI);
+  if (!name[0])
+    snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d, %d>%s>", type_name<T>(), C::N, C::WI, GELU ? "" : ", identity");
   set_last_kernel(name);
   return check_launch("dw_fc2_mx");
 }
@@ -645,8 +648,19 @@ extern "C" int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float*
   });
 }
 
+extern "C" int svk_mixffn_dw_fc2_packed_act(int dtype, const void* H, const void* packed, const float* b2,
+                                            const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, int act,
+                                            void* stream);
+
 extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const float* b2, const void* R,
                                         void* Y, int B, int Himg, int Wimg, int K, int N, void* stream) {
+  return svk_mixffn_dw_fc2_packed_act(dtype, H, packed, b2, R, Y, B, Himg, Wimg, K, N, SVK_ACT_GELU, stream);
+}
+
+extern "C" int svk_mixffn_dw_fc2_packed_act(int dtype, const void* H, const void* packed, const float* b2,
+                                            const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, int act,
+                                            void* stream) {
+  if (act != SVK_ACT_GELU && act != SVK_ACT_NONE) { set_error("svk_mixffn_dw_fc2_packed: act must be GELU or NONE"); return SVK_EINVAL; }
   if (B < 0 || Himg <= 0 || Wimg <= 0 || !H || !packed || !b2 || !Y) { set_error("svk_mixffn_dw_fc2_packed: bad args"); return SVK_EINVAL; }
   if (Himg != Wimg || svk_mixffn_dw_fc2_packed_bytes(dtype, Wimg, N, K) == 0) {
     set_error("svk_mixffn_dw_fc2_packed: (dtype=%d, %dx%d, N=%d, K=%d) has no packed form", dtype, Himg, Wimg, N, K);
@@ -658,6 +672,11 @@ extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* pa
   if (B == 0) return SVK_OK;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
+    if (act == SVK_ACT_NONE) {
+      if (Wimg == 7) return dwrw::launch<T, dwrw::Cfg<512, 7>, false>(H, packed, b2, R, Y, B, K, st);
+      if (Wimg == 28) { set_error("svk_mixffn_dw_fc2_packed: no identity form for 28 x 28"); return SVK_EUNSUPPORTED; }
+      return dwrw::launch<T, dwrw::Cfg<320, 14>, false>(H, packed, b2, R, Y, B, K, st);
+    }
     if (Wimg == 7) return dwrw::launch<T, dwrw::Cfg<512, 7>>(H, packed, b2, R, Y, B, K, st);
     if (Wimg == 28) return dwrw::launch<T, dwrw::Cfg<128, 28>>(H, packed, b2, R, Y, B, K, st);
     return dwrw::launch<T, dwrw::Cfg<320, 14>>(H, packed, b2, R, Y, B, K, st);

@@ -465,12 +465,16 @@ def mixffn_dw_fc2_pack(taps, dbias, w2, W):
     return out
 
 
-def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None):
+def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu"):
     """fc2(GELU(dwconv3x3(h) + dbias)) + b2 (+ residual) with the GELU map kept on chip (svk_mixffn_dw_fc2):
     h [B, H, W, K] fc1 output (16-bit NHWC), taps [9, K] / dbias [K] f32 as DWConv packs them, w2 [N, K];
     returns [B, H * W, N].  Where the map has the matrix-core form (14 x 14 with N = 320, 7 x 7 with N = 512,
     28 x 28 with N = 128) it runs that,
-    from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form."""
+    from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form.
+    ``act="none"`` drops the GELU (matrix-core form only, 14 x 14 / 7 x 7): with flipped taps, zero dbias and
+    w2 = W1ᵀ it is the data gradient through a frozen DWConv + fc1 (svk/train.py)."""
+    if act not in ("gelu", "none"):
+        raise _lib.SvkError("svk.mixffn_dw_fc2: act must be 'gelu' or 'none'")
     if h.dtype not in H16:
         raise _lib.SvkError("svk.mixffn_dw_fc2: bf16 / f16 only")
     _chk(h, "h"); _chk(w2, "w2", h.dtype); _chk(residual, "residual", h.dtype)
@@ -486,10 +490,15 @@ def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None):
     if residual is not None and (residual.numel() != B * H * W * N or not residual.is_contiguous()):
         raise _lib.SvkError("svk.mixffn_dw_fc2: residual must be a contiguous [B, H*W, N] map")
     out = torch.empty(B, H * W, N, device=h.device, dtype=h.dtype)
-    if DWFC2_MX and packed is None:
+    if (DWFC2_MX or act == "none") and packed is None:
         packed = mixffn_dw_fc2_pack(taps, dbias, w2, W)
+    if act == "none" and packed is None:
+        raise _lib.SvkError(f"svk.mixffn_dw_fc2: no identity-activation form for {W} x {W}, N = {N}")
     t0 = _prof_begin()
-    if DWFC2_MX and packed is not None:
+    if act == "none":
+        _lib.call("svk_mixffn_dw_fc2_packed_act", dtype_code(h.dtype), _p(h), _p(packed), _p(b2), _p(residual),
+                  _p(out), B, H, W, K, N, 0, _stream())
+    elif DWFC2_MX and packed is not None:
         _lib.call("svk_mixffn_dw_fc2_packed", dtype_code(h.dtype), _p(h), _p(packed), _p(b2), _p(residual), _p(out),
                   B, H, W, K, N, _stream())
     else:

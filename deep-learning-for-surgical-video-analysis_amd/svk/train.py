@@ -41,6 +41,9 @@ TRAIN_UNPATCHIFY_SPLIT = os.environ.get("SVK_TRAIN_UNPATCHIFY_SPLIT", "1") == "1
 # conv data gradients (frozen patch embeds, handcrafted-prompt convs) as per-tap GEMM + col2im gather (A/B
 # switch; 0 = the transposed-conv gather GEMM over input pixels)
 TRAIN_COL2IM = os.environ.get("SVK_TRAIN_COL2IM", "1") == "1"
+# stages 3-4 (14 x 14 / C = 320, 7 x 7 / C = 512): the frozen DWConv + fc1 data gradient as ONE kernel — the
+# matrix-core dw_fc2 with flipped taps, no activation and W1ᵀ in place of W2 — instead of dwconv3x3 + GEMM
+TRAIN_DWFC_BWD = os.environ.get("SVK_TRAIN_DWFC_BWD", "1") == "1"
 TRAIN_FC1_DWCONV_C = tuple(int(c) for c in os.environ.get("SVK_TRAIN_FC1_DWCONV_C", "32,64,128").split(","))
 
 TRAINABLE = ("head", "prompt", "flow_encoder", "cross_attn_s3", "cross_attn_s4")
@@ -628,13 +631,33 @@ class EVPTrainStep:
                         pin.shape[1], pin.shape[2], pin.shape[3], h["k"], h["st"], h["k"] // 2,
                         residual=dhc[s - 1].view(pin.shape).contiguous())
 
+    def _dwfc_bwd_pack(self, b, H, W, C):
+        """The packed operands of the fused DWConv + fc1 data gradient for this block's map, or None where
+        the matrix-core dw_fc2 has no form for it (cached in the block's parameter dict)."""
+        key = ("dwfc_bwd", H, W)
+        if key not in b:
+            pk = None
+            if H == W and ops.mixffn_dw_fc2_supported(self.dt, W, C, b["w1T"].shape[1]):
+                pk = ops.mixffn_dw_fc2_pack(b["taps_flip"], b["zero"], b["w1T"], W)
+            if pk is not None and W == 28:
+                pk = None                                     # (no identity-activation form at 28 x 28)
+            b[key] = pk
+            b["zeroC"] = torch.zeros(C, device=self.dev, dtype=torch.float32)
+        return b[key]
+
     def _block_bwd(self, d, b, sb, B, H, W, C):
         """Data gradient through one frozen block (given d = dL/d out) -> dL/d xp."""
         N = H * W
         hid = sb["u"].shape[-1]
         du = ops.gemm(d, b["w2T"], row_scale=sb["mm"], rows_per=N, dact="gelu", dact_src=sb["u"].view(B, N, hid))
-        dh = ops.dwconv3x3(du.view(B, H, W, hid), b["taps_flip"], b["zero"]).view(B, N, hid)
-        dxn2 = ops.gemm(dh, b["w1T"])
+        pk = self._dwfc_bwd_pack(b, H, W, C) if TRAIN_DWFC_BWD and self.dt in ops.H16 else None
+        if pk is not None:
+            # dX = (dwconv3x3ᵀ dU) W1 in one kernel: the depthwise map never reaches HBM
+            dxn2 = ops.mixffn_dw_fc2(du.view(B, H, W, hid), b["taps_flip"], b["zero"], b["w1T"], b["zeroC"],
+                                     packed=pk, act="none").view(B, N, C)
+        else:
+            dh = ops.dwconv3x3(du.view(B, H, W, hid), b["taps_flip"], b["zero"]).view(B, N, hid)
+            dxn2 = ops.gemm(dh, b["w1T"])
         d1 = ops.layernorm_bwd(sb["x1"], dxn2, b["g2"], BLOCK_EPS, dres=d)
         do = ops.gemm(d1, b["wpT"], row_scale=sb["ma"], rows_per=N)
         kv = sb["kv"]

@@ -159,6 +159,12 @@ int svk_mixffn_dw_fc2_pack(int dtype, const float* taps, const float* dbias, con
                            void* packed, void* stream);
 int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const float* b2, const void* R, void* Y,
                              int B, int Himg, int Wimg, int K, int N, void* stream);
+/* The same with the activation chosen: act = SVK_ACT_GELU (svk_mixffn_dw_fc2_packed) or SVK_ACT_NONE, i.e.
+ * Y = (dwconv3x3(H) + dbias) W2^T + b2 (+ R) — with flipped taps, zero dbias and W2 = W1^T the data gradient of
+ * a frozen MixFFN's DWConv + fc1 (train_evp.py's backward through mix_transformer_evp.py:60-62, svk/train.py).
+ * 14 x 14 / N = 320 and 7 x 7 / N = 512 only for SVK_ACT_NONE. */
+int svk_mixffn_dw_fc2_packed_act(int dtype, const void* H, const void* packed, const float* b2, const void* R,
+                                 void* Y, int B, int Himg, int Wimg, int K, int N, int act, void* stream);
 
 /* GEMM + bias + residual + LayerNorm over the full output row in one kernel (csrc/gemm_ln.hip): X = A W^T + bias
  * (+ R) rounded to the 16-bit type, H = LayerNorm(X; gamma, beta, eps) — Block's x + proj(...) followed by norm2,

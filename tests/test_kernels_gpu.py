@@ -257,6 +257,34 @@ def test_mixffn_dw_fc2(cuda, dt, B, res, W, K, N, mx, monkeypatch):
 
 
 @pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,W,K,N", [(88, 14, 1280, 320), (5, 7, 2048, 512), (3, 14, 640, 320)])
+def test_mixffn_dw_fc2_identity(cuda, dt, B, W, K, N):
+    """The identity-activation form (svk_mixffn_dw_fc2_packed_act, act none) as the train step uses it: the
+    data gradient through a frozen DWConv + fc1, dX = dwconv3x3(dU, flipped taps) · W1, against the unfused
+    svk path (dwconv3x3 + gemm: the same roundings, within a few 16-bit ulps) and fp64 (the transposed
+    depthwise conv of the fp64 graph)."""
+    from svk import ops
+    du = _rand(B, W, W, K, dt=dt, dev=cuda, seed=91)
+    taps = _rand(9, K, dt=torch.float32, dev=cuda, scale=0.3, seed=92)
+    flip = taps.flip(0).contiguous()
+    zero, zc = torch.zeros(K, device=cuda), torch.zeros(N, device=cuda)
+    w1 = _rand(K, N, dt=dt, dev=cuda, scale=N ** -0.5, seed=93)          # fc1.weight [hid, C]
+    w1t = w1.t().contiguous()
+    pk = ops.mixffn_dw_fc2_pack(flip, zero, w1t, W)
+    got = ops.mixffn_dw_fc2(du, flip, zero, w1t, zc, packed=pk, act="none")
+    assert ops._last_kernel().startswith("dw_fc2_mx") and "identity" in ops._last_kernel(), ops._last_kernel()
+    dh = ops.dwconv3x3(du, flip, zero)
+    ref16 = ops.gemm(dh.view(B, W * W, K), w1t)
+    d = (got.float() - ref16.float()).abs().max().item()
+    assert d <= 4 * float(ref16.float().abs().max()) * (2 ** -8 if dt == torch.bfloat16 else 2 ** -11), d
+    # fp64: the adjoint of the forward depthwise conv (taps as the forward packs them) applied to dU
+    kf = taps.to(dt).double().cpu().t().reshape(K, 1, 3, 3)
+    dhd = F.conv_transpose2d(du.double().cpu().permute(0, 3, 1, 2), kf, padding=1, groups=K)
+    ref = dhd.permute(0, 2, 3, 1).reshape(B, W * W, K) @ w1.double().cpu()
+    _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("M,N,K,res,bias", [(50176, 320, 320, True, True), (12544, 512, 512, True, True),
                                             (1000, 320, 80, True, True), (77, 512, 128, True, False),
                                             (130, 320, 40, False, True)])
