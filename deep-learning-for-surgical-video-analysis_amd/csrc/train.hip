@@ -519,6 +519,21 @@ __global__ void keep_mask_kernel(float* __restrict__ out, long n, float keep, ui
   out[i] = u < keep ? 1.0f / keep : 0.f;
 }
 
+// nm masks of n floats each in one launch (mask m: keep[m], seed[m]); element (m, e) is the value
+// keep_mask_kernel gives element e of a mask with that keep / seed, bit for bit
+__global__ void keep_mask_multi_kernel(float* __restrict__ out, long n, int nm, const float* __restrict__ keeps,
+                                       const uint32_t* __restrict__ seeds, const long long* __restrict__ counter) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n * nm) return;
+  const int m = (int)(i / n);
+  const long e = i - (long)m * n;
+  uint32_t seed = seeds[m];
+  if (counter) seed = hash32(seed ^ hash32((uint32_t)*counter * 0x85EBCA6BU));
+  const float keep = keeps[m];
+  const float u = (hash32((uint32_t)e * 0x9E3779B9U ^ hash32(seed)) >> 8) * (1.0f / 16777216.0f);
+  out[i] = u < keep ? 1.0f / keep : 0.f;
+}
+
 // ---- phase losses: CrossEntropy(sum) + SmoothL1(sum) and their gradients (train_evp.py:390-391, 500-509)
 __global__ void phase_loss_kernel(const float* __restrict__ logits, const float* __restrict__ ant,
                                   const long* __restrict__ labels, const float* __restrict__ ant_t, int B, int K,
@@ -815,6 +830,15 @@ extern "C" int svk_keep_mask(float* out, long n, float keep, unsigned seed, cons
   if (n == 0) return SVK_OK;
   hipLaunchKernelGGL(keep_mask_kernel, g1(n), dim3(256), 0, (hipStream_t)stream, out, n, keep, (uint32_t)seed, counter);
   return check_launch("keep_mask");
+}
+
+extern "C" int svk_keep_mask_multi(float* out, long n, int nm, const float* keeps, const unsigned* seeds,
+                                   const long long* counter, void* stream) {
+  if (n < 0 || nm < 0 || (n * nm > 0 && (!out || !keeps || !seeds))) { set_error("svk_keep_mask_multi: bad args"); return SVK_EINVAL; }
+  if (n * nm == 0) return SVK_OK;
+  hipLaunchKernelGGL(keep_mask_multi_kernel, g1(n * nm), dim3(256), 0, (hipStream_t)stream, out, n, nm, keeps,
+                     (const uint32_t*)seeds, counter);
+  return check_launch("keep_mask_multi");
 }
 
 extern "C" int svk_phase_loss(const float* logits, const float* ant, const long* labels, const float* ant_t, int B,

@@ -105,6 +105,7 @@ SIGNATURES = {
     "svk_row_scale": [c_int, P, P, P, c_long, c_int, c_int, P],
     "svk_mul_f32": [P, P, P, c_long, P],
     "svk_keep_mask": [P, c_long, c_float, ctypes.c_uint, P, P],
+    "svk_keep_mask_multi": [P, c_long, c_int, P, P, P, P],
     "svk_phase_loss": [P, P, P, P, c_int, c_int, P, P, P, P],
     "svk_sgd": [P, P, P, c_long, c_float, c_float, c_float, c_float, c_int, c_int, P],
     "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],

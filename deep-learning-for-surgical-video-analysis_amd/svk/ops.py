@@ -1336,6 +1336,19 @@ def keep_mask(n, keep, seed, device, counter=None):
     return out
 
 
+def keep_mask_multi(n, keeps, seeds, counter=None):
+    """[len(keeps), n] f32: row m = keep_mask(n, keep, seed) for the m-th (keep, seed), bit for bit, in one
+    launch.  keeps: device f32 [nm] (the float32 values keep_mask would receive), seeds: device int32 [nm]
+    (the low 32 bits of the seeds)."""
+    _chk(keeps, "keeps", torch.float32); _chk(seeds, "seeds", torch.int32); _chk(counter, "counter", torch.int64)
+    nm = keeps.numel()
+    if seeds.numel() != nm or not (keeps.is_contiguous() and seeds.is_contiguous()):
+        raise _lib.SvkError("svk.keep_mask_multi: keeps / seeds must be contiguous [nm]")
+    out = torch.empty(nm, n, device=keeps.device, dtype=torch.float32)
+    _lib.call("svk_keep_mask_multi", _p(out), n, nm, _p(keeps), _p(seeds), _p(counter), _stream())
+    return out
+
+
 def phase_loss(logits, ant, labels, ant_targets):
     """CE(sum) + SmoothL1(sum) -> (loss f32 [2], dlogits, dant)."""
     for t, nm in ((logits, "logits"), (ant, "ant"), (ant_targets, "ant_targets")):

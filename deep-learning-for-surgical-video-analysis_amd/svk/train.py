@@ -44,6 +44,8 @@ TRAIN_COL2IM = os.environ.get("SVK_TRAIN_COL2IM", "1") == "1"
 # stages 3-4 (14 x 14 / C = 320, 7 x 7 / C = 512): the frozen DWConv + fc1 data gradient as ONE kernel — the
 # matrix-core dw_fc2 with flipped taps, no activation and W1ᵀ in place of W2 — instead of dwconv3x3 + GEMM
 TRAIN_DWFC_BWD = os.environ.get("SVK_TRAIN_DWFC_BWD", "1") == "1"
+# the step's DropPath masks in one launch (svk_keep_mask_multi) instead of one keep_mask launch per mask
+TRAIN_MASK_MULTI = os.environ.get("SVK_TRAIN_MASK_MULTI", "1") == "1"
 TRAIN_FC1_DWCONV_C = tuple(int(c) for c in os.environ.get("SVK_TRAIN_FC1_DWCONV_C", "32,64,128").split(","))
 
 TRAINABLE = ("head", "prompt", "flow_encoder", "cross_attn_s3", "cross_attn_s4")
@@ -149,6 +151,7 @@ class EVPTrainStep:
         self._setup_frozen()
         self._setup_packs()
         self.counter = torch.zeros(1, device=self.dev, dtype=torch.int64)   # device step count (mask RNG)
+        self._mask_cache = {}
         self.graph = self.graph_rest = self.graph_opt = None
         self._pending = None
 
@@ -355,12 +358,31 @@ class EVPTrainStep:
         dpr = torch.linspace(0, DROP_PATH_RATE, sum(self.depths)).tolist()
         blocks, cur = [], 0
         base = (self.seed * 1000003) & 0x7FFFFFFF      # the step enters through the device counter
-        ones = torch.ones(B, device=self.dev, dtype=torch.float32)
+        # constant per (B, schedule): the ones rows and the per-mask keep / seed tables, built once (eagerly,
+        # before any capture) so a replayed step holds no fill or copy nodes for them
+        key = ("mask_tables", B, self.drop, base)
+        if key not in self._mask_cache:
+            keeps, seeds = [], []
+            for k in range(sum(self.depths)):
+                if self.drop and dpr[k] > 0:
+                    for j in range(2):
+                        keeps.append(1.0 - dpr[k])
+                        seeds.append((base + 2 * k + j) & 0xFFFFFFFF)
+            kt = torch.tensor(keeps, dtype=torch.float32).to(self.dev)
+            st_ = torch.tensor([v - (1 << 32) if v >= 1 << 31 else v for v in seeds], dtype=torch.int32).to(self.dev)
+            self._mask_cache[key] = (torch.ones(B, device=self.dev, dtype=torch.float32), kt, st_)
+        ones, kt, st_ = self._mask_cache[key]
+        # every block's two DropPath masks in one launch (rows in block order), bit-identical to keep_mask
+        allm = ops.keep_mask_multi(B, kt, st_, self.counter) if kt.numel() and TRAIN_MASK_MULTI else None
+        mi = 0
         for s, d in enumerate(self.depths):
             st = []
             for i in range(d):
                 r = dpr[cur + i]
-                if self.drop and r > 0:
+                if self.drop and r > 0 and allm is not None:
+                    st.append((allm[mi], allm[mi + 1]))
+                    mi += 2
+                elif self.drop and r > 0:
                     st.append(tuple(ops.keep_mask(B, 1.0 - r, base + 2 * (cur + i) + j, self.dev, self.counter)
                                     for j in range(2)))
                 else:

@@ -546,6 +546,11 @@ int svk_mul_f32(const float* a, const float* b, float* y, long n, void* stream);
 /* Counter-based Bernoulli(keep) mask scaled by 1/keep (values 0 or 1/keep): DropPath / Dropout2d.
  * counter (device int64, may be NULL) is mixed into the seed at run time (graph replays). */
 int svk_keep_mask(float* out, long n, float keep, unsigned seed, const long long* counter, void* stream);
+/* nm keep masks of n floats each in one launch: out[m*n + e] is element e of svk_keep_mask(keeps[m], seeds[m])
+ * (keeps / seeds: device arrays of nm entries) — the step's DropPath masks (train_evp.py's drop_path_rate
+ * schedule over the blocks, mix_transformer_evp.py:150-171) without one launch per mask. */
+int svk_keep_mask_multi(float* out, long n, int nm, const float* keeps, const unsigned* seeds,
+                        const long long* counter, void* stream);
 
 /* CrossEntropyLoss(sum) + SmoothL1Loss(sum) (train_evp.py:390-391, 500-509): loss[0] += CE,
  * loss[1] += SmoothL1; dlogits / dant are the gradients of their sum. */

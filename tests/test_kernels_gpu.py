@@ -583,6 +583,20 @@ def test_resize_bilinear_multi(cuda, dt, OH):
     assert torch.equal(got.cpu(), ref.cpu())
 
 
+def test_keep_mask_multi(cuda):
+    """svk_keep_mask_multi (the train step's DropPath masks in one launch) equals one svk_keep_mask per mask bit
+    for bit, with and without the device step counter, seeds past 2^31 included."""
+    from svk import ops
+    keeps = [1.0 - r for r in (0.0125, 0.05, 0.3, 0.7, 0.9)]
+    seeds = [12345, 0x7FFFFFF0 + 17, 0xFFFFFFF0, 3, 0x80000001]
+    kt = torch.tensor(keeps, dtype=torch.float32).to(cuda)
+    st = torch.tensor([v - (1 << 32) if v >= 1 << 31 else v for v in seeds], dtype=torch.int32).to(cuda)
+    for counter in (None, torch.tensor([41], dtype=torch.int64, device=cuda)):
+        got = ops.keep_mask_multi(88, kt, st, counter)
+        for m, (k, sd) in enumerate(zip(keeps, seeds)):
+            assert torch.equal(got[m], ops.keep_mask(88, k, sd, cuda, counter)), m
+
+
 @pytest.mark.parametrize("dt", DTS)
 def test_mean_rows(cuda, dt):
     from svk import ops
