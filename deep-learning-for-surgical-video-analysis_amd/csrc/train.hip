@@ -467,6 +467,62 @@ __global__ void pack_params_kernel(const PackDesc* __restrict__ d, int nd, long 
   dst[e.dst + (i - e.start)] = from_f<T>(ok ? src[off] : 0.f);
 }
 
+// The same gather, 8 consecutive packed elements per thread: every descriptor starts at a multiple of 8 of the
+// linear index space (and of the packed buffer), so a thread's 8 elements share one descriptor; the 4-D index
+// is decomposed once and stepped, and the 8 values leave as one 16-byte store (two for f32).  Elements past a
+// tensor's end up to its 8-aligned slot end are written as zeros (the packed buffer's alignment padding).
+template <typename T>
+__global__ void pack_params8_kernel(const PackDesc* __restrict__ d, int nd, long total, const float* __restrict__ src,
+                                    T* __restrict__ dst) {
+  __shared__ int s_first;
+  const long blk0 = (long)blockIdx.x * blockDim.x * 8;
+  if (threadIdx.x == 0) {
+    int lo = 0, hi = nd - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (d[mid].start <= blk0) lo = mid; else hi = mid - 1;
+    }
+    s_first = lo;
+  }
+  __syncthreads();
+  const long i0 = blk0 + (long)threadIdx.x * 8;
+  if (i0 >= total) return;
+  int lo = s_first;
+  while (lo + 1 < nd && d[lo + 1].start <= i0) ++lo;
+  const PackDesc& e = d[lo];
+  const int numel = e.n[0] * e.n[1] * e.n[2] * e.n[3];
+  const int r0 = (int)(i0 - e.start);
+  if (r0 >= numel) return;
+  int idx[4];
+  {
+    int r = r0;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) { idx[k] = r % e.n[k]; r /= e.n[k]; }
+  }
+  T v[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float x = 0.f;
+    if (r0 + q < numel) {
+      const bool ok = idx[0] < e.lim[0] && idx[1] < e.lim[1] && idx[2] < e.lim[2] && idx[3] < e.lim[3];
+      if (ok) x = src[e.src + idx[0] * e.s[0] + idx[1] * e.s[1] + idx[2] * e.s[2] + idx[3] * e.s[3]];
+#pragma unroll
+      for (int k = 3; k >= 0; --k) {             // step the index: innermost first, with carry
+        if (++idx[k] < e.n[k]) break;
+        idx[k] = 0;
+      }
+    }
+    v[q] = from_f<T>(x);
+  }
+  T* out = dst + e.dst + r0;
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(out) = *reinterpret_cast<const uint4*>(v);
+  } else {
+    reinterpret_cast<uint4*>(out)[0] = *reinterpret_cast<const uint4*>(v);
+    reinterpret_cast<uint4*>(out)[1] = *reinterpret_cast<const uint4*>(v + 4);
+  }
+}
+
 // ---- transposed 2-D packs: one workgroup per 64 x 64 tile of a row-major [N, K] f32 master ----------
 struct PackTile {
   long src, dst;     // element offsets of the master matrix / the packed [K, N] view
@@ -918,6 +974,19 @@ extern "C" int svk_pack_transpose(int dtype, const void* tiles, int ntiles, cons
     hipLaunchKernelGGL((pack_transpose_kernel<T>), dim3((unsigned)ntiles), dim3(256), 0, (hipStream_t)stream,
                        (const PackTile*)tiles, src, (T*)dst);
     return check_launch("pack_transpose");
+  });
+}
+
+extern "C" int svk_pack_params8(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,
+                                void* stream) {
+  if (ndesc <= 0 || total < 0 || total % 8 || !desc || !src || !dst || ((uintptr_t)dst & 15)) {
+    set_error("svk_pack_params8: bad args (total %% 8 == 0, 16-byte aligned dst)"); return SVK_EINVAL;
+  }
+  if (total == 0) return SVK_OK;
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((pack_params8_kernel<T>), g1(total / 8), dim3(256), 0, (hipStream_t)stream,
+                       (const PackDesc*)desc, ndesc, total, src, (T*)dst);
+    return check_launch("pack_params8");
   });
 }
 

@@ -109,6 +109,7 @@ SIGNATURES = {
     "svk_phase_loss": [P, P, P, P, c_int, c_int, P, P, P, P],
     "svk_sgd": [P, P, P, c_long, c_float, c_float, c_float, c_float, c_int, c_int, P],
     "svk_pack_params": [c_int, P, c_int, c_long, P, P, P],
+    "svk_pack_params8": [c_int, P, c_int, c_long, P, P, P],
     "svk_pack_transpose": [c_int, P, c_int, P, P, P],
 }
 STRING_FUNCS = ("svk_version", "svk_last_error", "svk_last_kernel")

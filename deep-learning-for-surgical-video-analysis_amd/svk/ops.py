@@ -1372,6 +1372,11 @@ def pack_params(desc, ndesc, total, src, dst):
     _lib.call("svk_pack_params", dtype_code(dst.dtype), _p(desc), ndesc, total, _p(src), _p(dst), _stream())
 
 
+def pack_params8(desc, ndesc, total, src, dst):
+    """svk_pack_params8: descriptor starts and packed offsets 8-aligned, total % 8 == 0."""
+    _lib.call("svk_pack_params8", dtype_code(dst.dtype), _p(desc), ndesc, total, _p(src), _p(dst), _stream())
+
+
 def pack_transpose(tiles, ntiles, src, dst):
     _lib.call("svk_pack_transpose", dtype_code(dst.dtype), _p(tiles), ntiles, _p(src), _p(dst), _stream())
 

@@ -60,6 +60,8 @@ _TILE = np.dtype([("src", "<i8"), ("dst", "<i8"), ("K", "<i4"), ("N", "<i4"), ("
                   ("k0", "<i4")])         # csrc/train.hip PackTile
 # transposed weight packs through the tiled transpose kernel (A/B switch; 0 = the generic strided gather)
 PACK_TRANSPOSE = os.environ.get("SVK_PACK_TRANSPOSE", "1") == "1"
+# the generic gather 8 elements per thread (svk_pack_params8; 0 = one element per thread)
+PACK_PARAMS8 = os.environ.get("SVK_PACK_PARAMS8", "1") == "1"
 
 
 def is_trainable(name):
@@ -87,7 +89,7 @@ class _PackTable:
             self.trows.append((src, off, shape[0], shape[1]))      # [K, N] view of a row-major [N, K] master
         else:
             self.rows.append((src, off, n, s, lim, self.gtotal))
-            self.gtotal += numel
+            self.gtotal += (numel + 7) // 8 * 8    # 8-aligned descriptor starts: svk_pack_params8
         self.total += (numel + 7) // 8 * 8      # keep every packed tensor 16-byte aligned
         self.views.append((off, tuple(view or shape)))
         return len(self.views) - 1
@@ -109,7 +111,10 @@ class _PackTable:
     def run(self, master, dst=None):
         out = self.buf if dst is None else dst
         if self.rows:
-            ops.pack_params(self.desc, len(self.rows), self.gtotal, master, out)
+            if PACK_PARAMS8:
+                ops.pack_params8(self.desc, len(self.rows), self.gtotal, master, out)
+            else:
+                ops.pack_params(self.desc, len(self.rows), self.gtotal, master, out)
         if self.ntiles:
             ops.pack_transpose(self.tiles, self.ntiles, master, out)
 

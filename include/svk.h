@@ -567,6 +567,11 @@ int svk_sgd(float* p, const float* grad, float* buf, long n, float lr, float mom
  * {long src, dst; int n[4]; long s[4]; int lim[4]; long start} (see csrc/train.hip PackDesc). */
 int svk_pack_params(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,
                     void* stream);
+/* svk_pack_params with 8 packed elements per thread (one 16-byte store): every descriptor's start (in the
+ * linear index space) and its packed offset are multiples of 8, total % 8 == 0, dst 16-byte aligned; the
+ * elements between a tensor's end and its 8-aligned slot end are written as zeros. */
+int svk_pack_params8(int dtype, const void* desc, int ndesc, long total, const float* src, void* dst,
+                     void* stream);
 
 /* The transposed 2-D packs of the same refresh (dst[k * N + n] = src[n * K + k] for a row-major [N, K] f32
  * master matrix): tiles of 64 x 64 through LDS so both the master reads and the packed writes are
