@@ -811,6 +811,22 @@ extern "C" int svk_colstats(int dtype, const void* X, long ldx, int M, int C, fl
   });
 }
 
+extern "C" int svk_colstats_set(int dtype, const void* X, long ldx, int M, int C, float* sums, float* ws,
+                                void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (M == 0 && C > 0 && sums)   // no rows: zero sums (X and ws may be empty)
+    return hipMemsetAsync(sums, 0, sizeof(float) * 2 * C, st) == hipSuccess ? SVK_OK : SVK_ELAUNCH;
+  if (M < 0 || C <= 0 || !X || !sums || !ws) { set_error("svk_colstats_set: bad args"); return SVK_EINVAL; }
+  const int nb = stats_blocks(M);
+  SVK_DISPATCH_DTYPE(dtype, T, {
+    hipLaunchKernelGGL((colstats_part_kernel<T>), dim3(nb, (C + 63) / 64), dim3(256), 0, st, (const T*)X, ldx, M, C,
+                       ws, 1);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((C + kFinCols - 1) / kFinCols), dim3(256), 0, st, (const float*)ws, nb, C,
+                       (float*)nullptr, (float*)nullptr, sums);
+    return check_launch("colstats_set");
+  });
+}
+
 extern "C" int svk_bn_apply(int dtype, const void* X, const float* sum, const float* sumsq, const float* gamma,
                             const float* beta, void* Y, int M, int C, float eps, int act, void* stream) {
   if (M < 0 || C <= 0 || !X || !sum || !sumsq || !gamma || !beta || !Y) { set_error("svk_bn_apply: bad args"); return SVK_EINVAL; }

@@ -97,6 +97,7 @@ SIGNATURES = {
     "svk_layernorm_bwd": [c_int, P, c_long, P, c_long, P, P, c_long, P, c_long, P, P, c_int, c_int, c_float, P],
     "svk_act_bwd": [c_int, P, P, P, P, c_long, c_int, P],
     "svk_colstats": [c_int, P, c_long, c_int, c_int, P, P, P, P],
+    "svk_colstats_set": [c_int, P, c_long, c_int, c_int, P, P, P],
     "svk_bn_apply": [c_int, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P],
     "svk_bn_bwd": [c_int, P, P, P, P, P, P, P, P, P, c_int, c_int, c_float, c_int, P, P],
     "svk_bn_update_running": [P, P, c_int, c_int, c_float, P, P, P],

@@ -1271,6 +1271,19 @@ def colstats(x, s, sq=None):
     return s
 
 
+def colstats_set(x, out=None):
+    """f32 [2, C]: row 0 = column sums, row 1 = column sums of squares of x [M, C], written (not accumulated:
+    no zero-fill launch), the same fixed-order reduction as colstats."""
+    _chk(x, "x")
+    M, C, ldx = _rows(x, "x")
+    if out is None:
+        out = torch.empty(2, C, device=x.device, dtype=torch.float32)
+    _chk(out, "out", torch.float32)
+    _lib.call("svk_colstats_set", dtype_code(x.dtype), _p(x), ldx, M, C, _p(out), _p(_stats_ws(M, C, x.device)),
+              _stream())
+    return out
+
+
 def bn_apply(x, s, sq, gamma, beta, eps, act=None, out=None):
     _chk(x, "x")
     C = x.shape[-1]

@@ -460,9 +460,7 @@ class EVPTrainStep:
             nm = f"flow_encoder.conv{i}"
             z = ops.conv2d_nhwc(prev, self.W(nm + ".weight"), k, st_, pad, bias=self.P(nm + ".bias"))
             Cz = z.shape[-1]
-            s1 = torch.zeros(Cz, device=self.dev, dtype=torch.float32)
-            s2 = torch.zeros(Cz, device=self.dev, dtype=torch.float32)
-            ops.colstats(z.view(-1, Cz), s1, s2)
+            s1, s2 = ops.colstats_set(z.view(-1, Cz))          # written, not accumulated: no zero-fills
             bn = f"flow_encoder.bn{i}"
             yb = ops.bn_apply(z, s1, s2, self.P(bn + ".weight"), self.P(bn + ".bias"), BN_EPS, act="relu")
             fl.append(dict(inp=prev, z=z, y=yb, s1=s1, s2=s2, k=k, st=st_, pad=pad))
@@ -539,9 +537,7 @@ class EVPTrainStep:
             ops.gemm(r, self.W(nm + ".weight"), self.P(nm + ".bias"), out=E[:, j * Ed:(j + 1) * Ed])
             rs.append((lvl, r, H, W))
         Z = ops.gemm(E, self.W("head.linear_fuse.conv.weight"))
-        s1 = torch.zeros(Ed, device=self.dev, dtype=torch.float32)
-        s2 = torch.zeros(Ed, device=self.dev, dtype=torch.float32)
-        ops.colstats(Z, s1, s2)
+        s1, s2 = ops.colstats_set(Z)
         bn = "head.linear_fuse.bn"
         Yb = ops.bn_apply(Z, s1, s2, self.P(bn + ".weight"), self.P(bn + ".bias"), BN_EPS, act="relu")
         feat = ops.mul_f32(ops.mean_rows(Yb, R), d2mask)

@@ -518,6 +518,9 @@ int svk_act_bwd(int dtype, const void* U, const void* dY, const void* dR, void* 
 long svk_stats_ws_floats(int M, int C);
 int svk_colstats(int dtype, const void* X, long ldx, int M, int C, float* sum, float* sumsq, float* ws,
                  void* stream);
+/* The same statistics written, not accumulated: sums[0..C) = column sums, sums[C..2C) = sums of squares
+ * (no zero-fill of the outputs needed before the call). */
+int svk_colstats_set(int dtype, const void* X, long ldx, int M, int C, float* sums, float* ws, void* stream);
 
 /* BatchNorm2d train mode on [M = B*H*W, C]: Y = act((X - mean) rsqrt(var + eps) g + b) from colstats
  * sums (biased variance), and its backward with the optional ReLU recomputed from X (dgamma/dbeta +=;

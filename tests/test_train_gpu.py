@@ -80,6 +80,21 @@ def test_batchnorm_train_fwd_bwd(cuda, M, C):
     _close(rv, 0.9 + 0.1 * x.var(0, unbiased=True), 1e-4)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C", [(65536, 256), (4312, 2048), (7, 24), (0, 64)])
+def test_colstats_set_equals_colstats(cuda, dt, M, C):
+    """svk_colstats_set (the train step's BN statistics written into [2, C], no zero-fill launches) gives the
+    bits of svk_colstats accumulated into zeroed buffers; M = 0 writes zeros."""
+    from svk import ops
+    x = (torch.randn(M, C, generator=torch.Generator().manual_seed(3)) * 2 + 0.3).to(cuda).to(dt)
+    s1, s2 = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    if M:
+        ops.colstats(x, s1, s2)
+    got = ops.colstats_set(x) if M else ops.colstats_set(x, out=torch.full((2, C), 5.0, device=cuda))
+    torch.cuda.synchronize()
+    assert torch.equal(got[0], s1) and torch.equal(got[1], s2)
+
+
 def test_batchnorm_stats_bit_reproducible(cuda):
     """Round-5 root cause of the intermittent f32 train-gradient failure: the BN batch statistics
     were summed with per-block f32 atomics, so the last bit of the batch mean depended on the order the blocks
