@@ -341,7 +341,7 @@ extern "C" int svk_attn_block(int dtype, const void* Hn, const void* X, const vo
   const float sl2 = scale * 1.4426950408889634f;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
-    const int sel = g_tune[TUNE_FFN_DIAG];   // tile-shape sweep (tools/attn_block_bench.py)
+    const int sel = g_tune[TUNE_ATTN_CFG];   // tile-shape sweep (svk_tune("attn_cfg"), tools/attn_block_bench.py)
     // C = 64: 8 waves x 256 queries (same-box whole-step A/B vs 4 waves: +0.25 %, 3 x 3 runs)
     if (C == 64 && sel == 4) ab::launch<T, 1, 8, 512>(Hn, X, KV, ldkv, Wq, bq, Wp, bp, gamma2, beta2, eps, Y, H2, B, N, Nk, sl2, st);
     else if (C == 64 && sel == 6) ab::launch<T, 1, 4, 256>(Hn, X, KV, ldkv, Wq, bq, Wp, bp, gamma2, beta2, eps, Y, H2, B, N, Nk, sl2, st);

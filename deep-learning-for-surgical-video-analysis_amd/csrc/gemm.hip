@@ -737,12 +737,6 @@ extern "C" int svk_gemm_ex(int dtype, const void* A, long lda, const void* W, lo
   if (U && ldu < N) { set_error("svk_gemm: ldu too small"); return SVK_EINVAL; }
   a.U = U; a.ldu = ldu; a.uact = uact;
   hipStream_t st = (hipStream_t)stream;
-  {
-    long bytes = 0;
-    int nflags = 0;
-    if (stream_workspace(st, &a.sk_part, &bytes, &a.sk_flags, &nflags))
-      a.sk_slots = (int)std::min<long>(bytes / (8L * 32 * 64 * 16), nflags / 8);   // gemm_pp: 8 waves x 32 f32x4 x 64 lanes
-  }
   SVK_DISPATCH_DTYPE(dtype, T, {
     const long vecw = 16 / (long)sizeof(T);
     bool vec = aligned16(A) && aligned16(W) && (lda % vecw == 0) && (ldw % vecw == 0) && (K % 8 == 0);

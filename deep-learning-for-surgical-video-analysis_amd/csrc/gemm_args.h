@@ -26,9 +26,6 @@ struct GemmArgs {
   int out_mode, uH, uW, us, uC;
   // split-K (gemm_pk_conv_splitk): raw f32 partial sums of ksplit K parts -> slab [ksplit][M][N]
   int ksplit; float* slab;
-  // stream-K workspace of the launching stream (gemm_pp; svk_set_stream_workspace): partial sums for up to
-  // sk_slots workgroups and one flag per (workgroup, wave), zero between launches
-  void* sk_part; int* sk_flags; int sk_slots;
 };
 
 // gemm_pk.hip: persistent LDS-DMA bf16 / f16 GEMM / implicit-GEMM conv (asrc 1) for the plain-epilogue
@@ -43,7 +40,7 @@ inline int splitk_bm() {
   return bm == 128 ? 128 : 64;
 }
 // gemm_pp.hip: 256 x 256 ping-pong persistent GEMM, dense A, plain epilogue; variant 0 / 1 = first / deep DMA
-// schedule, 2 = deep + stream-K; returns 1 when not eligible.
+// schedule; returns 1 when not eligible.
 template <typename T> int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant);
 // gemm_wt.hip: wide-tile (one 256-thread workgroup per CU, 2 x 2 waves of 128-row sub-tiles) persistent GEMM,
 // dense A, plain epilogue; cfg 0 / 1 / 2 = 256 x 256 / 256 x 160 / 256 x 128 tiles; returns 1 when not eligible.

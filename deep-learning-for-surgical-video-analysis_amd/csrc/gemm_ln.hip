@@ -318,9 +318,10 @@ extern "C" int svk_gemm_ln(int dtype, const void* A, int M, int K, const void* p
   if (svk_gemm_ln_packed_bytes(dtype, N, K) == 0) {
     set_error("svk_gemm_ln: (dtype=%d, N=%d, K=%d) not instantiated", dtype, N, K); return SVK_EUNSUPPORTED;
   }
-  if ((((uintptr_t)A) | ((uintptr_t)packed) | ((uintptr_t)bias) | ((uintptr_t)gamma) | ((uintptr_t)beta)) & 15 ||
-      (((uintptr_t)R) | ((uintptr_t)X) | ((uintptr_t)H)) & 7) {
-    set_error("svk_gemm_ln: misaligned operand"); return SVK_EINVAL;
+  // X and H leave as 16-byte row chunks (stage_store), R is read as 8-byte pieces
+  if ((((uintptr_t)A) | ((uintptr_t)packed) | ((uintptr_t)bias) | ((uintptr_t)gamma) | ((uintptr_t)beta) |
+       ((uintptr_t)X) | ((uintptr_t)H)) & 15 || ((uintptr_t)R) & 7) {
+    set_error("svk_gemm_ln: misaligned operand (A, packed, bias, gamma, beta, X, H: 16 bytes; R: 8)"); return SVK_EINVAL;
   }
   if (M == 0) return SVK_OK;
   hipStream_t st = (hipStream_t)stream;

@@ -131,7 +131,7 @@ __device__ __forceinline__ void gload4(float& v, const char* src) {
 // reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
 template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
 __global__ __launch_bounds__(Cfg::NT, Cfg::OCC)
-void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int diag) {
+void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   typedef v8_t<T> tx8;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
@@ -393,7 +393,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int dia
           const int row = wm * WM + i * 16 + fr, col = wn * WN + j * 16 + fq * 4;
           *reinterpret_cast<uint2*>(stile + row * (BN * 2) + (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col >> 2) & 1) * 8) =
               *reinterpret_cast<const uint2*>(o);
-        } else if (m < p.M && n < p.N && !(diag & 2)) {   // N % 4 == 0: a 4-column group is all-in or all-out
+        } else if (m < p.M && n < p.N) {   // N % 4 == 0: a 4-column group is all-in or all-out
           *reinterpret_cast<uint2*>(C + (long)m * p.ldc + n) = *reinterpret_cast<const uint2*>(o);
         }
       }
@@ -410,7 +410,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int dia
         const int row = idx / CPR, c = idx % CPR;
         const uint4 v = *reinterpret_cast<const uint4*>(stile + row * (BN * 2) + ((c ^ (row & (CPR - 1))) << 4));
         const int m = m0 + row, n = n0 + c * 8;
-        if (m < p.M && n < p.N && !(diag & 2)) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
+        if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
       }
       barrier_mem();   // the next step's DMA overwrites this stage buffer
     }
@@ -465,7 +465,6 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks, int dia
       case SVK_ACT_TANH: epilogue(tile, std::integral_constant<int, SVK_ACT_TANH>{}); break;
       default: epilogue(tile, std::integral_constant<int, 0>{}); break;
     }
-    if (diag & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // timing ablation: drain the stores
   }
   // the last step's zero-block DMA is still in flight: retire it before the wave (and the workgroup's
   // LDS allocation) ends
@@ -502,7 +501,7 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
   hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
-                     (int)ntiles, nk, ks, g_tune[TUNE_PK_DIAG] > 0 ? g_tune[TUNE_PK_DIAG] : 0);
+                     (int)ntiles, nk, ks);
   static char name[112];
   if (!name[0])
     snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", type_name<T>(), Cfg::BM, Cfg::BN,

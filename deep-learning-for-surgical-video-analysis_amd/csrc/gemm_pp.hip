@@ -73,15 +73,7 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
 }
 
-// SK (stream-K): the grid's workgroups split the ntiles * nk K-tiles of the whole GEMM into equal contiguous
-// ranges, so no CU idles in a last partial wave of tiles.  A range starts and ends inside tiles: its first piece
-// (if it starts past a tile's K-tile 0) is written as f32 partial sums to part[w] and announced by one flag per
-// wave (plain 16-byte stores, vmcnt(0), agent release fence, relaxed agent flag store); its last piece, if it
-// ends before the tile's last K-tile, waits for the flags of the following workgroups that hold the rest of the
-// tile (relaxed poll, agent acquire), adds their partials in workgroup order and runs the epilogue.  Partials are
-// produced at the START of a range and consumed at its END, so the waits are short; a workgroup only waits for
-// higher-numbered ones, which never wait for it (no cycle).  The consumer resets each flag it consumed.
-template <typename T, class C, bool KTAIL, int ACT, int DEEP, bool SK>
+template <typename T, class C, bool KTAIL, int ACT, int DEEP>
 __global__ __launch_bounds__(512, 2)
 void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   typedef v8_t<T> tx8;
@@ -93,12 +85,8 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
   const int g = wave >> 2, wc = wave & 3;
   const int fr = lane & 15, fq = lane >> 4;
   const int G = gridDim.x;
-  const int first = xcd_remap(blockIdx.x, G);         // data-parallel: first tile; stream-K: range index
-  // (the host keeps ntiles * nk * G < 2^31; readfirstlane: the integer divisions run on the vector unit)
-  const int units = ntiles * nk;
-  const int ustart = SK ? __builtin_amdgcn_readfirstlane(first * units / G) : 0;
-  const int uend = SK ? __builtin_amdgcn_readfirstlane((first + 1) * units / G) : 0;
-  if (SK ? ustart >= uend : first >= ntiles) return;   // whole workgroup: no barrier is left waiting
+  const int first = xcd_remap(blockIdx.x, G);         // first tile of this workgroup
+  if (first >= ntiles) return;                        // whole workgroup: no barrier is left waiting
   const T* A = static_cast<const T*>(p.A);
   const T* Wt = static_cast<const T*>(p.W);
   const char* zero = reinterpret_cast<const char*>(g_zero);
@@ -238,69 +226,18 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
     }
   };
 
-  // ---- stream-K partial sums: part[((w * 8 + wave) * NST + i * TN + j) * 64 + lane] (f32x4, lane-major: every
-  // store / load instruction is one contiguous KiB), flags[w * 8 + wave]
-  f32x4* const part = reinterpret_cast<f32x4*>(p.sk_part);
-  int* const flags = p.sk_flags;
-  auto store_partial = [&]() {
-    // uniform slab base in SGPRs (first, wave are uniform), one VGPR lane offset for every store: no VGPR address
-    // registers at all (compiler-visible stores made hipcc materialise 32 addresses and spill)
-    const char* base = reinterpret_cast<const char*>(part) + (long)(first * 8 + wave) * NST * 1024;
-    const int lo = lane * 16;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const char* row = base + i * TN * 1024;
-      static_assert(TN <= 4, "immediate offsets up to 3 KiB");
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        asm volatile("global_store_dwordx4 %0, %1, %2 offset:%3" ::"v"(lo), "v"(acc[i][j]), "s"(row), "n"(j * 1024)
-                     : "memory");
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) __hip_atomic_store(flags + first * 8 + wave, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  };
-  auto fixup = [&](int tile) {
-    const int tend = (tile + 1) * nk;
-    for (int w2 = first + 1; w2 < G && __builtin_amdgcn_readfirstlane(w2 * units / G) < tend; ++w2) {
-      int* fl = flags + w2 * 8 + wave;
-      // bounded poll (~0.3 s): a schedule bug must end the kernel with wrong numbers, never hang the GPU
-      for (int spin = 0; spin < (1 << 21) && __hip_atomic_load(fl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0; ++spin)
-        __builtin_amdgcn_s_sleep(2);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int slot = (w2 * 8 + wave) * NST * 64 + lane;
-      asm volatile("" : "+v"(slot));
-      const f32x4* src = part + slot;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {               // one row block at a time: 16 registers of partials in flight
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] += src[(i * TN + j) * 64];
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (lane == 0) __hip_atomic_store(fl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-
   // ---- prologue: stream position 0 whole and the first OFF pieces of position 1 (their nominal issue intervals
   // are negative); position 0 retired before the first barrier
-  int dtile = SK ? __builtin_amdgcn_readfirstlane(ustart / nk) : first;
-  int dkt = SK ? __builtin_amdgcn_readfirstlane(ustart % nk) : 0, dbuf = 0;
-  int dunit = ustart;
+  int dtile = first, dkt = 0, dbuf = 0;
   bool dlive = true;
   // the consumer's cursor starts at stream position 0 (the DMA cursor is moved ahead by the prologue below)
   int tile = dtile, kt = dkt;
-  int kfirst = kt;                                    // K-tile the current piece of the tile started at
   auto advance = [&]() {
     dbuf ^= 1;
-    if constexpr (SK) dlive = ++dunit < uend;
     if (++dkt == nk) {
       dkt = 0;
-      dtile += SK ? 1 : G;
-      if constexpr (!SK) dlive = dtile < ntiles;
+      dtile += G;
+      dlive = dtile < ntiles;
       if (dlive) set_rows(dtile);
     }
   };
@@ -318,9 +255,8 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
 
   int buf = 0;
   int post = 0;                                       // intervals left in which the epilogue's stores may still fly
-  int u = ustart;
-  while (SK ? u < uend : tile < ntiles) {
-    const bool tlast = kt == nk - 1, rlast = SK && u == uend - 1;
+  while (tile < ntiles) {
+    const bool tlast = kt == nk - 1;
     const bool live = dlive;                          // (DEEP 2) pieces of the next position are issued in this one
     // the 8 intervals of this K-tile, each a compile-time slot (a runtime slot index would put the
     // accumulators in scratch)
@@ -351,16 +287,9 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
         }
       } else {                                        // ---- compute interval
         mfma_phase(ph);
-        if (s == 7 && (tlast || rlast)) {
-          if (SK && kfirst > 0) {                     // a piece that began mid-tile: partial sums out
-            store_partial();
-            post = 0;
-          } else if (!SK || tlast) {
-            epilogue(tile);
-            post = NW + 1;
-          }
-          // else: the range ends with a tile's head piece — fixup + epilogue after the loop (out of the
-          // pipelined body, which keeps its register allocation)
+        if (s == 7 && tlast) {
+          epilogue(tile);
+          post = NW + 1;
         }
       }
       // the epilogue's NST stores are younger than the NW pieces issued before them: for the NW + 1 intervals
@@ -395,25 +324,14 @@ void gemm_pp(GemmArgs p, int ntn, int ntiles, int nk) {
     slot(std::integral_constant<int, 6>{});
     slot(std::integral_constant<int, 7>{});
     buf ^= 1;
-    ++u;
     if (tlast) {
       kt = 0;
-      kfirst = 0;
-      tile += SK ? 1 : G;
+      tile += G;
     } else {
       ++kt;
     }
   }
   if (g == 0) barrier();                              // equal barrier counts: group 0 matches the stagger
-  if constexpr (SK) {
-    const int te = __builtin_amdgcn_readfirstlane((uend - 1) / nk), ke = __builtin_amdgcn_readfirstlane((uend - 1) % nk);
-    const int ts = __builtin_amdgcn_readfirstlane(ustart / nk), ks = __builtin_amdgcn_readfirstlane(ustart % nk);
-    if (ke < nk - 1 && !(ts == te && ks > 0)) {        // the last piece is a tile's head
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      fixup(te);
-      epilogue(te);
-    }
-  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -425,33 +343,32 @@ static int slots_of(const void* fn) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <typename T, int BN, bool KTAIL, int ACT, int DEEP, bool SK>
+template <typename T, int BN, bool KTAIL, int ACT, int DEEP>
 static int launch(const GemmArgs& a, hipStream_t st) {
   typedef Cfg<BN> C;
   const int ntm = (a.M + C::BM - 1) / C::BM, ntn = (a.N + BN - 1) / BN;
   const long ntiles = (long)ntm * ntn;
   const int nk = (a.K + 63) / 64;
-  static const int slots = slots_of(reinterpret_cast<const void*>(&gemm_pp<T, C, KTAIL, ACT, DEEP, SK>));
-  const int grid = (int)std::min<long>(SK ? ntiles * nk : ntiles, slots);
-  if (SK && (!a.sk_part || !a.sk_flags || a.sk_slots < grid || ntiles * (long)nk * grid >= (1L << 31))) return 1;
-  hipLaunchKernelGGL((gemm_pp<T, C, KTAIL, ACT, DEEP, SK>), dim3(grid), dim3(512), 0, st, a, ntn, (int)ntiles, nk);
+  static const int slots = slots_of(reinterpret_cast<const void*>(&gemm_pp<T, C, KTAIL, ACT, DEEP>));
+  const int grid = (int)std::min<long>(ntiles, slots);
+  hipLaunchKernelGGL((gemm_pp<T, C, KTAIL, ACT, DEEP>), dim3(grid), dim3(512), 0, st, a, ntn, (int)ntiles, nk);
   static char name[96];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pp<%s, Cfg<%d>, %s, %d, %d, %s>", type_name<T>(), BN, KTAIL ? "true" : "false", ACT,
-             DEEP, SK ? "true" : "false");
+    snprintf(name, sizeof(name), "gemm_pp<%s, Cfg<%d>, %s, %d, %d>", type_name<T>(), BN, KTAIL ? "true" : "false", ACT,
+             DEEP);
   set_last_kernel(name);
   return check_launch("gemm_pp");
 }
 
-template <typename T, int BN, int DEEP, bool SK>
+template <typename T, int BN, int DEEP>
 static int launch_bn(const GemmArgs& a, hipStream_t st) {
   const bool tail = a.K % 64 != 0;
   switch (a.act) {
     case SVK_ACT_GELU:
-      return tail ? launch<T, BN, true, SVK_ACT_GELU, DEEP, SK>(a, st) : launch<T, BN, false, SVK_ACT_GELU, DEEP, SK>(a, st);
+      return tail ? launch<T, BN, true, SVK_ACT_GELU, DEEP>(a, st) : launch<T, BN, false, SVK_ACT_GELU, DEEP>(a, st);
     case SVK_ACT_RELU:
-      return tail ? launch<T, BN, true, SVK_ACT_RELU, DEEP, SK>(a, st) : launch<T, BN, false, SVK_ACT_RELU, DEEP, SK>(a, st);
-    case 0: return tail ? launch<T, BN, true, 0, DEEP, SK>(a, st) : launch<T, BN, false, 0, DEEP, SK>(a, st);
+      return tail ? launch<T, BN, true, SVK_ACT_RELU, DEEP>(a, st) : launch<T, BN, false, SVK_ACT_RELU, DEEP>(a, st);
+    case 0: return tail ? launch<T, BN, true, 0, DEEP>(a, st) : launch<T, BN, false, 0, DEEP>(a, st);
     default: return 1;
   }
 }
@@ -469,12 +386,12 @@ int gemm_pp_try(const GemmArgs& a, hipStream_t st, int variant) {
   if (!al(a.A, 16) || !al(a.W, 16) || !al(a.C, 8) || (a.R && !al(a.R, 8)) || (a.bias && !al(a.bias, 16))) return 1;
   // 32-bit byte offsets of the DMA rows
   if ((long)a.M * a.lda * 2 + 256 >= (1L << 32) || (long)a.N * a.ldw * 2 + 256 >= (1L << 32)) return 1;
-  // variant: 0 = first DMA schedule, 1 = deep DMA schedule, 2 = deep + stream-K (needs the stream's workspace)
-  if (variant == 0) return pp::launch_bn<T, 256, 3, false>(a, st);
-  if (variant == 1) return pp::launch_bn<T, 256, 2, false>(a, st);
-  // variant 2 (stream-K) is not instantiated: hipcc spills ~55-67 VGPRs of its in-loop partial-sum path, and a
-  // scratch access is a vector-memory operation the counted DMA waits do not know about (isa_check rejects it)
-  (void)variant;
+  // variant: 0 = first DMA schedule, 1 = deep DMA schedule
+  if (variant == 0) return pp::launch_bn<T, 256, 3>(a, st);
+  if (variant == 1) return pp::launch_bn<T, 256, 2>(a, st);
+  // (round 6: the stream-K variant — f32 partial slabs + per-wave flags in a per-stream workspace — was removed: its
+  // in-loop partial-sum path spilled 55-67 VGPRs, a scratch access the counted DMA waits cannot see, so it was never
+  // instantiated, and its workspace registry had no caller left)
   return 1;
 }
 

@@ -132,7 +132,13 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
                                                      const float* __restrict__ b2, T* __restrict__ Y,
                                                      T* __restrict__ Yn, const float* __restrict__ gamma,
                                                      const float* __restrict__ beta, float eps, int H,
-                                                     int nstrip, int total, int diag) {
+                                                     int nstrip, int total, int diag_in) {
+#ifdef SVK_DIAG
+  const int diag = diag_in;   // timing ablations of the diagnostic build (SVK_FFN_DIAG)
+#else
+  constexpr int diag = 0;     // product build: the ablation branches below are compiled out
+  (void)diag_in;
+#endif
   typedef v8_t<T> tx8;
   constexpr int W = K::W, C = K::C, HC = K::HC, HID = K::HID, NPC = K::NPC, CS = K::CS, NCH = K::NCH;
   constexpr int CPR1 = C / 8, CPR2 = HID / 8;           // 16-byte chunks per W1 / W2 row
@@ -400,7 +406,7 @@ __global__ __launch_bounds__(K::NT, 3) void mixffn_ws(const T* __restrict__ XN, 
             for (int h = 0; h < 2; ++h) {
               const int o = (dg * K::RV + rr) * W + 2 * dp + h;
               uint2 v;
-              if (diag == 1) {   // timing diagnostics only (svk_tune("ffn_diag", n)): 1 = GELU replaced by ReLU,
+              if (diag == 1) {   // timing diagnostics only (-DSVK_DIAG build, SVK_FFN_DIAG=n): 1 = GELU replaced by ReLU,
                                  // 2 = dwconv waves idle, 3 = producer waves idle (outputs meaningless)
                 v.x = pack2<T>(fmaxf(acc[rr][0][h], 0.f), fmaxf(acc[rr][1][h], 0.f));
                 v.y = pack2<T>(fmaxf(acc[rr][2][h], 0.f), fmaxf(acc[rr][3][h], 0.f));
@@ -438,7 +444,12 @@ static int launch(const void* XN, const void* X, const void* W1, const float* b1
   const int grid = (int)std::min<long>(total, cus);
   hipLaunchKernelGGL((mixffn_ws<T, K>), dim3(grid), dim3(K::NT), K::LDS, st, (const T*)XN, (const T*)X, (const T*)W1,
                      b1, (const uint4*)tpk, (const T*)W2, b2, (T*)Y, (T*)Yn, gamma, beta, eps, H, nstrip, (int)total,
-                     g_tune[TUNE_FFN_DIAG] > 0 ? g_tune[TUNE_FFN_DIAG] : 0);
+                     
+#ifdef SVK_DIAG
+                     diag_knob("SVK_FFN_DIAG"));
+#else
+                     0);
+#endif
   static char name[96];
   if (!name[0])
     snprintf(name, sizeof(name), "mixffn_ws<%s, Cfg<%d, %d, %d, %d, %d>>", type_name<T>(), K::C, K::W, K::R, K::RV,

@@ -3,7 +3,6 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
-#include <mutex>
 
 #include "svk_common.h"
 
@@ -34,52 +33,23 @@ int check_launch(const char* what) {
 }
 
 // Tuning knobs (tile configuration / kernel variant overrides for A/B measurements in one process);
-// initial values from the environment, -1 = automatic choice.
-static const char* const k_knob_names[TUNE_NKNOBS] = {"pk_cfg", "pk_elds", "dw_lds", "dw_rows", "ffn_diag", "pk_diag"};
-static const char* const k_knob_env[TUNE_NKNOBS] = {"SVK_PK_CFG", "SVK_PK_ELDS", "SVK_DW_LDS", "SVK_DW_LR", "SVK_FFN_DIAG", "SVK_PK_DIAG"};
+// initial values from the environment, -1 = automatic choice.  Every value selects a complete kernel variant.
+static const char* const k_knob_names[TUNE_NKNOBS] = {"pk_cfg", "pk_elds", "dw_lds", "dw_rows", "attn_cfg"};
+static const char* const k_knob_env[TUNE_NKNOBS] = {"SVK_PK_CFG", "SVK_PK_ELDS", "SVK_DW_LDS", "SVK_DW_LR", "SVK_ATTN_CFG"};
 static int init_knob(int i) {
   const char* e = getenv(k_knob_env[i]);
   return e ? atoi(e) : -1;
 }
-int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3), init_knob(4), init_knob(5)};
+int g_tune[TUNE_NKNOBS] = {init_knob(0), init_knob(1), init_knob(2), init_knob(3), init_knob(4)};
 
-// Caller-owned per-stream workspaces (svk_set_stream_workspace): the stream-K GEMM's partial sums and flags.
-struct StreamWs { hipStream_t st; void* part; long bytes; int* flags; int nflags; };
-static StreamWs g_ws[16];
-static int g_nws = 0, g_ws_next = 0;   // full table: entries are replaced oldest first
-static std::mutex g_ws_mu;
-
-bool stream_workspace(hipStream_t st, void** part, long* bytes, int** flags, int* nflags) {
-  std::lock_guard<std::mutex> lk(g_ws_mu);
-  for (int i = 0; i < g_nws; ++i)
-    if (g_ws[i].st == st) {
-      *part = g_ws[i].part; *bytes = g_ws[i].bytes; *flags = g_ws[i].flags; *nflags = g_ws[i].nflags;
-      return true;
-    }
-  return false;
+#ifdef SVK_DIAG
+int diag_knob(const char* env) {
+  const char* e = getenv(env);
+  return e ? atoi(e) : 0;
 }
+#endif
 
 }  // namespace svk
-
-extern "C" int svk_set_stream_workspace(void* stream, void* part, long part_bytes, int* flags, int nflags) {
-  if ((part && part_bytes <= 0) || (flags && nflags <= 0) || ((uintptr_t)part & 15)) {
-    svk::set_error("svk_set_stream_workspace: bad args"); return SVK_EINVAL;
-  }
-  std::lock_guard<std::mutex> lk(svk::g_ws_mu);
-  hipStream_t st = (hipStream_t)stream;
-  for (int i = 0; i < svk::g_nws; ++i)
-    if (svk::g_ws[i].st == st) {
-      svk::g_ws[i] = svk::StreamWs{st, part, part_bytes, flags, nflags};
-      return SVK_OK;
-    }
-  if (svk::g_nws == 16) {                 // evict the oldest registration instead of failing the 17th stream
-    svk::g_ws[svk::g_ws_next] = svk::StreamWs{st, part, part_bytes, flags, nflags};
-    svk::g_ws_next = (svk::g_ws_next + 1) % 16;
-    return SVK_OK;
-  }
-  svk::g_ws[svk::g_nws++] = svk::StreamWs{st, part, part_bytes, flags, nflags};
-  return SVK_OK;
-}
 
 extern "C" int svk_tune(const char* knob, int value) {
   for (int i = 0; i < svk::TUNE_NKNOBS; ++i)

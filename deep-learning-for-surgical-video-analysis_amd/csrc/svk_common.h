@@ -22,10 +22,13 @@ namespace svk {
 void set_error(const char* fmt, ...);
 int check_launch(const char* what);
 // Tuning knobs set through svk_tune (runtime.hip); -1 = automatic.
-enum { TUNE_PK_CFG = 0, TUNE_PK_ELDS = 1, TUNE_DW_LDS = 2, TUNE_DW_ROWS = 3, TUNE_FFN_DIAG = 4, TUNE_PK_DIAG = 5, TUNE_NKNOBS = 6 };
+enum { TUNE_PK_CFG = 0, TUNE_PK_ELDS = 1, TUNE_DW_LDS = 2, TUNE_DW_ROWS = 3, TUNE_ATTN_CFG = 4, TUNE_NKNOBS = 5 };
 extern int g_tune[TUNE_NKNOBS];
-// Caller-owned workspace registered for a stream (svk_set_stream_workspace); false when none.
-bool stream_workspace(hipStream_t st, void** part, long* bytes, int** flags, int* nflags);
+#ifdef SVK_DIAG
+// Timing-ablation switch of the diagnostic build only (-DSVK_DIAG: SVK_FFN_DIAG / SVK_PK_DIAG in the environment);
+// the product library has no code path that skips work or stores.
+int diag_knob(const char* env);
+#endif
 // Name of the kernel instantiation the calling thread launched last (svk_last_kernel; profiling).
 void set_last_kernel(const char* name);
 void set_pk_reject(const char* why);   // why the last GEMM call missed gemm_pk (fallback kernel names)

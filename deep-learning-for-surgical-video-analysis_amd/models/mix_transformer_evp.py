@@ -197,6 +197,7 @@ class Attention(nn.Module):
         o = ops.attention(q, k, v, self.num_heads, self.scale)
         return ops.gemm(o, p["wp"], p["bp"], residual=residual)
 
+    @get_local("attn")   # same capture contract as forward (attention-map capture refused loudly when activated)
     def forward_ln(self, x, H, W, residual, ln):
         """(residual + attn(x), LayerNorm(residual + attn(x))) with proj, the residual add and the norm in one
         kernel (svk_gemm_ln: N in {320, 512}); None where not covered."""
@@ -216,6 +217,7 @@ class Attention(nn.Module):
         return (ops.FUSED_ATTN_BLOCK and x.dtype in ops.H16 and self.dim in (64, 128) and self.dim == 64 * self.num_heads
                 and r > 1 and (H // r) * (W // r) <= 64)
 
+    @get_local("attn")
     def forward_block(self, hn, H, W, x, ln2):
         """(x + attn(hn), norm2(x + attn(hn))) for the stage-1/2 shapes in one kernel after the sequence
         reduction (q, attention, proj + residual and the next LayerNorm never leave the chip)."""

@@ -58,7 +58,6 @@ SIGNATURES = {
     "svk_frame_preproc": [P, P, P, P, P, c_int, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P,
                           P],
     "svk_flow_preproc": [P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P],
-    "svk_set_stream_workspace": [P, P, c_long, P, c_int],
     "svk_train_augment": [P, P, P, P, P, P, P, c_int, P, P, c_int, P, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                           P, P, P],
     "svk_train_augment_flow": [P, P, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_float, c_float, P],

@@ -72,7 +72,8 @@ def set_profiler(records):
 
 
 def tune(knob, value):
-    """Set a kernel-selection knob (svk_tune: "pk_cfg", "pk_elds", "dw_lds", "dw_rows"; -1 = auto)."""
+    """Set a kernel-selection knob (svk_tune: "pk_cfg", "pk_elds", "dw_lds", "dw_rows", "attn_cfg"; -1 = auto).
+    Every value selects a complete, parity-tested variant: the product library has no work-skipping switch."""
     _lib.call("svk_tune", knob.encode(), int(value))
 
 
@@ -471,6 +472,8 @@ def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu"
     returns [B, H * W, N].  Where the map has the matrix-core form (14 x 14 with N = 320, 7 x 7 with N = 512,
     28 x 28 with N = 128) it runs that,
     from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form.
+    When ``packed`` is given, the kernel reads the taps, dbias and W2 baked into it (``taps`` / ``dbias`` / ``w2``
+    are then only shape-checked); its size is checked against svk_mixffn_dw_fc2_packed_bytes(dtype, W, N, K).
     ``act="none"`` drops the GELU (matrix-core form only, 14 x 14 / 7 x 7): with flipped taps, zero dbias and
     w2 = W1ᵀ it is the data gradient through a frozen DWConv + fc1 (svk/train.py)."""
     if act not in ("gelu", "none"):
@@ -494,6 +497,14 @@ def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu"
         packed = mixffn_dw_fc2_pack(taps, dbias, w2, W)
     if act == "none" and packed is None:
         raise _lib.SvkError(f"svk.mixffn_dw_fc2: no identity-activation form for {W} x {W}, N = {N}")
+    if packed is not None:
+        # the packed buffer carries the taps, dbias and W2 (the arguments above are then unused by the kernel):
+        # it must have been built for this (dtype, W, N, K), or the kernel would read past it
+        want = int(_lib.load().svk_mixffn_dw_fc2_packed_bytes(dtype_code(h.dtype), int(W), int(N), int(K)))
+        if (want == 0 or not packed.is_cuda or not packed.is_contiguous()
+                or packed.numel() * packed.element_size() != want or packed.data_ptr() % 16):
+            raise _lib.SvkError(f"svk.mixffn_dw_fc2: packed buffer is not the ({h.dtype}, W={W}, N={N}, K={K}) pack "
+                                f"({packed.numel() * packed.element_size()} bytes, expected {want})")
     t0 = _prof_begin()
     if act == "none":
         _lib.call("svk_mixffn_dw_fc2_packed_act", dtype_code(h.dtype), _p(h), _p(packed), _p(b2), _p(residual),
@@ -1279,6 +1290,8 @@ def colstats_set(x, out=None):
     if out is None:
         out = torch.empty(2, C, device=x.device, dtype=torch.float32)
     _chk(out, "out", torch.float32)
+    if tuple(out.shape) != (2, C) or not out.is_contiguous():
+        raise _lib.SvkError(f"svk.colstats_set: out must be a contiguous f32 [2, {C}] tensor, got {tuple(out.shape)}")
     _lib.call("svk_colstats_set", dtype_code(x.dtype), _p(x), ldx, M, C, _p(out), _p(_stats_ws(M, C, x.device)),
               _stream())
     return out

@@ -38,16 +38,14 @@ const char* svk_version(void);
 const char* svk_last_error(void);
 /* Kernel instantiation launched last by the calling thread (GEMM / conv family; for profilers). */
 const char* svk_last_kernel(void);
-/* Tuning knobs for A/B measurements inside one process (no effect on results): "pk_cfg" (persistent
- * GEMM tile: -1 auto, 0 128x128, 10 128x64, 20 64x128, 30 64x64), "pk_elds" (-1 auto,
- * 0/1 staged epilogue), "dw_lds" (1 = LDS-tiled depthwise conv), "dw_rows" (its strip height).
- * Initial values from SVK_PK_CFG / SVK_PK_ELDS / SVK_DW_LDS / SVK_DW_LR. */
+/* Tuning knobs for A/B measurements inside one process (no effect on results: every setting selects a
+ * complete, parity-tested kernel variant): "pk_cfg" (persistent GEMM tile: -1 auto, 0 128x128, 10 128x64,
+ * 20 64x128, 30 64x64), "pk_elds" (-1 auto, 0/1 staged epilogue), "dw_lds" (1 = LDS-tiled depthwise conv),
+ * "dw_rows" (its strip height), "attn_cfg" (stage-1 fused attention block tile: -1 auto, 4 = 8 waves x 512
+ * queries, 6 = 4 waves x 256).  Initial values from SVK_PK_CFG / SVK_PK_ELDS / SVK_DW_LDS / SVK_DW_LR /
+ * SVK_ATTN_CFG.  (Round 6: the timing-ablation switches that skipped work or stores — "pk_diag", "ffn_diag" —
+ * exist only in a -DSVK_DIAG build of the library, never in the product .so.) */
 int svk_tune(const char* knob, int value);
-
-/* Register caller-owned scratch for launches on `stream` (the library allocates nothing): the stream-K GEMM's
- * f32 partial sums (part, part_bytes; 256 KiB per workgroup) and its flags (nflags int32, zero on registration,
- * left zero by every launch).  One registration per stream; a later call replaces it. */
-int svk_set_stream_workspace(void* stream, void* part, long part_bytes, int* flags, int nflags);
 
 /* C[m, n] = act(sum_k A[m, k] * W[n, k] + bias[n]) + R[m, n]
  * Replaces nn.Linear (+ activation, + residual add) at: Attention q/kv/proj
@@ -172,7 +170,8 @@ int svk_mixffn_dw_fc2_packed_act(int dtype, const void* H, const void* packed, c
  * svk_gemm + svk_layernorm).  16-bit, N in {320, 512}, K % 8 == 0.  W is consumed PACKED: svk_gemm_ln_pack writes
  * svk_gemm_ln_packed_bytes(dtype, N, K) bytes (0 where not instantiated) from W [N][K]; then svk_gemm_ln reads A
  * [M][K] (row-contiguous), the packed buffer, bias [N] / gamma [N] / beta [N] f32 (bias may be NULL), R / X / H
- * [M][N] (R and X may be NULL).  A, packed, bias, gamma, beta 16-byte aligned; R, X, H 8-byte. */
+ * [M][N] (R and X may be NULL).  A, packed, bias, gamma, beta, X, H 16-byte aligned (X and H are stored as
+ * 16-byte row chunks); R 8-byte. */
 long svk_gemm_ln_packed_bytes(int dtype, int N, int K);
 int svk_gemm_ln_pack(int dtype, const void* W, int N, int K, void* packed, void* stream);
 int svk_gemm_ln(int dtype, const void* A, int M, int K, const void* packed, const float* bias, const void* R,

@@ -77,6 +77,35 @@ def test_library_version_and_error_path():
     assert rc == -1 and b"Nk" in lib.svk_last_error()
 
 
+def test_tune_knobs_select_variants_only():
+    """svk_tune accepts only variant-selecting knobs; the round-5 timing ablations that skipped stores or work
+    ("pk_diag", "ffn_diag") exist only in a -DSVK_DIAG build, and the stream-K workspace
+    registry is gone with the variant it served."""
+    from svk import _lib
+    lib = _lib.load()
+    for knob in (b"pk_cfg", b"pk_elds", b"dw_lds", b"dw_rows", b"attn_cfg"):
+        assert lib.svk_tune(knob, -1) == 0, knob
+    for knob in (b"pk_diag", b"ffn_diag"):
+        assert lib.svk_tune(knob, 2) == -1 and b"unknown knob" in lib.svk_last_error()
+    assert not hasattr(lib, "svk_set_stream_workspace") and "svk_set_stream_workspace" not in _lib.SIGNATURES
+
+
+def test_gemm_ln_requires_16_byte_outputs():
+    """svk_gemm_ln stores X and H as 16-byte row chunks: an 8-byte-aligned X or H is rejected on the host before
+    any launch (fake device addresses are never dereferenced)."""
+    from svk import _lib
+    lib = _lib.load()
+    args = dict(A=0x10000, packed=0x20000, bias=0x30000, R=0x40008, gamma=0x50000, beta=0x60000, X=0x70000, H=0x80000)
+
+    def run(**kw):
+        a = dict(args, **kw)
+        return lib.svk_gemm_ln(2, a["A"], 64, 320, a["packed"], a["bias"], a["R"], a["gamma"], a["beta"], 1e-6,
+                               a["X"], a["H"], 320, None)
+    assert run(X=0x70008) == -1 and b"misaligned" in lib.svk_last_error()
+    assert run(H=0x80008) == -1 and b"misaligned" in lib.svk_last_error()
+    assert run(A=0x10008) == -1
+
+
 @pytest.mark.parametrize("variant", ["mit_b0_evp", "mit_b2_evp", "mit_b3_evp"])
 def test_build_state_dict_matches_reference(golden, variant):
     from models import mix_transformer_evp as mte

@@ -926,3 +926,25 @@ def test_gauss5x5_s2d(cuda, dt, B, C, H, W):
     ref = pad.view(B, OH + 1, 4, OW + 1, 4, 3).permute(0, 1, 3, 2, 4, 5).reshape(B, OH + 1, OW + 1, 48)
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+def test_packed_and_stats_buffers_are_validated(cuda):
+    """a dw_fc2 pack built for another (W, N, K) and a wrongly shaped colstats_set output are rejected
+    on the host instead of being read / written out of bounds."""
+    from svk import ops, _lib
+    dt = torch.float16
+    h = _rand(2, 14, 14, 1280, dt=dt, dev=cuda, seed=1)
+    taps = _rand(9, 1280, dt=torch.float32, dev=cuda, scale=0.3, seed=2)
+    db = _rand(1280, dt=torch.float32, dev=cuda, scale=0.1, seed=3)
+    w2 = _rand(320, 1280, dt=dt, dev=cuda, scale=1280 ** -0.5, seed=4)
+    b2 = _rand(320, dt=torch.float32, dev=cuda, seed=5)
+    pk = ops.mixffn_dw_fc2_pack(taps, db, w2, 14)
+    ops.mixffn_dw_fc2(h, taps, db, w2, b2, packed=pk)                     # the matching pack runs
+    pk_short = ops.mixffn_dw_fc2_pack(taps[:, :640].contiguous(), db[:640].contiguous(), w2[:, :640].contiguous(), 14)
+    with pytest.raises(_lib.SvkError, match="packed buffer"):
+        ops.mixffn_dw_fc2(h, taps, db, w2, b2, packed=pk_short)          # built for K = 640
+    x = _rand(300, 64, dt=dt, dev=cuda, seed=6)
+    ops.colstats_set(x, out=torch.empty(2, 64, device=cuda))
+    for bad in (torch.empty(2, 32, device=cuda), torch.empty(64, 2, device=cuda).t()):
+        with pytest.raises(_lib.SvkError, match="colstats_set"):
+            ops.colstats_set(x, out=bad)

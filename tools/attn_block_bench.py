@@ -45,9 +45,9 @@ def run(N, C):
         from svk import _lib
         for rep in range(3):
             for sel, what in ((6, "4 waves x 256 queries"), (4, "8 waves x 512 queries"), (0, "8 waves x 256 queries")):
-                _lib.load().svk_tune(b"ffn_diag", sel)
+                _lib.load().svk_tune(b"attn_cfg", sel)
                 print(f"C=64 {what}: fused {timeit(fused):7.1f} us")
-        _lib.load().svk_tune(b"ffn_diag", 0)
+        _lib.load().svk_tune(b"attn_cfg", -1)
     tf = timeit(fused)
     tp = {k: timeit(f) for k, f in parts.items()}
     print(f"C={C}: fused {tf:7.1f} us | unfused {sum(tp.values()):7.1f} us = " + " + ".join(f"{k} {v:.1f}" for k, v in tp.items()))
