@@ -43,6 +43,10 @@ TORCH_DT = {"bf16": torch.bfloat16, "fp16": torch.float16, "fp32": torch.float32
 # algorithmic work of one extraction frame: the reference formulation of MiT-b2 + flow
 # minus the dead head work that the exact resize-first rewrite removes (10.77 - 1.08)
 EXTRACT_GFLOP_PER_FRAME = 9.69
+# per variant (b3 + flow 16.66 in the reference formulation; the head is the same, so the
+# resize-first rewrite removes the same 1.08): the callers' extraction model is mit_b3_evp
+# (generate_evp_LFB.py:412)
+EXTRACT_GFLOP = {"mit_b2_evp": EXTRACT_GFLOP_PER_FRAME, "mit_b3_evp": 16.66 - 1.08}
 # one train_evp stage-1 frame (forward + backward through every frozen block + SGD):
 # the count profiles/r03/bench_train.jsonl prices the train step against
 TRAIN_GFLOP_PER_FRAME = 25.94
@@ -96,13 +100,14 @@ def pmc_traffic(workload, kernel):
     return round(sum(v["hbm_bytes_per_launch"] * v["dispatches"] for v in ents) / n), src + " (all instantiations)"
 
 
-def pmc_mfma_busy(workload, dtype):
+def pmc_mfma_busy(workload, dtype, variant="mit_b2_evp"):
     """Whole-step MFMA busy fraction from the committed rocprofv3 counter pass (tools/pmc_mfma.py):
     sum of SQ_VALU_MFMA_BUSY_CYCLES over the step's kernels / (SIMDs x the step's GPU-active cycles)."""
     path = _profile_json("pmc_mfma.json")
     try:
         with open(path) as f:
-            rec = json.load(f)[f"{workload}_{dtype}"]
+            table = json.load(f)
+        rec = table[f"{workload}_{dtype}" if variant == "mit_b2_evp" else f"{workload}_{variant}_{dtype}"]
     except (OSError, ValueError, KeyError, TypeError):
         return None
     return dict(rec, source=os.path.relpath(path, REPO))
@@ -830,7 +835,8 @@ def timed(step, steps, world):
     return out, float(dt.item())
 
 
-def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value, world, dump_gemm=None):
+def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value, world, dump_gemm=None,
+                variant="mit_b2_evp"):
     """Dominant kernel (the GEMM / conv instantiation with the most HIP-event device time over the profiled
     eager iterations) priced against its roof: algorithmic FLOP or bytes per launch / average launch time."""
     per, shapes = {}, {}
@@ -868,14 +874,15 @@ def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value
                 "kernel_tflops": round(tflops, 2), "kernel_gbs": round(gbs, 1),
                 "all_gemm_tflops": round(sum(v[1] for v in per.values()) / (gemm_ms * 1e-3) / 1e12, 2),
                 "gemm_share_of_step": round(gemm_ms / prof_steps / (elapsed * 1e3 / steps), 3)}
-    if workload in ("extract", "e2e"):
+    if workload in ("extract", "e2e") and variant in EXTRACT_GFLOP:
         # whole-step MFMA utilisation: measured frames/s x algorithmic work / dense peak
-        roofline["step_mfma_util"] = round(value / world * EXTRACT_GFLOP_PER_FRAME * 1e9 / (peak * 1e12), 4)
-        roofline["step_gflop_per_frame"] = EXTRACT_GFLOP_PER_FRAME
+        gf = EXTRACT_GFLOP[variant]
+        roofline["step_mfma_util"] = round(value / world * gf * 1e9 / (peak * 1e12), 4)
+        roofline["step_gflop_per_frame"] = round(gf, 2)
     elif workload == "train":
         roofline["step_mfma_util"] = round(value / world * TRAIN_GFLOP_PER_FRAME * 1e9 / (peak * 1e12), 4)
         roofline["step_gflop_per_frame"] = TRAIN_GFLOP_PER_FRAME
-    busy = pmc_mfma_busy(workload, dtype_name)
+    busy = pmc_mfma_busy(workload, dtype_name, variant)
     if busy is not None:
         roofline["mfma_busy_counters"] = busy
     traffic, src = pmc_traffic(workload, name)
@@ -926,13 +933,13 @@ def run_leg(args, dev, rank, world, dtype):
                 torch.cuda.synchronize()
                 ops.set_profiler(None)
                 other[name]["roofline"] = roofline_of(rec2, prof_steps, el2, n2, args.workload, name,
-                                                      world * units * n2 / el2, world, None)
+                                                      world * units * n2 / el2, world, None, args.variant)
             step.set_dtype(dtype)
     value = world * units * args.steps / elapsed
     f32_only = args.workload in ("mstcn", "mamba", "preproc", "tecno_train", "augment")
     dtype_name = "fp32" if f32_only else args.dtype
     roofline = roofline_of(records, prof_steps, elapsed, args.steps, args.workload, dtype_name, value, world,
-                           args.dump_gemm if rank == 0 else None)
+                           args.dump_gemm if rank == 0 else None, args.variant)
     leg = {"value": round(value, 2), "unit": "frames/s", "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "dtype": dtype_name, "config": config,
            "roofline": roofline}
@@ -945,12 +952,19 @@ def other_workloads(args, dev, rank, world):
     """BASELINE.json's metric has two halves and config 5 a chain: on the headline run (N = 1) the same box
     also times the train_evp step (config 2: B = 88, bf16, graph-replayed) and the config-5 chain (fp16,
     256-frame chunks, graph-replayed), each with its own dominant-kernel roofline and CPU baseline (the
-    chain's carries the one-off GPU-vs-oracle check of the benched configuration)."""
+    chain's carries the one-off GPU-vs-oracle check of the benched configuration), and the callers' own
+    extraction model, mit_b3_evp (generate_evp_LFB.py:412; 18 stage-3 blocks), at fp16 and fp32 on the same
+    B = 256 synthetic batch (VERDICT r05 #8), each dtype with its own roofline."""
     legs = {}
-    for name, argv in (("train", ["--workload", "train", "--steps", "10", "--warmup", "3"]),
-                       ("e2e_config5", ["--workload", "e2e", "--steps", "10", "--warmup", "3"])):
-        a = parse_args(argv + ["--variant", args.variant, "--cpu-baseline-seconds",
-                               str(min(args.cpu_baseline_seconds, 10.0))])
+    b3 = "mit_b3_evp"
+    for name, argv in (("train", ["--workload", "train", "--steps", "10", "--warmup", "3", "--variant", args.variant]),
+                       ("e2e_config5", ["--workload", "e2e", "--steps", "10", "--warmup", "3",
+                                        "--variant", args.variant]),
+                       ("extract_" + b3, ["--workload", "extract", "--steps", "10", "--warmup", "3", "--variant", b3,
+                                          "--other-dtypes", "fp32"])):
+        if name.startswith("extract_") and args.variant == b3:
+            continue                                 # the headline already is b3
+        a = parse_args(argv + ["--cpu-baseline-seconds", str(min(args.cpu_baseline_seconds, 10.0))])
         try:
             leg, cpu_fn = run_leg(a, dev, rank, world, TORCH_DT[a.dtype])
             if not args.no_cpu_baseline:

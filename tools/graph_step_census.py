@@ -64,6 +64,36 @@ def analyse(args):
         foreign = collections.Counter(r["Kernel_Name"][:90] for r in st if "svk" not in r["Kernel_Name"])
         print(f"step {k}: {len(st)} launches, span {(e1 - s0) / 1e6:.3f} ms, sum of kernel times {busy / 1e6:.3f} ms, "
               f"non-svk: {dict(foreign) if foreign else 'none'}")
+    if steps:   # critical path: per queue, the union of its kernels' intervals vs the step's span
+        use = steps[1:] or steps
+        tot = collections.defaultdict(float)
+        span_sum = 0.0
+        for st in use:
+            s0, e1 = int(st[0]["Start_Timestamp"]), max(int(r["End_Timestamp"]) for r in st)
+            span_sum += e1 - s0
+            byq = collections.defaultdict(list)
+            for r in st:
+                byq[r["Queue_Id"]].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
+            allq = [iv for v in byq.values() for iv in v]
+            for q, ivs in list(byq.items()) + [("any", allq)]:
+                ivs.sort()
+                busy, cs, ce = 0, None, None
+                for a, b in ivs:
+                    if ce is None or a > ce:
+                        busy += 0 if ce is None else ce - cs
+                        cs, ce = a, b
+                    else:
+                        ce = max(ce, b)
+                busy += ce - cs
+                tot[q] += busy
+        n = len(use)
+        span = span_sum / n / 1e3
+        main_q = max((q for q in tot if q != "any"), key=lambda q: tot[q])   # the queue carrying most of the step
+        print(f"critical path: span {span:.1f} us per step; main queue q{main_q} busy {tot[main_q] / n / 1e3:.1f} us "
+              f"({tot[main_q] / span_sum:.3f} of the span, idle {(span_sum - tot[main_q]) / n / 1e3:.1f} us); "
+              + "; ".join(f"q{q} busy {v / n / 1e3:.1f} us" for q, v in sorted(tot.items()) if q not in (main_q, "any"))
+              + f"; any queue busy {tot['any'] / n / 1e3:.1f} us ({tot['any'] / span_sum:.3f} of the span: the GPU idles "
+              f"{(span_sum - tot['any']) / n / 1e3:.1f} us per step between kernels)")
     if args.by_kernel and steps:   # per-kernel time per replayed step (all replays but the first)
         use = steps[1:] or steps
         agg, cnt = collections.Counter(), collections.Counter()

@@ -8,7 +8,10 @@ inter-kernel gaps are not counted).  ``calibration`` = measured MFMA busy cycles
 its algorithmic MFMA cycles (FLOPs / 1024: a v_mfma_f32_16x16x32 instruction is 16384 FLOP in 16
 cycles), i.e. how the counter's unit relates to issued MFMA work on this ROCm.
 
-Usage: python tools/pmc_mfma.py COUNTER_CSV OUT_JSON KEY STEPS [KERNEL_SUBSTR FLOP_PER_LAUNCH]"""
+Usage: python tools/pmc_mfma.py COUNTER_CSV OUT_JSON KEY STEPS [KERNEL_SUBSTR FLOP_PER_LAUNCH] [--graph]
+--graph: STEPS is the number of graph replays the profiled program ended with (tools/graph_step_census.py run);
+only those dispatches are counted (the product step: no eager warm-up, input staging or torch copies), and the
+per-step figures divide by that true number of steps (VERDICT r05 #4)."""
 import csv
 import json
 import os
@@ -16,23 +19,30 @@ import sys
 from collections import defaultdict
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from pmc_traffic import kernel_key   # noqa: E402
+from pmc_traffic import graph_step_dispatches, kernel_key   # noqa: E402
 
 
 def main():
-    path, out_json, key, steps = sys.argv[1], sys.argv[2], sys.argv[3], float(sys.argv[4])
-    dom = sys.argv[5] if len(sys.argv) > 5 else None
-    dom_flop = float(sys.argv[6]) if len(sys.argv) > 6 else None
+    argv = [a for a in sys.argv[1:] if a != "--graph"]
+    graph = "--graph" in sys.argv
+    path, out_json, key, steps = argv[0], argv[1], argv[2], float(argv[3])
+    dom = argv[4] if len(argv) > 4 else None
+    dom_flop = float(argv[5]) if len(argv) > 5 else None
+    keep, counts = graph_step_dispatches(path, int(steps)) if graph else (None, None)
     per = defaultdict(lambda: defaultdict(float))       # (dispatch id) -> counter -> value
     names = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            d = r.get("Dispatch_Id") or r.get("Correlation_Id")
+            d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            if keep is not None and d not in keep:
+                continue
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
             names[d] = kernel_key(r["Kernel_Name"])
     busy = sum(v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for v in per.values())
     gui = sum(v.get("GRBM_GUI_ACTIVE", 0.0) for v in per.values())
     rec = {"dispatches": len(per), "steps": steps,
+           "scope": (f"the last {int(steps)} graph-replayed steps ({counts} launches each)" if graph
+                     else "every dispatch of the profiled program"),
            "mfma_busy_cycles_per_step": busy / steps, "kernel_cycles_per_step": gui / 8 / steps,
            "step_mfma_busy_frac": busy / (1024.0 * gui / 8) if gui else None,
            "formula": "sum SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x sum GRBM_GUI_ACTIVE / 8) over the step's dispatches"}

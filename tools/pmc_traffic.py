@@ -3,7 +3,8 @@ pass, MI355X_MICROARCH.md 'HBM'): bytes = 2 x FETCH_SIZE x 1024 (gfx950 FETCH_SI
 bytes of a wide streaming read) + WRITE_SIZE x 1024, averaged over every dispatch of a kernel.
 Writes {workload: {kernel: {...}}} into a JSON file that bench.py reads for roofline.traffic.
 
-Usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON WORKLOAD"""
+Usage: python tools/pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON WORKLOAD [GRAPH_STEPS]
+GRAPH_STEPS: keep only the dispatches of the last GRAPH_STEPS replayed graph steps (graph_step_census.py run)."""
 import csv
 import json
 import os
@@ -48,10 +49,34 @@ def kernel_key(name):
     return n
 
 
-def per_kernel(path, counter):
+def graph_step_dispatches(path, steps, last_kernel="mean_rows"):
+    """Dispatch ids of the last ``steps`` replayed graph steps of a counter CSV (the counter
+    passes must describe the product step only).  The profiled program (tools/graph_step_census.py run) ends
+    with ``steps`` replays of the captured extraction step and nothing else; dispatches are ordered by id and
+    split after each step's last kernel (``last_kernel``).  Returns (ids, per-step launch counts)."""
+    order = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            order[d] = r["Kernel_Name"]
+    groups, cur = [], []
+    for d in sorted(order):
+        cur.append(d)
+        if last_kernel in order[d]:
+            groups.append(cur)
+            cur = []
+    use = groups[-steps:]
+    if len(use) < steps:
+        raise SystemExit(f"{path}: only {len(use)} complete steps found, {steps} asked")
+    return {d for g in use for d in g}, [len(g) for g in use]
+
+
+def per_kernel(path, counter, keep=None):
     vals = defaultdict(list)
     with open(path) as f:
         for r in csv.DictReader(f):
+            if keep is not None and int(r.get("Dispatch_Id") or r.get("Correlation_Id")) not in keep:
+                continue
             if r["Counter_Name"] == counter:
                 vals[kernel_key(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return vals
@@ -59,7 +84,10 @@ def per_kernel(path, counter):
 
 def main():
     fetch_csv, write_csv, out_json, workload = sys.argv[1:5]
-    fetch, write = per_kernel(fetch_csv, "FETCH_SIZE"), per_kernel(write_csv, "WRITE_SIZE")
+    gsteps = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    kf = graph_step_dispatches(fetch_csv, gsteps)[0] if gsteps else None
+    kw = graph_step_dispatches(write_csv, gsteps)[0] if gsteps else None
+    fetch, write = per_kernel(fetch_csv, "FETCH_SIZE", kf), per_kernel(write_csv, "WRITE_SIZE", kw)
     table = {}
     for k in sorted(set(fetch) & set(write)):
         f, w = fetch[k], write[k]
@@ -71,6 +99,7 @@ def main():
         with open(out_json) as fh:
             data = json.load(fh)
     data[workload] = {"source": [os.path.relpath(fetch_csv), os.path.relpath(write_csv)],
+                      "scope": (f"the last {gsteps} graph-replayed steps only" if gsteps else "every dispatch"),
                       "formula": "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 per dispatch, averaged", "kernels": table}
     with open(out_json, "w") as fh:
         json.dump(data, fh, indent=1, sort_keys=True)
