@@ -129,9 +129,23 @@ __device__ __forceinline__ void gload4(float& v, const char* src) {
 // SPLIT: split-K — unit u = (tile u / ks, K part u % ks) covers nk K-steps of the tile's ks * nk; the
 // epilogue stores raw f32 partial sums to slab part (p.slab + (part * M + m) * N + n) and a separate
 // reduction adds the parts (+ bias, LayerNorm: svk_conv2d_ln_nhwc).
+//
+// -DSVK_DIAG (libsvk_diag.so, tools only): timing ablations from SVK_PK_DIAG — 1 drain the stores after each
+// epilogue, 2 no C stores, 4 no MFMAs (loads, barriers and fragment reads only), 8 every DMA re-reads the
+// workgroup's first tile's K-step 0 (L2-hot operands).  The product build has no such path.
+#ifdef SVK_DIAG
+#define PK_DIAG_PARAM , int diag
+#define PK_DIAG_ARG , diag_knob("SVK_PK_DIAG")
+#else
+#define PK_DIAG_PARAM
+#define PK_DIAG_ARG
+#endif
 template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
 __global__ __launch_bounds__(Cfg::NT, Cfg::OCC)
-void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
+void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_PARAM) {
+#ifndef SVK_DIAG
+  constexpr int diag = 0;
+#endif
   typedef v8_t<T> tx8;
   constexpr int BM = Cfg::BM, BN = Cfg::BN, NS = Cfg::NSTAGE;
   constexpr int WM = BM / Cfg::WGM, WN = BN / Cfg::WGN, TM = WM / 16, TN = WN / 16;
@@ -158,6 +172,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
   // live == false: past the workgroup's last (tile, K-step) — the same instructions run (branch-free
   // around the DMA issue) with every source replaced by the zero block
   auto issue = [&](int unit, int kt, int buf, bool live) {
+    if (diag & 8) { unit = first; kt = 0; }
     const int tile = SPLIT ? unit / ks : unit, part = unit - tile * ks;
     const int m0 = (tile / ntn) * BM, n0 = (tile % ntn) * BN, k0 = (SPLIT ? part * nk + kt : kt) * Cfg::BK;
     const uint32_t sa = lds0 + buf * Cfg::STAGE, sb = sa + Cfg::A_BYTES;
@@ -191,7 +206,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
     } else if constexpr (SOFF) {
       // a new tile's first K-step: the per-lane offsets; past the last unit (live == false) the last live tile's
       // offsets stay and the DMA re-reads its K-step 0 into a stage nobody reads any more (in bounds, no select)
-      if (live && kt == 0) {
+      if (live && (kt == 0 || (diag & 8))) {
 #pragma unroll
         for (int i = 0; i < Cfg::A_LD; ++i) {
           const int q = (wave * Cfg::A_LD + i) * 64 + lane;
@@ -255,6 +270,13 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const tx8*>(sa + (wm * WM + i * 16 + fr) * 128 + cc);
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const tx8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
+      if (diag & 4) {                   // (diagnostic build) keep the fragment reads alive, skip the MFMAs
+#pragma unroll
+        for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
+#pragma unroll
+        for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(fb[j]));
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -393,7 +415,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
           const int row = wm * WM + i * 16 + fr, col = wn * WN + j * 16 + fq * 4;
           *reinterpret_cast<uint2*>(stile + row * (BN * 2) + (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col >> 2) & 1) * 8) =
               *reinterpret_cast<const uint2*>(o);
-        } else if (m < p.M && n < p.N) {   // N % 4 == 0: a 4-column group is all-in or all-out
+        } else if (m < p.M && n < p.N && !(diag & 2)) {   // N % 4 == 0: a 4-column group is all-in or all-out
           *reinterpret_cast<uint2*>(C + (long)m * p.ldc + n) = *reinterpret_cast<const uint2*>(o);
         }
       }
@@ -410,7 +432,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
         const int row = idx / CPR, c = idx % CPR;
         const uint4 v = *reinterpret_cast<const uint4*>(stile + row * (BN * 2) + ((c ^ (row & (CPR - 1))) << 4));
         const int m = m0 + row, n = n0 + c * 8;
-        if (m < p.M && n < p.N) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
+        if (m < p.M && n < p.N && !(diag & 2)) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
       }
       barrier_mem();   // the next step's DMA overwrites this stage buffer
     }
@@ -465,6 +487,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks) {
       case SVK_ACT_TANH: epilogue(tile, std::integral_constant<int, SVK_ACT_TANH>{}); break;
       default: epilogue(tile, std::integral_constant<int, 0>{}); break;
     }
+    if (diag & 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (diagnostic build) drain the stores
   }
   // the last step's zero-block DMA is still in flight: retire it before the wave (and the workgroup's
   // LDS allocation) ends
@@ -501,7 +524,7 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
   hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
-                     (int)ntiles, nk, ks);
+                     (int)ntiles, nk, ks PK_DIAG_ARG);
   static char name[112];
   if (!name[0])
     snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", type_name<T>(), Cfg::BM, Cfg::BN,
@@ -644,6 +667,12 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 40: return launch_pk_k<T, PkCfg<128, 160, 2, 2, 2>, 0>(a, st, false);
     case 50: return launch_pk_k<T, PkCfg<256, 128, 4, 2, 2>, 0>(a, st, false);
     case 60: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, true);   // 128 x 128, staged epilogue
+    // round 6 sweep candidates: 8-wave 128 x 128 (64 x 32 / 32 x 64 per wave: 4 waves per SIMD at 2 workgroups per
+    // CU), 8-wave 128 x 256 (64 x 64 per wave, one workgroup per CU), 8-wave 128 x 128 with a 3-stage ring
+    case 80: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 2>, 0>(a, st, true);
+    // (32 x 64 per wave, PkCfg<128, 128, 4, 2, 2>: the f16 ELDS instantiation spills 3 VGPRs at the 128-register budget)
+    case 82: return launch_pk_k<T, PkCfg<128, 256, 2, 4, 2>, 0>(a, st, false);
+    case 84: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 3>, 0>(a, st, true);
     // (256 x 256 with 4 waves: 512 registers and ~15 VGPR spills, which the counted DMA waits cannot tolerate;
     // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128, and 256 x 256 with 8 waves of
     // 128 x 64 (225 VGPRs, one workgroup per CU) 1.2-2x slower: per-tile prologue / epilogue / store drain

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6, first GPU call: GPU suite after the diag/ADVICE changes, the default bench line (now with the mit_b3
-# legs), the replayed-step census with the critical-path figure, and the counter passes scoped to the replayed
-# graph steps (pmc_mfma / pmc_traffic --graph).
+# legs), the replayed-step census with the critical-path figure, the counter passes scoped to the replayed
+# graph steps (pmc_mfma / pmc_traffic --graph), and the GEMM tile sweep + ablations (diagnostic library).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 O=gpurun_out/r06a
@@ -9,6 +9,12 @@ mkdir -p $O
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ "$rc" -eq 0 ] || exit $rc; }
 step pytest timeout -k 10 900 python -u -m pytest tests -m gpu -q -x -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 tail -1 $O/pytest_gpu.log
+step sweep timeout -k 10 300 python tools/pk_cfg_sweep.py --cfgs -1,60,80,82,84,100 --shapes "s3 fc1,head,s4 fc2,s4 fc1,s2 fc2,s3 fc2,s4 kv" > $O/sweep.txt 2>&1
+cat $O/sweep.txt | grep -v amdgpu.ids | cut -c1-400
+for d in 0 1 2 4 8 12; do
+  SVK_LIB=$PWD/deep-learning-for-surgical-video-analysis_amd/svk/libsvk_diag.so SVK_PK_DIAG=$d step diag$d timeout -k 10 120 python tools/pk_cfg_sweep.py --cfgs 60 --rounds 3 --shapes "s3 fc1,head" > $O/diag$d.txt 2>&1
+  echo "diag=$d: $(grep -v amdgpu.ids $O/diag$d.txt | cut -c1-120 | tr '\n' ' ')"
+done
 step bench timeout -k 10 600 python bench.py > $O/bench_default.log 2>&1
 grep '^{' $O/bench_default.log | tail -1 > $O/bench_default.json
 cut -c1-200 $O/bench_default.json
