@@ -702,9 +702,14 @@ def test_train_graph_replay_matches_eager(cuda):
     # biases in front of a batch-statistics BatchNorm)
     na = sum(ua[n].pow(2).sum() for n in ua).sqrt().item()
     ee = sum((ua[n] - ub[n]).pow(2).sum() for n in ua).sqrt().item() / na
-    eg = sum((ua[n] - ug[n]).pow(2).sum() for n in ua).sqrt().item() / na
-    print(f"relative update distance: graph-vs-eager {eg:.3e}, eager-vs-eager {ee:.3e}")
-    assert eg <= 3 * ee + 1e-3, (eg, ee)
+    # the graph run against the NEARER eager run: the bf16 step is not bit-reproducible (f32 atomics in the
+    # weight gradients), and at B = 4 one ReLU gate at its kink can land on either side, which moves the whole
+    # 3-step update by ~1.5e-2 relative — observed both as eager-vs-eager 1.55e-2 / graph-vs-eager 2.6e-3 (a
+    # round-4 run) and as 2.9e-3 / 1.5e-2 (round 6, first box).  A capture bug (stale masks, parameters or BN
+    # buffers in the replay) moves it by O(0.1-1), so the bound keeps a 0.03 floor above that bimodal spread.
+    eg = min(sum((u[n] - ug[n]).pow(2).sum() for n in u).sqrt().item() for u in (ua, ub)) / na
+    print(f"relative update distance: graph-vs-nearest-eager {eg:.3e}, eager-vs-eager {ee:.3e}")
+    assert eg <= max(3 * ee + 1e-3, 0.03), (eg, ee)
     _close(rg, ra, 1e-2)
 
 
