@@ -7,10 +7,10 @@ export TMPDIR=/tmp
 O=gpurun_out/r06a
 mkdir -p $O
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ "$rc" -eq 0 ] || exit $rc; }
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+[ -n "$SKIP_PYTEST" ] || timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
 case $rc in 0|1) ;; *) exit $rc;; esac   # test failures: go on; a crash / timeout: stop
-step sweep timeout -k 10 300 python tools/pk_cfg_sweep.py --cfgs -1,60,80,82,84,100 --shapes "s3 fc1,head,s4 fc2,s4 fc1,s2 fc2,s3 fc2,s4 kv" > $O/sweep.txt 2>&1
+step sweep timeout -k 10 300 python tools/pk_cfg_sweep.py --cfgs=-1,60,80,82,84,100 --shapes "s3 fc1,head,s4 fc2,s4 fc1,s2 fc2,s3 fc2,s4 kv" > $O/sweep.txt 2>&1
 cat $O/sweep.txt | grep -v amdgpu.ids | cut -c1-400
 for d in 0 1 2 4 8 12; do
   SVK_LIB=$PWD/deep-learning-for-surgical-video-analysis_amd/svk/libsvk_diag.so SVK_PK_DIAG=$d step diag$d timeout -k 10 120 python tools/pk_cfg_sweep.py --cfgs 60 --rounds 3 --shapes "s3 fc1,head" > $O/diag$d.txt 2>&1
