@@ -458,13 +458,20 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   };
   // One pipeline step: top up the DMA ring (into the stage computed one step ago), wait for the
   // oldest stage `buf` (the NS - 1 steps issued after it may stay in flight), compute from it.  The
-  // epilogue operands of a tile are issued just before the DMA of its step nk - NS + 1 (NS - 1 steps
-  // before its last step), so on the last step they are older than every step still allowed in
-  // flight: the same unconditional wait retires them (the host keeps nk >= NS - 1).
+  // epilogue operands of a tile are issued just before the DMA of its step nk - EA (EA = min(NS - 1, 2)
+  // steps before its last step), and the last step's wait leaves only the EA youngest DMA steps in flight,
+  // so it retires them (the host keeps nk >= EA).  (Round 6: with deeper rings the operands held NS - 1 steps
+  // made hipcc move their registers before the wait — isa_check; two steps is what the 3-stage ring always
+  // used, and the deep rings pay a shallower wait once per tile.)
+  constexpr int EA = NS - 1 < 2 ? NS - 1 : 2;
   auto step = [&](bool last) {
     issue_next();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * Cfg::LD) : "memory");
-    if (last) tie_epi();               // the epilogue loads are older than the NS - 1 steps still in flight
+    if (last) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(EA * Cfg::LD) : "memory");
+      tie_epi();                       // the epilogue loads are older than the EA steps still in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * Cfg::LD) : "memory");
+    }
     barrier_mem();
     compute(buf);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -476,10 +483,10 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   for (int s = 0; s < NS - 1; ++s) issue_next();
   for (int tile = first; tile < ntiles; tile += G) {
     for (int kt = 0; kt < nk - 1; ++kt) {
-      if (kt == nk - NS + 1) epi_load(tile);    // (NS > 2) fly during the last NS - 1 steps
+      if (EA > 1 && kt == nk - EA) epi_load(tile);    // (NS > 2) fly during the last EA steps
       step(false);
     }
-    if (NS == 2) epi_load(tile);      // epilogue operands fly during the last step's wait and MFMAs
+    if (EA == 1) epi_load(tile);      // epilogue operands fly during the last step's wait and MFMAs
     step(true);
     switch (EXT ? p.uact : p.act) {
       case SVK_ACT_GELU: epilogue(tile, std::integral_constant<int, SVK_ACT_GELU>{}); break;
@@ -509,8 +516,9 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ks = SPLIT ? a.ksplit : 1;
   const long ntiles = (long)ntm * ntn * ks;
   const int nk = (a.K + 63) / 64 / ks;   // K-steps per unit (the caller makes ks divide them)
-  if (nk < Cfg::NSTAGE - 1) {             // the epilogue loads are issued NSTAGE - 2 steps before a tile's last
-    set_error("gemm_pk: %d K-steps per tile, the %d-stage ring needs %d", nk, Cfg::NSTAGE, Cfg::NSTAGE - 1);
+  constexpr int EA = Cfg::NSTAGE - 1 < 2 ? Cfg::NSTAGE - 1 : 2;
+  if (nk < EA) {                          // the epilogue loads are issued EA - 1 steps before a tile's last
+    set_error("gemm_pk: %d K-steps per tile, the %d-stage ring needs %d", nk, Cfg::NSTAGE, EA);
     return SVK_EUNSUPPORTED;
   }
   static const int slots =
@@ -569,7 +577,13 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
     if constexpr (Cfg::ELDS_FITS) {
       if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, false>(a, st) : launch_pk<T, Cfg, false, true, 0, false>(a, st);
     }
-    return tail ? launch_pk<T, Cfg, true, false, 0, false>(a, st) : launch_pk<T, Cfg, false, false, 0, false>(a, st);
+    // deep rings keep the register epilogue's operands in flight NSTAGE - 1 steps: hipcc then moves those
+    // registers before the counted wait retires them (isa_check), so deep rings run with the staged epilogue only
+    if constexpr (Cfg::NSTAGE > 2) {
+      return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, ASRC>(a, st, elds);
+    } else {
+      return tail ? launch_pk<T, Cfg, true, false, 0, false>(a, st) : launch_pk<T, Cfg, false, false, 0, false>(a, st);
+    }
   }
 }
 
@@ -642,7 +656,7 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   // Round-3 sweep (profiles/r03/pk_cfg_sweep.txt, every variant interleaved in one process): three-stage
   // rings (256x128 / 128x64 / 128x128 / 128x256-8-wave) never beat the two-stage tiles on the MiT-b2 shapes
   // and 256x256 with 8 waves spills (128 accumulator + 96 epilogue-operand VGPRs): not instantiated.  The
-  // kernel keeps NSTAGE generic (epilogue loads issued NSTAGE - 2 steps before a tile's last step).
+  // kernel keeps NSTAGE generic (epilogue loads issued min(NSTAGE - 1, 2) steps before a tile's last step).
   if (cfg == 40 && a.N % 160 != 0) cfg = 10;
   // 90 / 91 / 92 / 93: the wide-tile kernel (gemm_wt.hip: 256 x 256 / 256 x 160 / 256 x 128 / 256 x 192)
   if (asrc == 0 && cfg >= 90 && cfg <= 93 && gemm_wt_try<T>(a, st, cfg - 90) == 0) return 0;
@@ -673,6 +687,11 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     // (32 x 64 per wave, PkCfg<128, 128, 4, 2, 2>: the f16 ELDS instantiation spills 3 VGPRs at the 128-register budget)
     case 82: return launch_pk_k<T, PkCfg<128, 256, 2, 4, 2>, 0>(a, st, false);
     case 84: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 3>, 0>(a, st, true);
+    // deep rings, one 8-wave workgroup per CU: 3 / 4 K-steps (96 / 128 KiB) of LDS-DMA in flight per CU instead of
+    // the two workgroups' 2 x 1 (64 KiB) — the r06 ablations put the load pipeline, not the MFMAs, on the critical path
+    case 85: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 5>, 0>(a, st, true);
+    case 86: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 4>, 0>(a, st, true);
+    case 87: return launch_pk_k<T, PkCfg<128, 256, 2, 4, 3>, 0>(a, st, false);
     // (256 x 256 with 4 waves: 512 registers and ~15 VGPR spills, which the counted DMA waits cannot tolerate;
     // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128, and 256 x 256 with 8 waves of
     // 128 x 64 (225 VGPRs, one workgroup per CU) 1.2-2x slower: per-tile prologue / epilogue / store drain

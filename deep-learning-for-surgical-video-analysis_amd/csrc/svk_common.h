@@ -84,6 +84,82 @@ template <> __device__ __forceinline__ f32x2 unpack2<f16>(uint32_t u) {
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
 
+// ---- packed-f32 VALU (v_pk_fma / v_pk_mul / v_pk_add_f32: two f32 lanes per instruction, the rate of one
+// v_fma_f32).  hipcc is built with -packed-fp32-ops (Makefile: on gfx950 a v_pk_*_f32 whose low lane reads,
+// THROUGH op_sel, a VGPR the preceding VALU wrote is stale in lanes 48-63 under MFMA load), so packed f32
+// arithmetic is written by hand here: natural register pairs and the default op_sel only — the form
+// tools/hazard/pk_hazard.hip (variant 7: the same dependency without op_sel, MFMA load on the SIMD) measured
+// exact over 10.5 M lane results (profiles/r03/pk_hazard/pk_hazard.log).  csrc/isa_check.py admits v_pk_*_f32
+// only without op_sel / op_sel_hi.  A 64-bit SGPR pair is a legal packed source (one scalar operand per
+// instruction): constants are passed that way.
+constexpr unsigned long long kpair(float f) { return (unsigned long long)__builtin_bit_cast(unsigned, f) * 0x100000001ull; }
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, unsigned long long c) {   // c: SGPR pair
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(c));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, unsigned long long b, f32x2 c) {   // b: SGPR pair
+  f32x2 d;
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, f32x2 b) {
+  f32x2 d;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_mul(f32x2 a, unsigned long long b) {
+  f32x2 d;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "s"(b));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_rsub(unsigned long long a, f32x2 b) {             // a - b, a: SGPR pair
+  f32x2 d;
+  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "s"(a), "v"(b));
+  return d;
+}
+
+// GELU on a pair, erf form: relu(x) - |x| * 0.5 erfc(|x| / sqrt 2) with erfc(z) = t q(t) exp(-z^2),
+// t = 1 / (1 + c z).  |x| t = (1 - t) / c' (c' = c / sqrt 2), so the correction is (1 - t) (q(t) / c')
+// exp(-x^2 / 2): the rcp / exp2 / relu per element, everything else packed — per pair 4 VALU + 7 (NQ = 3) or
+// 9 (NQ = 5) packed + 4 transcendental, against 2 x (9 or 11) VALU + 4 transcendental element-wise.
+//   NQ = 3: Abramowitz & Stegun 7.1.25 (|erf err| <= 2.5e-5: mixffn_rw's gelu_rw);
+//   NQ = 5: 7.1.26 (|err| <= 1.5e-7: stencil / dw_fc2's gelu_rl).
+// (1 - t) loses relative precision as |x| -> 0, where the correction itself -> 0.5 |x|: its absolute error
+// stays within an f32 ulp of 1 times 0.5 |x| / (c' |x|) ~ 1.3e-7 — far below the 16-bit output rounding.
+template <int NQ>
+__device__ __forceinline__ f32x2 gelu_pk(f32x2 x) {
+  constexpr float c = NQ == 3 ? 0.47047f * 0.70710678118654752f : 0.3275911f * 0.70710678118654752f;
+  // q(t) / c, coefficients of -0.5 (a_1 + a_2 t + ...) (the 0.5 of Phi and the sign of the correction)
+  constexpr float s = -0.5f / c;
+  constexpr float a1 = NQ == 3 ? 0.3480242f : 0.254829592f, a2 = NQ == 3 ? -0.0958798f : -0.284496736f;
+  constexpr float a3 = NQ == 3 ? 0.7478556f : 1.421413741f, a4 = -1.453152027f, a5 = 1.061405429f;
+  f32x2 u, t, e;
+  u.x = fmaf(c, fabsf(x.x), 1.0f);
+  u.y = fmaf(c, fabsf(x.y), 1.0f);
+  t.x = __builtin_amdgcn_rcpf(u.x);
+  t.y = __builtin_amdgcn_rcpf(u.y);
+  f32x2 q;
+  if constexpr (NQ == 3) {
+    q = pk_fma(t, kpair(s * a3), f32x2{s * a2, s * a2});
+  } else {
+    q = pk_fma(t, kpair(s * a5), f32x2{s * a4, s * a4});
+    q = pk_fma(q, t, kpair(s * a3));
+    q = pk_fma(q, t, kpair(s * a2));
+  }
+  q = pk_fma(q, t, kpair(s * a1));
+  const f32x2 a = pk_mul(pk_rsub(kpair(1.0f), t), q);
+  const f32x2 w = pk_mul(pk_mul(x, x), kpair(-0.72134752044448170f));     // -x^2 / 2 * log2(e)
+  e.x = __builtin_amdgcn_exp2f(w.x);
+  e.y = __builtin_amdgcn_exp2f(w.y);
+  return pk_fma(a, e, f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)});
+}
+
 // Branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute): one rcp, one exp, five
 // FMAs — no range-split branches, so a wave never diverges.  Used by the bf16 kernels, whose outputs
 // are rounded to 8 significant bits anyway; the f32 parity path keeps erff.
