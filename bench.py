@@ -69,25 +69,36 @@ def synthetic_batch(B, dev, seed):
     return x.contiguous(), y.contiguous(), flow
 
 
-def _profile_json(name):
-    """Newest committed profiles/rNN/<name> (this round's collection first)."""
+def _profile_jsons(name):
+    """Committed profiles/rNN/<name>, newest round first."""
     base = os.path.join(REPO, "profiles")
     for r in sorted((d for d in os.listdir(base) if d.startswith("r")), reverse=True) if os.path.isdir(base) else []:
         path = os.path.join(base, r, name)
         if os.path.exists(path):
-            return path
-    return None
+            yield path
+
+
+def _profile_entry(name, key):
+    """(entry, path) of the newest committed profiles/rNN/<name> that holds ``key`` (a round's collection may
+    cover only some workloads: older rounds fill the rest)."""
+    for path in _profile_jsons(name):
+        try:
+            with open(path) as f:
+                table = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if key in table:
+            return table[key], path
+    return None, None
 
 
 def pmc_traffic(workload, kernel):
     """HBM bytes per launch of ``kernel`` from the committed rocprofv3 PMC passes of this workload
     (FETCH_SIZE / WRITE_SIZE in separate passes, gfx950 FETCH correction; tools/pmc_traffic.py)."""
-    path = _profile_json("pmc_traffic.json")
-    try:
-        with open(path) as f:
-            table = json.load(f)[workload]["kernels"]
-    except (OSError, ValueError, KeyError, TypeError):
+    ent, path = _profile_entry("pmc_traffic.json", workload)
+    if ent is None or "kernels" not in ent:
         return None, None
+    table = ent["kernels"]
     src = os.path.relpath(path, REPO)
     if kernel in table:
         return table[kernel]["hbm_bytes_per_launch"], src
@@ -103,12 +114,9 @@ def pmc_traffic(workload, kernel):
 def pmc_mfma_busy(workload, dtype, variant="mit_b2_evp"):
     """Whole-step MFMA busy fraction from the committed rocprofv3 counter pass (tools/pmc_mfma.py):
     sum of SQ_VALU_MFMA_BUSY_CYCLES over the step's kernels / (SIMDs x the step's GPU-active cycles)."""
-    path = _profile_json("pmc_mfma.json")
-    try:
-        with open(path) as f:
-            table = json.load(f)
-        rec = table[f"{workload}_{dtype}" if variant == "mit_b2_evp" else f"{workload}_{variant}_{dtype}"]
-    except (OSError, ValueError, KeyError, TypeError):
+    rec, path = _profile_entry("pmc_mfma.json",
+                               f"{workload}_{dtype}" if variant == "mit_b2_evp" else f"{workload}_{variant}_{dtype}")
+    if rec is None:
         return None
     return dict(rec, source=os.path.relpath(path, REPO))
 
@@ -836,7 +844,7 @@ def timed(step, steps, world):
 
 
 def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value, world, dump_gemm=None,
-                variant="mit_b2_evp"):
+                variant="mit_b2_evp", prof_elapsed=None):
     """Dominant kernel (the GEMM / conv instantiation with the most HIP-event device time over the profiled
     eager iterations) priced against its roof: algorithmic FLOP or bytes per launch / average launch time."""
     per, shapes = {}, {}
@@ -873,7 +881,10 @@ def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value
                 "arith_intensity_flop_per_byte": round(intensity, 1),
                 "kernel_tflops": round(tflops, 2), "kernel_gbs": round(gbs, 1),
                 "all_gemm_tflops": round(sum(v[1] for v in per.values()) / (gemm_ms * 1e-3) / 1e12, 2),
-                "gemm_share_of_step": round(gemm_ms / prof_steps / (elapsed * 1e3 / steps), 3)}
+                # GEMM device time of the profiled EAGER iterations over those iterations' own wall time (round 6:
+                # dividing by the graph-replayed step made it exceed 1)
+                "gemm_share_of_step": round(gemm_ms / (prof_elapsed * 1e3) if prof_elapsed
+                                            else gemm_ms / prof_steps / (elapsed * 1e3 / steps), 3)}
     if workload in ("extract", "e2e") and variant in EXTRACT_GFLOP:
         # whole-step MFMA utilisation: measured frames/s x algorithmic work / dense peak
         gf = EXTRACT_GFLOP[variant]
@@ -907,9 +918,12 @@ def run_leg(args, dev, rank, world, dtype):
         records = []
         ops.set_profiler(records)
         prof_steps = max(1, min(args.steps, 5))
+        torch.cuda.synchronize()
+        tp0 = time.perf_counter()
         for _ in range(prof_steps):
             (step.profile if hasattr(step, "profile") else step)()
         torch.cuda.synchronize()
+        prof_elapsed = time.perf_counter() - tp0
         ops.set_profiler(None)
         # the same inputs at the other compute dtypes (extraction): fp32 is the precision of the
         # reference's generate_evp_LFB.py, bf16 the narrower 16-bit format
@@ -928,18 +942,21 @@ def run_leg(args, dev, rank, world, dtype):
                 # priced against the 157 TF f32 MFMA peak), from profiled eager iterations of the same step
                 rec2 = []
                 ops.set_profiler(rec2)
+                torch.cuda.synchronize()
+                tp0 = time.perf_counter()
                 for _ in range(prof_steps):
                     (step.profile if hasattr(step, "profile") else step)()
                 torch.cuda.synchronize()
+                pe2 = time.perf_counter() - tp0
                 ops.set_profiler(None)
                 other[name]["roofline"] = roofline_of(rec2, prof_steps, el2, n2, args.workload, name,
-                                                      world * units * n2 / el2, world, None, args.variant)
+                                                      world * units * n2 / el2, world, None, args.variant, pe2)
             step.set_dtype(dtype)
     value = world * units * args.steps / elapsed
     f32_only = args.workload in ("mstcn", "mamba", "preproc", "tecno_train", "augment")
     dtype_name = "fp32" if f32_only else args.dtype
     roofline = roofline_of(records, prof_steps, elapsed, args.steps, args.workload, dtype_name, value, world,
-                           args.dump_gemm if rank == 0 else None, args.variant)
+                           args.dump_gemm if rank == 0 else None, args.variant, prof_elapsed)
     leg = {"value": round(value, 2), "unit": "frames/s", "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": round(elapsed * 1e3 / args.steps, 3), "dtype": dtype_name, "config": config,
            "roofline": roofline}
