@@ -345,6 +345,12 @@ __global__ __launch_bounds__(256) void dwfc2_pack(const float* __restrict__ taps
   }
 }
 
+// gelu_rl's formula on two packed pairs (svk_common.h gelu_pk<5>: the polynomial, squares and the final fma
+// as v_pk_*_f32, two chains interleaved; round 6) — not bit-identical to gelu_rl (|x| t is formed as (1 - t) / c)
+__device__ __forceinline__ f32x4 gelu4_pk(f32x4 x) {
+  const f32x2 a = gelu_pk<5>(f32x2{x[0], x[1]}), b = gelu_pk<5>(f32x2{x[2], x[3]});
+  return f32x4{a.x, a.y, b.x, b.y};
+}
 // gelu_rl (dwfc::gelu_rl, bit-identical) on four values in lockstep, so four independent chains interleave
 // (measured no faster than the per-element form in this kernel, kept for the explicit schedule)
 __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
@@ -378,7 +384,7 @@ __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
 
 // GELU = false: the activation is the identity — the data gradient of a frozen MixFFN's DWConv + fc1
 // (svk/train.py: dX = (dwconv3x3ᵀ dU) W1, the transposed depthwise conv being the conv with flipped taps)
-template <typename T, class C, bool GELU = true>
+template <typename T, class C, bool GELU = true, bool PKG = false>
 __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restrict__ Hm, const char* __restrict__ pk,
                                                                const float* __restrict__ b2, const T* __restrict__ R,
                                                                T* __restrict__ Y, int ntiles, int K) {
@@ -461,7 +467,7 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   auto gelu_store = [&](int gb) {
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
-      const f32x4 gv = GELU ? gelu4(dacc[m]) : dacc[m];
+      const f32x4 gv = GELU ? (PKG ? gelu4_pk(dacc[m]) : gelu4(dacc[m])) : dacc[m];
       const T o[4] = {from_f<T>(gv[0]), from_f<T>(gv[1]), from_f<T>(gv[2]), from_f<T>(gv[3])};
       const int s = (mb0 + m) * 16 + fr, cw = 16 * cb + 4 * fq;
       *reinterpret_cast<uint2*>(smem + C::G_OFF + gb * C::GBYTES + s * 128 + ((((cw >> 3) ^ (s & 7)) << 4) | ((cw & 4) << 1))) =
@@ -562,18 +568,25 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   }
 }
 
+
 template <typename T, class C, bool GELU = true>
 static int launch(const void* H, const void* pk, const float* b2, const void* R, void* Y, int B, int K, hipStream_t st) {
   const long nt = (long)B * C::TILES_PER_FRAME;
   if (nt > 0x7fffffffL || (long)B * C::WI * C::WI * K > 0x7fffffffL) return SVK_EUNSUPPORTED;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dwfc2_rw<T, C, GELU>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dwfc2_rw<T, C, GELU, false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dwfc2_rw<T, C, GELU, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL((dwfc2_rw<T, C, GELU>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H, (const char*)pk,
-                     b2, (const T*)R, (T*)Y, (int)nt, K);
+  if (GELU && gelu_pk_on())   // GELU on packed f32 pairs (svk_common.h gelu_pk; SVK_GELU_PK=0: element-wise)
+    hipLaunchKernelGGL((dwfc2_rw<T, C, GELU, true>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H,
+                       (const char*)pk, b2, (const T*)R, (T*)Y, (int)nt, K);
+  else
+    hipLaunchKernelGGL((dwfc2_rw<T, C, GELU, false>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H,
+                       (const char*)pk, b2, (const T*)R, (T*)Y, (int)nt, K);
   static char name[64];
   if (!name[0])
     snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d, %d>%s>", type_name<T>(), C::N, C::WI, GELU ? "" : ", identity");

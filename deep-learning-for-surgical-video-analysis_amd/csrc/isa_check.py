@@ -84,7 +84,9 @@ def check_packed(funcs):
     bad = []
     for f, ins in funcs.items():
         for addr, op, ops, _ in ins:
-            if re.match(r"v_pk_(add|mul|fma)_f32", op) or (op == "v_pk_mov_b32" and "op_sel" in ops):
+            # packed f32 arithmetic is allowed only with the default op_sel (the hand-written svk_common.h pk_*
+            # helpers): the gfx950 hazard needs a low lane read THROUGH op_sel (tools/hazard/pk_hazard.hip)
+            if (re.match(r"v_pk_(add|mul|fma)_f32", op) and "op_sel" in ops) or (op == "v_pk_mov_b32" and "op_sel" in ops):
                 bad.append(f"{f}+0x{addr:x}: {op} {ops}")
             if re.match(r"v_ashr_pk_[iu]8_i32", op):
                 bad.append(f"{f}+0x{addr:x}: {op} {ops} (16-bit result, upper half kept by the hardware)")

@@ -343,9 +343,10 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rw(const f16* __restrict
 // row's pair P_{y+1} = (hi(P_y), f16(fc1)) replaces P_{y-1} once its n-tile's dwconv has read it.  The
 // products of the f16 hidden values and f16 taps are exact in f32 (the conv of the reference's autocast
 // in f16 with f32 accumulation); only the summation order differs from the f32-FMA form.
-template <int C_, int W_, int R_, int OCC_>
+template <int C_, int W_, int R_, int OCC_, bool PKG_ = true>
 struct DCfg {
   static constexpr int C = C_, W = W_, R = R_, OCC = OCC_;
+  static constexpr bool PKG = PKG_;                  // GELU on packed f32 pairs (svk_common.h gelu_pk<3>, round 6)
   static constexpr int HID = 4 * C, NW = HID / 64, NT = 64 * NW;
   static constexpr int KS = C / 32, NC2 = C / 16, XT = (W + 13) / 14;
   static constexpr int TPW = 16 / NW, LPT = 64 / TPW;
@@ -594,8 +595,16 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rwd(const f16* __restric
 #pragma unroll
           for (int c = 0; c < 4; ++c) P[S0][j][c] = hpair(P[S1][j][c], hv[c]);
         }
+        if constexpr (K::PKG) {
+          const f32x2 g01 = gelu_pk<3>(f32x2{acc[0], acc[1]}), g23 = gelu_pk<3>(f32x2{acc[2], acc[3]});
+          g[j >> 1][4 * (j & 1) + 0] = (_Float16)g01.x;
+          g[j >> 1][4 * (j & 1) + 1] = (_Float16)g01.y;
+          g[j >> 1][4 * (j & 1) + 2] = (_Float16)g23.x;
+          g[j >> 1][4 * (j & 1) + 3] = (_Float16)g23.y;
+        } else {
 #pragma unroll
-        for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)gelu_rw(acc[c]);
+          for (int c = 0; c < 4; ++c) g[j >> 1][4 * (j & 1) + c] = (_Float16)gelu_rw(acc[c]);
+        }
         if (j & 1) {   // a complete 32-channel k-step of fc2
 #pragma unroll
           for (int c = 0; c < NC2; ++c)
@@ -626,10 +635,11 @@ __global__ __launch_bounds__(K::NT, K::OCC) void mixffn_rwd(const f16* __restric
 // walks only units of its own hidden block).  No cross-wave reduction, no per-row barrier.  Per row and
 // wave: 4 KS fc1 MFMAs (hidden row y + 2, X loaded a row ahead), the 3x3 taps as DPP-fused v_fmac (taps
 // streamed from LDS one step ahead), GELU, 8-byte f16 stores of the 4 x 4 channels of the lane's token.
-template <int C_, int W_, int R_, bool BI_ = true>
+template <int C_, int W_, int R_, bool BI_ = true, bool PKG_ = true>
 struct DwCfg {
   static constexpr int C = C_, W = W_, R = R_;
   static constexpr bool BIAS_INIT = BI_;
+  static constexpr bool PKG = PKG_;                  // GELU on packed f32 pairs (gelu_pk<3>, round 6)
   static constexpr int KS = C / 32, XT = (W + 13) / 14, NT = 256;
   static constexpr int TBLK = 160;                  // tap block (wave, n-tile, fq): taps [9][4], dwb [4] (f32)
   static constexpr int LDS_TP = 256 * 4;            // b1 of the workgroup's 256 channels | tap blocks
@@ -748,9 +758,14 @@ __global__ __launch_bounds__(K::NT, 2) void fc1dw_rw(const f16* __restrict__ XN,
           if (jd + 1 < 12) tload(jd + 1, tq[(jd + 1) & 1]);
           taps3(acc, win[(ROT + dy) % 3][j], tq[jd & 1]);
         }
-        if (st)
-          *reinterpret_cast<f16x4*>(gy + 16 * j) =
-              f16x4{(f16)gelu_rw(acc[0]), (f16)gelu_rw(acc[1]), (f16)gelu_rw(acc[2]), (f16)gelu_rw(acc[3])};
+        if constexpr (K::PKG) {
+          const f32x2 g01 = gelu_pk<3>(f32x2{acc[0], acc[1]}), g23 = gelu_pk<3>(f32x2{acc[2], acc[3]});
+          if (st) *reinterpret_cast<f16x4*>(gy + 16 * j) = f16x4{(f16)g01.x, (f16)g01.y, (f16)g23.x, (f16)g23.y};
+        } else {
+          if (st)
+            *reinterpret_cast<f16x4*>(gy + 16 * j) =
+                f16x4{(f16)gelu_rw(acc[0]), (f16)gelu_rw(acc[1]), (f16)gelu_rw(acc[2]), (f16)gelu_rw(acc[3])};
+        }
       }
       fc1_pack(y + 2, a1, win[ROT]);
     };
@@ -810,6 +825,8 @@ int fc1dw_rw_try(int dtype, const void* XN, const void* W1, const float* b1, con
   static const int var = getenv("SVK_RW_VAR") ? atoi(getenv("SVK_RW_VAR")) : 0;   // 2: bias added after the MFMAs
   if (var == 2)
     return fc1dw_rw_launch<ffnrw::DwCfg<128, 28, 28, false>>(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, st);
+  if (var == 4 || !gelu_pk_on())   // element-wise GELU (SVK_GELU_PK=0)
+    return fc1dw_rw_launch<ffnrw::DwCfg<128, 28, 28, true, false>>(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, st);
   return fc1dw_rw_launch<ffnrw::DwCfg<128, 28, 28>>(dtype, XN, W1, b1, taps, dbias, G, B, H, W, C, hidden, act, st);
 }
 
@@ -868,5 +885,7 @@ extern "C" int svk_mixffn_rw(int dtype, const void* XN, const void* X, const voi
   // 3: the f32-FMA tap form (mixffn_rw); default: the f16-pair dot-product taps (mixffn_rwd), 310 vs 319 us
   // (profiles/r05/mixffn_rwd.txt; its 3-waves-per-SIMD build spills and ran 440 us)
   if (var == 3) return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  if (var == 4 || !gelu_pk_on())   // element-wise GELU (SVK_GELU_PK=0)
+    return ffnrw::launch<ffnrw::DCfg<64, 56, 28, 2, false>, true>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
   return ffnrw::launch<ffnrw::DCfg<64, 56, 28, 2>, true>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
 }

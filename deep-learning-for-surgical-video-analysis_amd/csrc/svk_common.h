@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <math.h>
 
 #include "../../include/svk.h"
@@ -132,6 +133,11 @@ __device__ __forceinline__ f32x2 pk_rsub(unsigned long long a, f32x2 b) {       
 //   NQ = 5: 7.1.26 (|err| <= 1.5e-7: stencil / dw_fc2's gelu_rl).
 // (1 - t) loses relative precision as |x| -> 0, where the correction itself -> 0.5 |x|: its absolute error
 // stays within an f32 ulp of 1 times 0.5 |x| / (c' |x|) ~ 1.3e-7 — far below the 16-bit output rounding.
+// host switch: SVK_GELU_PK=0 selects the element-wise GELU kernels (A/B runs)
+inline bool gelu_pk_on() {
+  static const bool on = getenv("SVK_GELU_PK") ? atoi(getenv("SVK_GELU_PK")) != 0 : true;
+  return on;
+}
 template <int NQ>
 __device__ __forceinline__ f32x2 gelu_pk(f32x2 x) {
   constexpr float c = NQ == 3 ? 0.47047f * 0.70710678118654752f : 0.3275911f * 0.70710678118654752f;
