@@ -93,6 +93,10 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + e
 // exact over 10.5 M lane results (profiles/r03/pk_hazard/pk_hazard.log).  csrc/isa_check.py admits v_pk_*_f32
 // only without op_sel / op_sel_hi.  A 64-bit SGPR pair is a legal packed source (one scalar operand per
 // instruction): constants are passed that way.
+// The hazard recognizer does not see inside inline asm: a VALU read of a TRANSCENDENTAL result (v_rcp / v_exp
+// ...) needs one wait state on gfx950 (the compiler adds it for its own instructions, not for an asm consumer —
+// the first build of gelu_pk read stale rcp / exp results and failed every GELU test, r06c), so the helpers that
+// consume rcp / exp2 outputs (pk_fma_tr, pk_rsub) open with s_nop 0.
 constexpr unsigned long long kpair(float f) { return (unsigned long long)__builtin_bit_cast(unsigned, f) * 0x100000001ull; }
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
   f32x2 d;
@@ -119,16 +123,27 @@ __device__ __forceinline__ f32x2 pk_mul(f32x2 a, unsigned long long b) {
   asm("v_pk_mul_f32 %0, %1, %2" : "=v"(d) : "v"(a), "s"(b));
   return d;
 }
-__device__ __forceinline__ f32x2 pk_rsub(unsigned long long a, f32x2 b) {             // a - b, a: SGPR pair
+__device__ __forceinline__ f32x2 pk_rsub(unsigned long long a, f32x2 b) {   // a - b, a: SGPR pair; b may be a trans result
   f32x2 d;
-  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "s"(a), "v"(b));
+  asm("s_nop 0\n\tv_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "s"(a), "v"(b));
+  return d;
+}
+// fma whose first / second operand may be a transcendental result: one wait state first (see above)
+__device__ __forceinline__ f32x2 pk_fma_tr(f32x2 a, f32x2 b, f32x2 c) {
+  f32x2 d;
+  asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+__device__ __forceinline__ f32x2 pk_fma_tr(f32x2 a, unsigned long long b, f32x2 c) {
+  f32x2 d;
+  asm("s_nop 0\n\tv_pk_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "s"(b), "v"(c));
   return d;
 }
 
 // GELU on a pair, erf form: relu(x) - |x| * 0.5 erfc(|x| / sqrt 2) with erfc(z) = t q(t) exp(-z^2),
 // t = 1 / (1 + c z).  |x| t = (1 - t) / c' (c' = c / sqrt 2), so the correction is (1 - t) (q(t) / c')
-// exp(-x^2 / 2): the rcp / exp2 / relu per element, everything else packed — per pair 4 VALU + 7 (NQ = 3) or
-// 9 (NQ = 5) packed + 4 transcendental, against 2 x (9 or 11) VALU + 4 transcendental element-wise.
+// exp(-x^2 / 2): the rcp / exp2 / relu / x^2 per element, everything else packed — per pair 6 VALU + 6 (NQ = 3)
+// or 8 (NQ = 5) packed + 4 transcendental + 3 s_nop, against 2 x (9 or 11) VALU + 4 transcendental element-wise.
 //   NQ = 3: Abramowitz & Stegun 7.1.25 (|erf err| <= 2.5e-5: mixffn_rw's gelu_rw);
 //   NQ = 5: 7.1.26 (|err| <= 1.5e-7: stencil / dw_fc2's gelu_rl).
 // (1 - t) loses relative precision as |x| -> 0, where the correction itself -> 0.5 |x|: its absolute error
@@ -152,18 +167,20 @@ __device__ __forceinline__ f32x2 gelu_pk(f32x2 x) {
   t.y = __builtin_amdgcn_rcpf(u.y);
   f32x2 q;
   if constexpr (NQ == 3) {
-    q = pk_fma(t, kpair(s * a3), f32x2{s * a2, s * a2});
+    q = pk_fma_tr(t, kpair(s * a3), f32x2{s * a2, s * a2});
   } else {
-    q = pk_fma(t, kpair(s * a5), f32x2{s * a4, s * a4});
+    q = pk_fma_tr(t, kpair(s * a5), f32x2{s * a4, s * a4});
     q = pk_fma(q, t, kpair(s * a3));
     q = pk_fma(q, t, kpair(s * a2));
   }
   q = pk_fma(q, t, kpair(s * a1));
   const f32x2 a = pk_mul(pk_rsub(kpair(1.0f), t), q);
-  const f32x2 w = pk_mul(pk_mul(x, x), kpair(-0.72134752044448170f));     // -x^2 / 2 * log2(e)
+  // x itself is read only by compiler-generated instructions (x may be an MFMA result, whose read-after-write wait
+  // the hazard recognizer inserts for its own instructions only)
+  const f32x2 w = pk_mul(f32x2{x.x * x.x, x.y * x.y}, kpair(-0.72134752044448170f));     // -x^2 / 2 * log2(e)
   e.x = __builtin_amdgcn_exp2f(w.x);
   e.y = __builtin_amdgcn_exp2f(w.y);
-  return pk_fma(a, e, f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)});
+  return pk_fma_tr(a, e, f32x2{fmaxf(x.x, 0.f), fmaxf(x.y, 0.f)});
 }
 
 // Branch-free erf (Abramowitz & Stegun 7.1.26, |error| <= 1.5e-7 absolute): one rcp, one exp, five
