@@ -30,7 +30,7 @@ def main():
     res = {}
     # stage 1: whole MixFFN (C = 64, 56 x 56)
     C, W = 64, 56
-    xn, x = r(B, W, W, C).to(dt), r(B, W * W, C).to(dt)
+    xn, x = r(B, W, W, C).to(dt), r(B, W, W, C).to(dt)
     w1, b1 = r(4 * C, C, sc=C ** -0.5).to(dt), r(4 * C, sc=0.1)
     taps, db = r(9, 4 * C, sc=0.3), r(4 * C, sc=0.1)
     w2, b2 = r(C, 4 * C, sc=(4 * C) ** -0.5).to(dt), r(C, sc=0.1)
