@@ -746,8 +746,17 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16* __restrict__
                                                         const bf16* __restrict__ dO, long lddo, long sbdo,
                                                         bf16* __restrict__ dQ, long lddq, long sbdq,
                                                         bf16* __restrict__ Pws, bf16* __restrict__ dSws, int Nq,
-                                                        int Nk, int hd, float scale) {
+                                                        int Nk, int hd, float scale, float4* __restrict__ zacc,
+                                                        long nzacc) {
   constexpr int NKP = NKC * 64;
+  // zero the dK / dV f32 accumulators the two batched reductions after this kernel add into (round 6: replaces
+  // a hipMemsetAsync — one runtime fill launch per attention backward): workgroup slices of nzacc float4
+  {
+    const long nwg = (long)gridDim.x * gridDim.y * gridDim.z;
+    const long wg = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+    const long per = (nzacc + nwg - 1) / nwg, z0 = wg * per, z1 = z0 + per < nzacc ? z0 + per : nzacc;
+    for (long i = z0 + threadIdx.x; i < z1; i += 256) zacc[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
   constexpr int LDK = HDP + 8;
   constexpr int LDT = NKP + 8;
   __shared__ __attribute__((aligned(16))) bf16 sK[NKP][LDK];
@@ -1112,9 +1121,16 @@ extern "C" int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, c
   const int C = heads * hd;
   float* acc = static_cast<float*>(ws);                 // [2][B][Nk][C] f32: dK | dV accumulators
   const long nacc = (long)B * Nk * C;
-  if (hipMemsetAsync(acc, 0, 2 * nacc * sizeof(float), st) != hipSuccess) { set_error("svk_attention_bwd: memset"); return SVK_ELAUNCH; }
   const bool vec_ok = al16(Q, ldq, sbq) && al16(K, ldk, sbk) && al16(V, ldv, sbv) && al16(O, ldo, sbo) &&
                       al16(dO, lddo, sbdo) && al16(dQ, lddq, sbdq);
+  // the MFMA path's dQ kernel zeroes the accumulators itself (16-byte chunks: 2 nacc % 4 == 0 for C % 2 == 0 and
+  // a 16-byte aligned workspace); every other path starts from a memset
+  const bool zero_in_dq = attn_bwd_mfma_ok(dtype, Nk, hd) && vec_ok && !(getenv("SVK_ATTN_BWD_FUSED") &&
+                          getenv("SVK_ATTN_BWD_FUSED")[0] == '1' && Nk <= 64) && (2 * nacc) % 4 == 0 &&
+                          ((uintptr_t)acc & 15) == 0;
+  if (!zero_in_dq && hipMemsetAsync(acc, 0, 2 * nacc * sizeof(float), st) != hipSuccess) {
+    set_error("svk_attention_bwd: memset"); return SVK_ELAUNCH;
+  }
   // fused path (opt-in, SVK_ATTN_BWD_FUSED=1): measured 0.35 ms per train step SLOWER than the dQ kernel +
   // two batched reductions below (5 135 vs 5 240 frames/s, same box): its workgroups walk their query
   // chunks serially behind three barriers each, while the unfused dQ kernel's one-chunk workgroups overlap
@@ -1153,7 +1169,8 @@ extern "C" int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, c
       constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
       hipLaunchKernelGGL((attn_bwd_dq_mfma<HDP, NKC>), grid, dim3(256), 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K,
                          ldk, sbk, (const bf16*)V, ldv, sbv, (const bf16*)O, ldo, sbo, (const bf16*)dO, lddo, sbdo,
-                         (bf16*)dQ, lddq, sbdq, Pws, dSws, Nq, Nk, hd, scale);
+                         (bf16*)dQ, lddq, sbdq, Pws, dSws, Nq, Nk, hd, scale, reinterpret_cast<float4*>(acc),
+                         zero_in_dq ? 2 * nacc / 4 : 0L);
     };
     using H32 = std::integral_constant<int, 32>;
     using H64 = std::integral_constant<int, 64>;

@@ -384,10 +384,14 @@ __device__ __forceinline__ f32x4 gelu4(f32x4 x) {
 
 // GELU = false: the activation is the identity — the data gradient of a frozen MixFFN's DWConv + fc1
 // (svk/train.py: dX = (dwconv3x3ᵀ dU) W1, the transposed depthwise conv being the conv with flipped taps)
+// Training forward (round 6): U (optional) receives the pre-activation dwconv3x3(H) + dbias as 16-bit [M][K]
+// (the GELU backward's source, as dwconv3x3's pre_out writes it), and rscale (optional) scales each token's
+// fc2 output by rscale[token / rdiv] before the residual add (DropPath per frame, as gemm's row_scale).
 template <typename T, class C, bool GELU = true, bool PKG = false>
 __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restrict__ Hm, const char* __restrict__ pk,
                                                                const float* __restrict__ b2, const T* __restrict__ R,
-                                                               T* __restrict__ Y, int ntiles, int K) {
+                                                               T* __restrict__ Y, int ntiles, int K, T* __restrict__ U,
+                                                               const float* __restrict__ rscale, int rdiv) {
   typedef v8_t<T> tx8;
   constexpr int WI = C::WI, WNB = C::WNB, SW = C::SW, NW = C::NW, MPW = C::MPW, DPW = C::DPW;
   // dynamic LDS (C::LDS bytes, up to 107 KiB for 28 x 28), sized through hipFuncAttributeMaxDynamicSharedMemorySize
@@ -464,7 +468,19 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
         dacc[m] = mfma16x16x32(afr[kk], *reinterpret_cast<const tx8*>(hs + hoff[kk] + m * 2048), dacc[m]);
   };
   // GELU of the dwconv outputs -> G tile gb: lane (fr, fq) of m-block mb = channels 16 cb + 4 fq .. + 3, slot 16 mb + fr
-  auto gelu_store = [&](int gb) {
+  // (U: the pre-activation of K-step kt to HBM, 8-byte pieces, padding slots skipped)
+  auto gelu_store = [&](int gb, int kt) {
+    if (U) {
+#pragma unroll
+      for (int m = 0; m < MPW; ++m) {
+        const int t = (mb0 + m) * 16 + fr, y = y0 + t / SW, x = t % SW - 1;
+        if (y < WI && x >= 0 && x < WI) {
+          const T o[4] = {from_f<T>(dacc[m][0]), from_f<T>(dacc[m][1]), from_f<T>(dacc[m][2]), from_f<T>(dacc[m][3])};
+          *reinterpret_cast<uint2*>(U + (fbase + (long)y * WI + x) * K + kt * 64 + 16 * cb + 4 * fq) =
+              *reinterpret_cast<const uint2*>(o);
+        }
+      }
+    }
 #pragma unroll
     for (int m = 0; m < MPW; ++m) {
       const f32x4 gv = GELU ? (PKG ? gelu4_pk(dacc[m]) : gelu4(dacc[m])) : dacc[m];
@@ -516,7 +532,7 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   tie_a();
   __syncthreads();
   dwconv(0);
-  gelu_store(0);
+  gelu_store(0, 0);
   load_a(min(1, nk - 1));
   load_w2(0, 0);
   load_w2(0, 1);
@@ -534,7 +550,7 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
     load_w2(kt + 1, 0);
     fc2_half(kt & 1, 1);
     load_w2(kt + 1, 1);
-    gelu_store((kt + 1) & 1);
+    gelu_store((kt + 1) & 1, kt + 1);
     dma_h(min(kt + 3, nk - 1), kt % 3);
     // A(kt + 2) [6] and W2(kt + 1) [2 WNB] retired; the DMA [DPW] not
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DPW) : "memory");
@@ -552,11 +568,16 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
     const int t = mb * 16 + fr, y = y0 + t / SW, x = t % SW - 1;
     if (y >= WI || x < 0 || x >= WI) continue;
     const long m = fbase + (long)y * WI + x;
+    const float rs = rscale ? rscale[m / rdiv] : 1.f;
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb) {
       const int n = n0w + nb * 16 + fq * 4;
       const float4 bb = *reinterpret_cast<const float4*>(b2 + n);
       float v[4] = {acc[mb][nb][0] + bb.x, acc[mb][nb][1] + bb.y, acc[mb][nb][2] + bb.z, acc[mb][nb][3] + bb.w};
+      if (rscale) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] *= rs;
+      }
       if (R) {
         const uint2 r = *reinterpret_cast<const uint2*>(R + m * C::N + n);
         const f32x2 r01 = unpack2<T>(r.x), r23 = unpack2<T>(r.y);
@@ -570,7 +591,8 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
 
 
 template <typename T, class C, bool GELU = true>
-static int launch(const void* H, const void* pk, const float* b2, const void* R, void* Y, int B, int K, hipStream_t st) {
+static int launch(const void* H, const void* pk, const float* b2, const void* R, void* Y, int B, int K, hipStream_t st,
+                  void* U = nullptr, const float* rscale = nullptr, int rdiv = 1) {
   const long nt = (long)B * C::TILES_PER_FRAME;
   if (nt > 0x7fffffffL || (long)B * C::WI * C::WI * K > 0x7fffffffL) return SVK_EUNSUPPORTED;
   static bool attr = false;
@@ -583,10 +605,10 @@ static int launch(const void* H, const void* pk, const float* b2, const void* R,
   }
   if (GELU && gelu_pk_on())   // GELU on packed f32 pairs (svk_common.h gelu_pk; SVK_GELU_PK=0: element-wise)
     hipLaunchKernelGGL((dwfc2_rw<T, C, GELU, true>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H,
-                       (const char*)pk, b2, (const T*)R, (T*)Y, (int)nt, K);
+                       (const char*)pk, b2, (const T*)R, (T*)Y, (int)nt, K, (T*)U, rscale, rdiv);
   else
     hipLaunchKernelGGL((dwfc2_rw<T, C, GELU, false>), dim3((unsigned)nt), dim3(C::NT), C::LDS, st, (const T*)H,
-                       (const char*)pk, b2, (const T*)R, (T*)Y, (int)nt, K);
+                       (const char*)pk, b2, (const T*)R, (T*)Y, (int)nt, K, (T*)U, rscale, rdiv);
   static char name[64];
   if (!name[0])
     snprintf(name, sizeof(name), "dw_fc2_mx<%s, Cfg<%d, %d>%s>", type_name<T>(), C::N, C::WI, GELU ? "" : ", identity");
@@ -670,21 +692,40 @@ extern "C" int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* pa
   return svk_mixffn_dw_fc2_packed_act(dtype, H, packed, b2, R, Y, B, Himg, Wimg, K, N, SVK_ACT_GELU, stream);
 }
 
+extern "C" int svk_mixffn_dw_fc2_packed_ex(int dtype, const void* H, const void* packed, const float* b2,
+                                           const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, int act,
+                                           void* U, const float* rscale, int rdiv, void* stream);
+
 extern "C" int svk_mixffn_dw_fc2_packed_act(int dtype, const void* H, const void* packed, const float* b2,
                                             const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, int act,
                                             void* stream) {
+  return svk_mixffn_dw_fc2_packed_ex(dtype, H, packed, b2, R, Y, B, Himg, Wimg, K, N, act, nullptr, nullptr, 1, stream);
+}
+
+extern "C" int svk_mixffn_dw_fc2_packed_ex(int dtype, const void* H, const void* packed, const float* b2,
+                                           const void* R, void* Y, int B, int Himg, int Wimg, int K, int N, int act,
+                                           void* U, const float* rscale, int rdiv, void* stream) {
   if (act != SVK_ACT_GELU && act != SVK_ACT_NONE) { set_error("svk_mixffn_dw_fc2_packed: act must be GELU or NONE"); return SVK_EINVAL; }
   if (B < 0 || Himg <= 0 || Wimg <= 0 || !H || !packed || !b2 || !Y) { set_error("svk_mixffn_dw_fc2_packed: bad args"); return SVK_EINVAL; }
   if (Himg != Wimg || svk_mixffn_dw_fc2_packed_bytes(dtype, Wimg, N, K) == 0) {
     set_error("svk_mixffn_dw_fc2_packed: (dtype=%d, %dx%d, N=%d, K=%d) has no packed form", dtype, Himg, Wimg, N, K);
     return SVK_EUNSUPPORTED;
   }
-  if ((((uintptr_t)H) | ((uintptr_t)packed) | ((uintptr_t)b2)) & 15 || (((uintptr_t)Y) | ((uintptr_t)R)) & 7) {
+  if ((((uintptr_t)H) | ((uintptr_t)packed) | ((uintptr_t)b2)) & 15 || (((uintptr_t)Y) | ((uintptr_t)R) | ((uintptr_t)U)) & 7) {
     set_error("svk_mixffn_dw_fc2_packed: misaligned operand"); return SVK_EINVAL;
   }
+  if (rscale && rdiv <= 0) { set_error("svk_mixffn_dw_fc2_packed: rdiv must be positive"); return SVK_EINVAL; }
   if (B == 0) return SVK_OK;
   hipStream_t st = (hipStream_t)stream;
   SVK_DISPATCH_H16(dtype, T, {
+    if (U || rscale) {                 // the training forward (GELU; 14 x 14 / 7 x 7)
+      if (act != SVK_ACT_GELU || Wimg == 28) {
+        set_error("svk_mixffn_dw_fc2_packed_ex: pre-activation / row scale need act GELU at 14 x 14 or 7 x 7");
+        return SVK_EUNSUPPORTED;
+      }
+      if (Wimg == 7) return dwrw::launch<T, dwrw::Cfg<512, 7>>(H, packed, b2, R, Y, B, K, st, U, rscale, rdiv);
+      return dwrw::launch<T, dwrw::Cfg<320, 14>>(H, packed, b2, R, Y, B, K, st, U, rscale, rdiv);
+    }
     if (act == SVK_ACT_NONE) {
       if (Wimg == 7) return dwrw::launch<T, dwrw::Cfg<512, 7>, false>(H, packed, b2, R, Y, B, K, st);
       if (Wimg == 28) { set_error("svk_mixffn_dw_fc2_packed: no identity form for 28 x 28"); return SVK_EUNSUPPORTED; }

@@ -75,6 +75,7 @@ SIGNATURES = {
     "svk_gemm_ln": [c_int, P, c_int, c_int, P, P, P, P, P, c_float, P, P, c_int, P],
     "svk_mixffn_dw_fc2_packed": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, P],
     "svk_mixffn_dw_fc2_packed_act": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P],
+    "svk_mixffn_dw_fc2_packed_ex": [c_int, P, P, P, P, P, c_int, c_int, c_int, c_int, c_int, c_int, P, P, c_int, P],
     "svk_conv2d_s2d_ln": [c_int, P, c_int, c_int, c_int, c_int, P, P, P, P, c_float, P, c_int, P],
     "svk_cast": [c_int, P, c_int, P, c_long, P],
     # training step

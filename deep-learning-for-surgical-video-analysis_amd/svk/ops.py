@@ -466,7 +466,8 @@ def mixffn_dw_fc2_pack(taps, dbias, w2, W):
     return out
 
 
-def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu"):
+def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu", pre_out=None, row_scale=None,
+                  rows_per=1):
     """fc2(GELU(dwconv3x3(h) + dbias)) + b2 (+ residual) with the GELU map kept on chip (svk_mixffn_dw_fc2):
     h [B, H, W, K] fc1 output (16-bit NHWC), taps [9, K] / dbias [K] f32 as DWConv packs them, w2 [N, K];
     returns [B, H * W, N].  Where the map has the matrix-core form (14 x 14 with N = 320, 7 x 7 with N = 512,
@@ -474,6 +475,9 @@ def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu"
     from ``packed`` (mixffn_dw_fc2_pack) or packing on the fly; ``SVK_DWFC2_MX=0`` keeps the LDS-tap form.
     When ``packed`` is given, the kernel reads the taps, dbias and W2 baked into it (``taps`` / ``dbias`` / ``w2``
     are then only shape-checked); its size is checked against svk_mixffn_dw_fc2_packed_bytes(dtype, W, N, K).
+    Training forward (matrix-core form, GELU, 14 x 14 / 7 x 7): ``pre_out`` [B, H, W, K] receives the
+    pre-activation dwconv3x3(h) + dbias (the GELU backward's source, as dwconv3x3(pre_out=) writes it), and
+    ``row_scale`` [B * H * W / rows_per] f32 scales each token's fc2 output before the residual (DropPath).
     ``act="none"`` drops the GELU (matrix-core form only, 14 x 14 / 7 x 7): with flipped taps, zero dbias and
     w2 = W1ᵀ it is the data gradient through a frozen DWConv + fc1 (svk/train.py)."""
     if act not in ("gelu", "none"):
@@ -505,6 +509,23 @@ def mixffn_dw_fc2(h, taps, dbias, w2, b2, residual=None, packed=None, act="gelu"
                 or packed.numel() * packed.element_size() != want or packed.data_ptr() % 16):
             raise _lib.SvkError(f"svk.mixffn_dw_fc2: packed buffer is not the ({h.dtype}, W={W}, N={N}, K={K}) pack "
                                 f"({packed.numel() * packed.element_size()} bytes, expected {want})")
+    if pre_out is not None or row_scale is not None:
+        if act != "gelu" or packed is None:
+            raise _lib.SvkError("svk.mixffn_dw_fc2: pre_out / row_scale need the matrix-core GELU form")
+        if pre_out is not None and (pre_out.dtype != h.dtype or pre_out.shape != h.shape or not pre_out.is_contiguous()):
+            raise _lib.SvkError("svk.mixffn_dw_fc2: pre_out must be a contiguous map like h")
+        if row_scale is not None and (row_scale.dtype != torch.float32 or not row_scale.is_contiguous()
+                                      or row_scale.numel() * rows_per != B * H * W):
+            raise _lib.SvkError("svk.mixffn_dw_fc2: row_scale must be f32 [tokens / rows_per]")
+        t0 = _prof_begin()
+        _lib.call("svk_mixffn_dw_fc2_packed_ex", dtype_code(h.dtype), _p(h), _p(packed), _p(b2), _p(residual),
+                  _p(out), B, H, W, K, N, ACT["gelu"], _p(pre_out), _p(row_scale), int(rows_per), _stream())
+        if t0 is not None:
+            M = B * H * W
+            _prof_end(t0, _last_kernel(), 2.0 * M * N * K + 2.0 * 9 * M * K,
+                      (M * K * (2 if pre_out is not None else 1) + N * K + M * N * (2 if residual is not None else 1))
+                      * h.element_size(), (M, N, K, "dw_fc2"))
+        return out
     t0 = _prof_begin()
     if act == "none":
         _lib.call("svk_mixffn_dw_fc2_packed_act", dtype_code(h.dtype), _p(h), _p(packed), _p(b2), _p(residual),

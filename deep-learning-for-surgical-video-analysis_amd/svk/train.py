@@ -46,6 +46,9 @@ TRAIN_COL2IM = os.environ.get("SVK_TRAIN_COL2IM", "1") == "1"
 TRAIN_DWFC_BWD = os.environ.get("SVK_TRAIN_DWFC_BWD", "1") == "1"
 # the step's DropPath masks in one launch (svk_keep_mask_multi) instead of one keep_mask launch per mask
 TRAIN_MASK_MULTI = os.environ.get("SVK_TRAIN_MASK_MULTI", "1") == "1"
+# stages 3-4 training forward: DWConv + GELU + fc2 (+ DropPath scale + residual) as one matrix-core dw_fc2 launch
+# that also stores the GELU pre-activation (round 6), instead of dwconv3x3(pre_out) + GEMM
+TRAIN_DWFC_FWD = os.environ.get("SVK_TRAIN_DWFC_FWD", "1") == "1"
 TRAIN_FC1_DWCONV_C = tuple(int(c) for c in os.environ.get("SVK_TRAIN_FC1_DWCONV_C", "32,64,128").split(","))
 
 TRAINABLE = ("head", "prompt", "flow_encoder", "cross_attn_s3", "cross_attn_s4")
@@ -504,6 +507,14 @@ class EVPTrainStep:
                                       pre_out=u)
         else:
             h = ops.gemm(xn2, b["w1"], b["bf1"])
+            pk = self._dwfc_fwd_pack(b, H, W, C) if TRAIN_DWFC_FWD and self.dt in ops.H16 else None
+            if pk is not None:
+                # stages 3-4 (round 6): DWConv + GELU + fc2 (+ DropPath scale, residual) in one matrix-core kernel
+                # that also stores the pre-activation u for the GELU backward — the GELU map never reaches HBM
+                out = ops.mixffn_dw_fc2(h.view(B, H, W, hid), b["taps"], b["dwb"], b["w2"], b["bf2"], residual=x1,
+                                        packed=pk, pre_out=u, row_scale=mm, rows_per=N)
+                sv.update(q=q, kv=kv, o=o, x1=x1, u=u, out=out)
+                return sv
             g = ops.dwconv3x3(h.view(B, H, W, hid), b["taps"], b["dwb"], act="gelu", pre_out=u)
         out = ops.gemm(g.view(B, N, hid), b["w2"], b["bf2"], residual=x1, row_scale=mm, rows_per=N)
         sv.update(q=q, kv=kv, o=o, x1=x1, u=u, out=out)
@@ -653,6 +664,18 @@ class EVPTrainStep:
                 dh = dg(dzm, self.W(nm + ".proj.weight." + ("C" if dg is ops.conv2d_dgrad_col2im else "D")),
                         pin.shape[1], pin.shape[2], pin.shape[3], h["k"], h["st"], h["k"] // 2,
                         residual=dhc[s - 1].view(pin.shape).contiguous())
+
+    def _dwfc_fwd_pack(self, b, H, W, C):
+        """The packed operands of the fused training-forward DWConv + GELU + fc2 (forward taps, the DWConv bias,
+        W2) for this block's map, or None where the matrix-core dw_fc2 has no training form (14 x 14 / 7 x 7 only;
+        cached in the block's parameter dict)."""
+        key = ("dwfc_fwd", H, W)
+        if key not in b:
+            pk = None
+            if H == W and W in (7, 14) and ops.mixffn_dw_fc2_supported(self.dt, W, C, b["w2"].shape[1]):
+                pk = ops.mixffn_dw_fc2_pack(b["taps"], b["dwb"], b["w2"], W)
+            b[key] = pk
+        return b[key]
 
     def _dwfc_bwd_pack(self, b, H, W, C):
         """The packed operands of the fused DWConv + fc1 data gradient for this block's map, or None where

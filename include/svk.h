@@ -161,6 +161,14 @@ int svk_mixffn_dw_fc2_packed(int dtype, const void* H, const void* packed, const
  * Y = (dwconv3x3(H) + dbias) W2^T + b2 (+ R) — with flipped taps, zero dbias and W2 = W1^T the data gradient of
  * a frozen MixFFN's DWConv + fc1 (train_evp.py's backward through mix_transformer_evp.py:60-62, svk/train.py).
  * 14 x 14 / N = 320 and 7 x 7 / N = 512 only for SVK_ACT_NONE. */
+/* The training forward (round 6; act = SVK_ACT_GELU, 14 x 14 / 7 x 7): as svk_mixffn_dw_fc2_packed, plus U
+ * (optional, [B][Himg][Wimg][K] 16-bit, 8-byte aligned) receives the pre-activation dwconv3x3(H) + dbias — the
+ * GELU backward's source — and rscale (optional, f32) scales each token's fc2 output by rscale[token / rdiv]
+ * before R is added (DropPath per frame: mix_transformer_evp.py:167-171 in train mode).  Replaces
+ * svk_dwconv3x3 (pre-activation store) + svk_gemm (row scale, residual) in svk/train.py's block forward. */
+int svk_mixffn_dw_fc2_packed_ex(int dtype, const void* H, const void* packed, const float* b2, const void* R,
+                                void* Y, int B, int Himg, int Wimg, int K, int N, int act, void* U,
+                                const float* rscale, int rdiv, void* stream);
 int svk_mixffn_dw_fc2_packed_act(int dtype, const void* H, const void* packed, const float* b2, const void* R,
                                  void* Y, int B, int Himg, int Wimg, int K, int N, int act, void* stream);
 

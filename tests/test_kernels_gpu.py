@@ -285,6 +285,42 @@ def test_mixffn_dw_fc2_identity(cuda, dt, B, W, K, N):
 
 
 @pytest.mark.parametrize("dt", H16)
+@pytest.mark.parametrize("B,W,K,N", [(88, 14, 1280, 320), (5, 7, 2048, 512), (3, 14, 640, 320)])
+def test_mixffn_dw_fc2_train_forward(cuda, dt, B, W, K, N):
+    """The training-forward form (svk_mixffn_dw_fc2_packed_ex, round 6): Y = rscale[frame] * (GELU(dwconv3x3(h) +
+    dbias) W2^T + b2) + R with the pre-activation U stored, against the path it replaces in svk/train.py
+    (dwconv3x3(pre_out=) + gemm(row_scale, residual): U within a 16-bit ulp — the mx form rounds its taps to the
+    16-bit type — and Y within a few ulps) and fp64 (taps rounded as the mx form rounds them)."""
+    from svk import ops
+    h = _rand(B, W, W, K, dt=dt, dev=cuda, seed=171)
+    taps = _rand(9, K, dt=torch.float32, dev=cuda, scale=0.3, seed=172)
+    db = _rand(K, dt=torch.float32, dev=cuda, scale=0.1, seed=173)
+    w2 = _rand(N, K, dt=dt, dev=cuda, scale=K ** -0.5, seed=174)
+    b2 = _rand(N, dt=torch.float32, dev=cuda, seed=175)
+    r = _rand(B, W * W, N, dt=dt, dev=cuda, seed=176)
+    keep = torch.tensor([(0.0 if i % 3 == 1 else 1.25) for i in range(B)], device=cuda)   # DropPath scales
+    pk = ops.mixffn_dw_fc2_pack(taps, db, w2, W)
+    u = torch.empty_like(h)
+    got = ops.mixffn_dw_fc2(h, taps, db, w2, b2, residual=r, packed=pk, pre_out=u, row_scale=keep, rows_per=W * W)
+    assert ops._last_kernel().startswith("dw_fc2_mx"), ops._last_kernel()
+    u16 = torch.empty_like(h)
+    g = ops.dwconv3x3(h, taps, db, act="gelu", pre_out=u16)
+    ref16 = ops.gemm(g.view(B, W * W, K), w2, b2, residual=r, row_scale=keep, rows_per=W * W)
+    ulp = 2 ** -8 if dt == torch.bfloat16 else 2 ** -11
+    du = (u.float() - u16.float()).abs().max().item()
+    assert du <= 2 * ulp * float(u16.float().abs().max()), du
+    d = (got.float() - ref16.float()).abs().max().item()
+    assert d <= 4 * ulp * float(ref16.float().abs().max()), d
+    tq = taps.to(dt).double().cpu()                                     # the mx form's 16-bit taps
+    hd = h.double().cpu().permute(0, 3, 1, 2)
+    cv = F.conv2d(hd, tq.t().reshape(K, 1, 3, 3), db.double().cpu(), padding=1, groups=K)
+    _close(u, cv.permute(0, 2, 3, 1), dt)
+    gd = F.gelu(cv).permute(0, 2, 3, 1).reshape(B, W * W, K)
+    ref = (gd @ w2.double().cpu().t() + b2.double().cpu()) * keep.double().cpu().view(B, 1, 1) + r.double().cpu()
+    _close(got, ref, dt)
+
+
+@pytest.mark.parametrize("dt", H16)
 @pytest.mark.parametrize("M,N,K,res,bias", [(50176, 320, 320, True, True), (12544, 512, 512, True, True),
                                             (1000, 320, 80, True, True), (77, 512, 128, True, False),
                                             (130, 320, 40, False, True)])
