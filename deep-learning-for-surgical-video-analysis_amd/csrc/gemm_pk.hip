@@ -432,7 +432,16 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
         const int row = idx / CPR, c = idx % CPR;
         const uint4 v = *reinterpret_cast<const uint4*>(stile + row * (BN * 2) + ((c ^ (row & (CPR - 1))) << 4));
         const int m = m0 + row, n = n0 + c * 8;
-        if (m < p.M && n < p.N && !(diag & 2)) *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
+        if (m < p.M && n < p.N && !(diag & 2)) {
+          uint4* dst = reinterpret_cast<uint4*>(C + (long)m * p.ldc + n);
+          if (p.nt_c) {   // (uniform branch) streaming store: the tile bypasses L2 residency
+            typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
+            const u32x4n vv = u32x4n{v.x, v.y, v.z, v.w};
+            asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(vv) : "memory");
+          } else {
+            *dst = v;
+          }
+        }
       }
       barrier_mem();   // the next step's DMA overwrites this stage buffer
     }
@@ -616,6 +625,8 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   if (!al(a.C, 8) || (a.R && !al(a.R, 8))) return no("C/R align");
   if (a.bias && !al(a.bias, 16)) return no("bias align");
   int cfg = force;
+  static const int nt_c = getenv("SVK_PK_NT") ? atoi(getenv("SVK_PK_NT")) : 0;
+  const_cast<GemmArgs&>(a).nt_c = nt_c;
   // Measured on the MiT-b2 B = 256 shapes, all variants interleaved in one process
   // (tools/tune_bench.py, profiles/r01/tune_r01.txt):
   //  * dense, long K (>= 512) with N % 128 == 0, or few rows (M < 32k, e.g. the stage-4 / head GEMMs
