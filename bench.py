@@ -23,8 +23,10 @@ profiles/ time the graph-replayed launches themselves.  cpu_baseline: the oracle
 reference's op graph restated on torch CPU ops, fp32) on a bounded sample, rank 0 at N=1 only.
 """
 import argparse
+import ast
 import json
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -51,6 +53,10 @@ EXTRACT_GFLOP = {"mit_b2_evp": EXTRACT_GFLOP_PER_FRAME, "mit_b3_evp": 16.66 - 1.
 # the count profiles/r03/bench_train.jsonl prices the train step against
 TRAIN_GFLOP_PER_FRAME = 25.94
 HBM_PEAK_GBS = 8000.0                              # MI355X HBM3E
+# on-chip operand-fetch ceiling of an LDS-DMA tile loader: rows served from the XCD's L2 into LDS at 66-73 GB/s
+# per CU = 16.8-18.8 TB/s chip-wide (MI355X_MICROARCH.md, 'Indexed rows: gather into LDS'); from the Infinity
+# Cache 8.6 TB/s.  The persistent GEMMs stream their A / W tiles through exactly that path.
+L2_LDS_PEAK_GBS = 18800.0
 DATA = "synthetic (seeded Cholec80-shaped frames/segmaps/flow, resident in HBM; random-init weights)"
 
 
@@ -843,6 +849,35 @@ def timed(step, steps, world):
     return out, float(dt.item())
 
 
+def operand_fetch(name, shapes, prof_steps, ms):
+    """The dominant persistent GEMM's on-chip operand traffic: every (BM x BN) tile DMAs its A rows and W rows
+    over the whole (64-padded) K into LDS, i.e. tiles x (BM + BN) x K x 2 bytes per launch — L2 / Infinity Cache
+    -> LDS, far above the algorithmic HBM bytes — priced against the measured L2-served LDS-DMA ceiling."""
+    m = re.match(r"gemm_pk<[^,]+, PkCfg<(\d+), (\d+)", name)
+    if not m:
+        return None
+    bm, bn = int(m.group(1)), int(m.group(2))
+    nbytes, n = 0.0, 0
+    for (kname, shape), (_, _, _, cnt) in shapes.items():
+        if kname != name:
+            continue
+        try:
+            sh = ast.literal_eval(shape)
+            M, N, K = int(sh[0]), int(sh[1]), int(sh[2])
+        except (ValueError, SyntaxError, TypeError, IndexError):
+            return None
+        tiles = -(-M // bm) * -(-N // bn)
+        nbytes += cnt * tiles * (bm + bn) * (-(-K // 64) * 64) * 2
+        n += cnt
+    if not n:
+        return None
+    gbs = nbytes / (ms * 1e-3) / 1e9
+    return {"bytes_per_launch": round(nbytes / n), "achieved_gbs": round(gbs, 1), "ceiling_gbs": L2_LDS_PEAK_GBS,
+            "frac": round(gbs / L2_LDS_PEAK_GBS, 4),
+            "note": "tiles x (BM + BN) x K x 2 B per launch over the same HIP-event launch time as roofline.achieved; "
+                    "ceiling = L2-served LDS-DMA 73 GB/s per CU (MI355X_MICROARCH.md)"}
+
+
 def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value, world, dump_gemm=None,
                 variant="mit_b2_evp", prof_elapsed=None):
     """Dominant kernel (the GEMM / conv instantiation with the most HIP-event device time over the profiled
@@ -893,6 +928,9 @@ def roofline_of(records, prof_steps, elapsed, steps, workload, dtype_name, value
     elif workload == "train":
         roofline["step_mfma_util"] = round(value / world * TRAIN_GFLOP_PER_FRAME * 1e9 / (peak * 1e12), 4)
         roofline["step_gflop_per_frame"] = TRAIN_GFLOP_PER_FRAME
+    fetch = operand_fetch(name, shapes, prof_steps, ms)
+    if fetch is not None:
+        roofline["operand_fetch"] = fetch
     busy = pmc_mfma_busy(workload, dtype_name, variant)
     if busy is not None:
         roofline["mfma_busy_counters"] = busy

@@ -47,8 +47,10 @@ TRAIN_DWFC_BWD = os.environ.get("SVK_TRAIN_DWFC_BWD", "1") == "1"
 # the step's DropPath masks in one launch (svk_keep_mask_multi) instead of one keep_mask launch per mask
 TRAIN_MASK_MULTI = os.environ.get("SVK_TRAIN_MASK_MULTI", "1") == "1"
 # stages 3-4 training forward: DWConv + GELU + fc2 (+ DropPath scale + residual) as one matrix-core dw_fc2 launch
-# that also stores the GELU pre-activation (round 6), instead of dwconv3x3(pre_out) + GEMM
-TRAIN_DWFC_FWD = os.environ.get("SVK_TRAIN_DWFC_FWD", "1") == "1"
+# that also stores the GELU pre-activation (round 6), instead of dwconv3x3(pre_out) + GEMM.  Parity-tested but OFF:
+# at B = 88 its one-tile-per-workgroup grid (352 workgroups for 512 slots) ran the step 0.3 % slower
+# (profiles/r06/train_dwfc_fwd_ab.txt: 6 157 / 6 166 vs 6 181 / 6 178 frames/s, interleaved, same box)
+TRAIN_DWFC_FWD = os.environ.get("SVK_TRAIN_DWFC_FWD", "0") == "1"
 TRAIN_FC1_DWCONV_C = tuple(int(c) for c in os.environ.get("SVK_TRAIN_FC1_DWCONV_C", "32,64,128").split(","))
 
 TRAINABLE = ("head", "prompt", "flow_encoder", "cross_attn_s3", "cross_attn_s4")
