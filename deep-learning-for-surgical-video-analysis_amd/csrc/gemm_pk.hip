@@ -167,7 +167,8 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   int crb[Cfg::A_LD], ciy[Cfg::A_LD], cix[Cfg::A_LD];
   // dense, no K tail: per-lane byte offsets of this thread's A / W chunks within the current issue tile
   // (32-bit: the host routes operands of 4 GiB or more to the KTAIL instantiation)
-  constexpr bool SOFF = ASRC == 0 && !KTAIL && !SPLIT && Cfg::BM * Cfg::BN <= 128 * 128;   // (bigger tiles: no registers left)
+  constexpr bool SOFF = ASRC == 0 && !KTAIL && !SPLIT &&
+                        (Cfg::BM * Cfg::BN <= 128 * 128 || (Cfg::BM == 192 && Cfg::BN == 128));   // (128 x 160: spills)
   uint32_t offA[SOFF ? Cfg::A_LD : 1], offB[SOFF ? Cfg::B_LD : 1];
   // live == false: past the workgroup's last (tile, K-step) — the same instructions run (branch-free
   // around the DMA issue) with every source replaced by the zero block
@@ -703,6 +704,9 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 85: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 5>, 0>(a, st, true);
     case 86: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 4>, 0>(a, st, true);
     case 87: return launch_pk_k<T, PkCfg<128, 256, 2, 4, 3>, 0>(a, st, false);
+    // 192 x 128, 4 waves of 96 x 64, two workgroups per CU (80 KiB each): 17 % fewer operand bytes per FLOP
+    // than 128 x 128 through the L2 -> LDS path that bounds it (r06 ablations), 1.5x the MFMAs per barrier
+    case 88: return launch_pk_k<T, PkCfg<192, 128, 2, 2, 2>, 0>(a, st, false);
     // (256 x 256 with 4 waves: 512 registers and ~15 VGPR spills, which the counted DMA waits cannot tolerate;
     // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128, and 256 x 256 with 8 waves of
     // 128 x 64 (225 VGPRs, one workgroup per CU) 1.2-2x slower: per-tile prologue / epilogue / store drain

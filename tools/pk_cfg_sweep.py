@@ -22,7 +22,7 @@ SHAPES = [  # (M, N, K, residual, what)
 ]
 CFGS = [(-1, "auto"), (10, "128x64"), (20, "64x128"), (30, "64x64"), (40, "128x160"), (60, "128x128e"), (70, "ppRF"),
         (71, "ppPair"), (80, "128x128w8"), (82, "128x256w8"), (84, "128x128w8s3"), (85, "w8s5"), (86, "w8s4"),
-        (87, "128x256s3"), (90, "wt256"), (91, "wt160"),
+        (87, "128x256s3"), (88, "192x128"), (90, "wt256"), (91, "wt160"),
         (92, "wt128"), (93, "wt192"), (100, "torch")]
 
 
