@@ -24,8 +24,6 @@ struct GemmArgs {
   // out_mode 1: C (and R) are an NHWC map [B, uH, uW, uC] and GEMM row m = (b, py, px) of the
   // (uH/us) x (uW/us) patch grid, column n = (i, j, ci): the adjoint of a k = s patchify conv.
   int out_mode, uH, uW, us, uC;
-  // gemm_pk: output stores with the non-temporal hint (set by gemm_pk_try from SVK_PK_NT; round-6 experiment)
-  int nt_c;
   // split-K (gemm_pk_conv_splitk): raw f32 partial sums of ksplit K parts -> slab [ksplit][M][N]
   int ksplit; float* slab;
 };

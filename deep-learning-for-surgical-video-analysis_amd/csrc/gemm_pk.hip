@@ -167,8 +167,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   int crb[Cfg::A_LD], ciy[Cfg::A_LD], cix[Cfg::A_LD];
   // dense, no K tail: per-lane byte offsets of this thread's A / W chunks within the current issue tile
   // (32-bit: the host routes operands of 4 GiB or more to the KTAIL instantiation)
-  constexpr bool SOFF = ASRC == 0 && !KTAIL && !SPLIT &&
-                        (Cfg::BM * Cfg::BN <= 128 * 128 || (Cfg::BM == 192 && Cfg::BN == 128));   // (128 x 160: spills)
+  constexpr bool SOFF = ASRC == 0 && !KTAIL && !SPLIT && Cfg::BM * Cfg::BN <= 128 * 128;   // (bigger tiles: no registers left)
   uint32_t offA[SOFF ? Cfg::A_LD : 1], offB[SOFF ? Cfg::B_LD : 1];
   // live == false: past the workgroup's last (tile, K-step) — the same instructions run (branch-free
   // around the DMA issue) with every source replaced by the zero block
@@ -434,14 +433,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
         const uint4 v = *reinterpret_cast<const uint4*>(stile + row * (BN * 2) + ((c ^ (row & (CPR - 1))) << 4));
         const int m = m0 + row, n = n0 + c * 8;
         if (m < p.M && n < p.N && !(diag & 2)) {
-          uint4* dst = reinterpret_cast<uint4*>(C + (long)m * p.ldc + n);
-          if (p.nt_c) {   // (uniform branch) streaming store: the tile bypasses L2 residency
-            typedef uint32_t u32x4n __attribute__((ext_vector_type(4)));
-            const u32x4n vv = u32x4n{v.x, v.y, v.z, v.w};
-            asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(vv) : "memory");
-          } else {
-            *dst = v;
-          }
+          *reinterpret_cast<uint4*>(C + (long)m * p.ldc + n) = v;
         }
       }
       barrier_mem();   // the next step's DMA overwrites this stage buffer
@@ -626,8 +618,6 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   if (!al(a.C, 8) || (a.R && !al(a.R, 8))) return no("C/R align");
   if (a.bias && !al(a.bias, 16)) return no("bias align");
   int cfg = force;
-  static const int nt_c = getenv("SVK_PK_NT") ? atoi(getenv("SVK_PK_NT")) : 0;
-  const_cast<GemmArgs&>(a).nt_c = nt_c;
   // Measured on the MiT-b2 B = 256 shapes, all variants interleaved in one process
   // (tools/tune_bench.py, profiles/r01/tune_r01.txt):
   //  * dense, long K (>= 512) with N % 128 == 0, or few rows (M < 32k, e.g. the stage-4 / head GEMMs
@@ -693,20 +683,9 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
     case 40: return launch_pk_k<T, PkCfg<128, 160, 2, 2, 2>, 0>(a, st, false);
     case 50: return launch_pk_k<T, PkCfg<256, 128, 4, 2, 2>, 0>(a, st, false);
     case 60: return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, 0>(a, st, true);   // 128 x 128, staged epilogue
-    // round 6 sweep candidates: 8-wave 128 x 128 (64 x 32 / 32 x 64 per wave: 4 waves per SIMD at 2 workgroups per
-    // CU), 8-wave 128 x 256 (64 x 64 per wave, one workgroup per CU), 8-wave 128 x 128 with a 3-stage ring
-    case 80: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 2>, 0>(a, st, true);
-    // (32 x 64 per wave, PkCfg<128, 128, 4, 2, 2>: the f16 ELDS instantiation spills 3 VGPRs at the 128-register budget)
-    case 82: return launch_pk_k<T, PkCfg<128, 256, 2, 4, 2>, 0>(a, st, false);
-    case 84: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 3>, 0>(a, st, true);
-    // deep rings, one 8-wave workgroup per CU: 3 / 4 K-steps (96 / 128 KiB) of LDS-DMA in flight per CU instead of
-    // the two workgroups' 2 x 1 (64 KiB) — the r06 ablations put the load pipeline, not the MFMAs, on the critical path
-    case 85: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 5>, 0>(a, st, true);
-    case 86: return launch_pk_k<T, PkCfg<128, 128, 2, 4, 4>, 0>(a, st, true);
-    case 87: return launch_pk_k<T, PkCfg<128, 256, 2, 4, 3>, 0>(a, st, false);
-    // 192 x 128, 4 waves of 96 x 64, two workgroups per CU (80 KiB each): 17 % fewer operand bytes per FLOP
-    // than 128 x 128 through the L2 -> LDS path that bounds it (r06 ablations), 1.5x the MFMAs per barrier
-    case 88: return launch_pk_k<T, PkCfg<192, 128, 2, 2, 2>, 0>(a, st, false);
+    // (round 6, measured and not instantiated — profiles/r06/pk_cfg_sweep_*.txt, DESIGN §5: 8-wave 128 x 128 at
+    // 2 / 1 workgroups per CU with 2-5-stage rings, 8-wave 128 x 256 with 2 / 3 stages, 4-wave 192 x 128: none beats
+    // this 128 x 128 staged-epilogue tile on the MiT-b2 shapes; the deep rings lost 15-25 %, 192 x 128 up to 70 %)
     // (256 x 256 with 4 waves: 512 registers and ~15 VGPR spills, which the counted DMA waits cannot tolerate;
     // 256 x 128 / 128 x 256 at one wave per SIMD run 2-4x slower than 128 x 128, and 256 x 256 with 8 waves of
     // 128 x 64 (225 VGPRs, one workgroup per CU) 1.2-2x slower: per-tile prologue / epilogue / store drain
