@@ -597,6 +597,7 @@ static const int g_pk_policy = getenv("SVK_PK_POLICY") ? atoi(getenv("SVK_PK_POL
 // ran 8.60 ms with it vs 8.42 ms without (same box, profiles/r04/bench_pp_ab.txt): one 128 KiB-LDS workgroup per
 // CU for the whole persistent launch leaves no room for the side stream's kernels to co-run
 static const int g_pp_policy = getenv("SVK_PP") ? atoi(getenv("SVK_PP")) : 0;
+static const int g_pk_ext_policy = getenv("SVK_PK_EXT_POLICY") ? atoi(getenv("SVK_PK_EXT_POLICY")) : 1;  // A/B switch
 template <typename T>
 int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
   const int force = g_tune[TUNE_PK_CFG];
@@ -651,6 +652,15 @@ int gemm_pk_try(const GemmArgs& a, hipStream_t st, int asrc) {
       }
       // (round-2 sweep: 128 x 128 for the stage-3 fc1 and 128 x 160 for its fc2 win 5-7 us each in
       // isolation but lost 2 % of the whole graph-replayed step: kept 128 x 64)
+      // round 6, extended epilogue (train backward: DropPath row scale / activation backward from a saved
+      // pre-activation; profiles/r06/ext_sweep.txt, bf16 B = 88): the extra U operand makes the register
+      // epilogue of 128 x 128 the slowest tile everywhere; 64 x 64 wins where 128 x 128 would leave < 1024 tiles
+      // (4312 x 512 x 2048: 30.8 -> 22.5 us, 68992 x 128 x 512: 34.1 -> 30.3), 128 x 64 elsewhere
+      // (17248 x 1280 x 320: 49.7 -> 47.2)
+      if (g_pk_policy && g_pk_ext_policy && (a.U || a.rscale)) {
+        const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128);
+        cfg = (a.N % 128 == 0 && t128 < 1024) ? 30 : 10;
+      }
     }
   }
   const bool reg_epi = cfg == 0 && (big || a.M < 32768);
