@@ -896,6 +896,162 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_mfma(const bf16* __restrict__
   }
 }
 
+// ---- MFMA attention backward with transposed scores (round 6): same outputs as attn_bwd_dq_mfma ----------------
+// The scores are computed transposed, S^T = K Q^T and dP^T = V dO^T (A = K / V rows, B = the wave's Q / dO rows
+// held in registers; K and V are staged once per workgroup in LDS, row-major), so a lane's accumulator column is ONE
+// query (lane & 15) and its rows are the keys 16 t + 4 g + r (g = lane >> 4).  Then
+//   * the softmax and D = rowsum(dO * O) reduce in registers plus two shuffles (no LDS, no 64-lane serial loop);
+//   * P^T / dS'^T leave as 8-byte pieces (4 consecutive keys of one query) instead of 2-byte stores;
+//   * dQ^T = K^T dS'^T takes dS'^T from registers as the B operand, keys permuted {32 s + 4 g + j} ++
+//     {32 s + 16 + 4 g + j} as in the forward's P.V, A = K^T gathered from sK: no dS' LDS round trip, no K^T copy.
+// LDS is K and V only: 18 KB at NKC = 1, 74 KB at NKC = 4 (the 196-token cross-attention), where the previous kernel
+// needed 141 KB and ran one workgroup per CU.  (A first version read the K / V A operands straight from global
+// memory, every wave the whole K and V: 0.74 GB of L2 requests at NKC = 4, 41 % missing — slower at <= 64 keys.)
+template <int HDP, int NKC>
+__global__ __launch_bounds__(256) void attn_bwd_dq_t(const bf16* __restrict__ Q, long ldq, long sbq,
+                                                     const bf16* __restrict__ K, long ldk, long sbk,
+                                                     const bf16* __restrict__ V, long ldv, long sbv,
+                                                     const bf16* __restrict__ O, long ldo, long sbo,
+                                                     const bf16* __restrict__ dO, long lddo, long sbdo,
+                                                     bf16* __restrict__ dQ, long lddq, long sbdq,
+                                                     bf16* __restrict__ Pws, bf16* __restrict__ dSws, int Nq,
+                                                     int Nk, int hd, float scale, float4* __restrict__ zacc,
+                                                     long nzacc) {
+  constexpr int NKP = NKC * 64, NKS = HDP / 32, NDT = HDP / 16, NT = NKC * 4;
+  {   // zero this workgroup's slice of the dK / dV accumulators (as attn_bwd_dq_mfma)
+    const long nwg = (long)gridDim.x * gridDim.y * gridDim.z;
+    const long wg = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+    const long per = (nzacc + nwg - 1) / nwg, z0 = wg * per, z1 = z0 + per < nzacc ? z0 + per : nzacc;
+    for (long i = z0 + threadIdx.x; i < z1; i += 256) zacc[i] = float4{0.f, 0.f, 0.f, 0.f};
+  }
+  constexpr int LDK = HDP + 8;
+  __shared__ __attribute__((aligned(16))) bf16 sK[NKP][LDK];
+  __shared__ __attribute__((aligned(16))) bf16 sV[NKP][LDK];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int q0 = blockIdx.x * 64, h = blockIdx.y, b = blockIdx.z, heads = gridDim.y;
+  const long co = (long)h * hd;
+  const bf16* Kb = K + b * sbk + co;
+  const bf16* Vb = V + b * sbv + co;
+  const bf16 zero = (bf16)0.f;
+  // K, V [key][d] (zeros past Nk / hd), 16-byte pieces
+  for (int idx = tid; idx < NKP * (HDP / 8); idx += 256) {
+    const int key = idx / (HDP / 8), c8 = (idx % (HDP / 8)) * 8;
+    bf16x8 kv, vv;
+    if (key < Nk && c8 < hd) {
+      kv = *reinterpret_cast<const bf16x8*>(Kb + (long)key * ldk + c8);
+      vv = *reinterpret_cast<const bf16x8*>(Vb + (long)key * ldv + c8);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { kv[e] = zero; vv[e] = zero; }
+    }
+    *reinterpret_cast<bf16x8*>(&sK[key][c8]) = kv;
+    *reinterpret_cast<bf16x8*>(&sV[key][c8]) = vv;
+  }
+  // B operands: this lane's query row of Q and dO (k = d = 32 ks + 8 g + j); D = rowsum(dO * O) from the same pieces
+  const int qn = q0 + 16 * w + c;
+  const bool qok = qn < Nq;
+  bf16x8 bq[NKS], bg[NKS];
+  float D = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int d0 = 32 * ks + 8 * g;
+    if (qok && d0 < hd) {
+      bq[ks] = *reinterpret_cast<const bf16x8*>(Q + b * sbq + (long)qn * ldq + co + d0);
+      bg[ks] = *reinterpret_cast<const bf16x8*>(dO + b * sbdo + (long)qn * lddo + co + d0);
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(O + b * sbo + (long)qn * ldo + co + d0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) D += (float)ov[e] * (float)bg[ks][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { bq[ks][e] = zero; bg[ks][e] = zero; }
+    }
+  }
+  D += __shfl_xor(D, 16, 64);
+  D += __shfl_xor(D, 32, 64);
+  __syncthreads();   // K, V staged
+  // S^T, dP^T: A = K / V rows from LDS (key 16 t + c, k = d = 32 ks + 8 g + j)
+  f32x4 S[NT], dP[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    S[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dP[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const bf16x8 ka = *reinterpret_cast<const bf16x8*>(&sK[16 * t + c][32 * ks + 8 * g]);
+      const bf16x8 va = *reinterpret_cast<const bf16x8*>(&sV[16 * t + c][32 * ks + 8 * g]);
+      S[t] = mfma16x16x32(ka, bq[ks], S[t]);
+      dP[t] = mfma16x16x32(va, bg[ks], dP[t]);
+    }
+  }
+  // softmax over keys for this lane's query: in-register over (t, r), then across the 4 lane groups
+  const float sl2 = scale * 1.4426950408889634f;
+  float m = -INFINITY;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (16 * t + 4 * g + r < Nk) m = fmaxf(m, S[t][r]);
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = 16 * t + 4 * g + r < Nk ? exp2f((S[t][r] - m) * sl2) : 0.f;
+      S[t][r] = p;
+      l += p;
+    }
+  l += __shfl_xor(l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  const float inv = 1.f / l;
+  // P^T, dS'^T -> workspace rows [z][query][NKP] (8-byte pieces; padded keys get p = dS' = 0); dS' kept as bf16
+  bf16x4 ds4[NT];
+  bf16* Prow = Pws + (((long)b * heads + h) * Nq + qn) * NKP;
+  bf16* dSrow = dSws + (((long)b * heads + h) * Nq + qn) * NKP;
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    bf16x4 p4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = S[t][r] * inv;
+      p4[r] = (bf16)p;
+      ds4[t][r] = (bf16)(scale * p * (dP[t][r] - D));
+    }
+    if (qok) {
+      *reinterpret_cast<bf16x4*>(Prow + 16 * t + 4 * g) = p4;
+      *reinterpret_cast<bf16x4*>(dSrow + 16 * t + 4 * g) = ds4[t];
+    }
+  }
+  // dQ^T = K^T dS'^T: k-step s covers keys {32 s + 4 g + j} ++ {32 s + 16 + 4 g + j} (tiles 2 s, 2 s + 1); the A
+  // operand (row d = 16 dt + c) gathers K^T from the row-major sK with 2-byte reads (16 lanes read 16 consecutive d
+  // of one key row; the 4 lane groups' rows sit 16 banks apart: conflict-free)
+#pragma unroll
+  for (int dt = 0; dt < NDT; ++dt) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NT / 2; ++s) {
+      bf16x8 a, bb;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        a[j] = sK[32 * s + 4 * g + j][16 * dt + c];
+        a[4 + j] = sK[32 * s + 16 + 4 * g + j][16 * dt + c];
+        bb[j] = ds4[2 * s][j]; bb[4 + j] = ds4[2 * s + 1][j];
+      }
+      acc = mfma16x16x32(a, bb, acc);
+    }
+    // C: rows d = 16 dt + 4 g + r, column = this lane's query -> 4 consecutive d (hd % 8 == 0)
+    const int d = 16 * dt + 4 * g;
+    if (qok && d < hd) {
+      bf16x4 o4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o4[r] = (bf16)acc[r];
+      *reinterpret_cast<bf16x4*>(dQ + b * sbdq + (long)qn * lddq + co + d) = o4;
+    }
+  }
+}
+
 // ---- fused MFMA attention backward (bf16, <= 64 keys): dQ and the dK / dV reductions in one kernel -------
 // One workgroup per (frame, head, query range); it stages K, V, K^T in LDS once and walks its range in
 // 64-query chunks (wave w: queries 16w .. 16w + 15 of the chunk).  Per chunk: S = Q K^T, dP = dO V^T,
@@ -1165,12 +1321,23 @@ extern "C" int svk_attention_bwd(int dtype, const void* Q, long ldq, long sbq, c
     bf16* Pws = reinterpret_cast<bf16*>(acc + 2 * nacc);
     bf16* dSws = Pws + (long)B * heads * Nq * nkp;
     dim3 grid((Nq + 63) / 64, heads, B);
+    // transposed-score kernel (round 6, profiles/r06/attn_bwd_t.txt: whole svk_attention_bwd at the train shapes
+    // 101 -> 89 us at 3136 queries, 289 -> 213 us for the 196-token cross-attention); SVK_ATTN_BWD_T=0 selects the
+    // round-5 kernel (A/B, tests; read at every call like SVK_ATTN_BWD_FUSED)
+    const char* tenv = getenv("SVK_ATTN_BWD_T");
+    const bool tscore = !(tenv && tenv[0] == '0');
     auto go = [&](auto hdp_c, auto nkc_c) {
       constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
-      hipLaunchKernelGGL((attn_bwd_dq_mfma<HDP, NKC>), grid, dim3(256), 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K,
-                         ldk, sbk, (const bf16*)V, ldv, sbv, (const bf16*)O, ldo, sbo, (const bf16*)dO, lddo, sbdo,
-                         (bf16*)dQ, lddq, sbdq, Pws, dSws, Nq, Nk, hd, scale, reinterpret_cast<float4*>(acc),
-                         zero_in_dq ? 2 * nacc / 4 : 0L);
+      if (tscore)
+        hipLaunchKernelGGL((attn_bwd_dq_t<HDP, NKC>), grid, dim3(256), 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K,
+                           ldk, sbk, (const bf16*)V, ldv, sbv, (const bf16*)O, ldo, sbo, (const bf16*)dO, lddo, sbdo,
+                           (bf16*)dQ, lddq, sbdq, Pws, dSws, Nq, Nk, hd, scale, reinterpret_cast<float4*>(acc),
+                           zero_in_dq ? 2 * nacc / 4 : 0L);
+      else
+        hipLaunchKernelGGL((attn_bwd_dq_mfma<HDP, NKC>), grid, dim3(256), 0, st, (const bf16*)Q, ldq, sbq, (const bf16*)K,
+                           ldk, sbk, (const bf16*)V, ldv, sbv, (const bf16*)O, ldo, sbo, (const bf16*)dO, lddo, sbdo,
+                           (bf16*)dQ, lddq, sbdq, Pws, dSws, Nq, Nk, hd, scale, reinterpret_cast<float4*>(acc),
+                           zero_in_dq ? 2 * nacc / 4 : 0L);
     };
     using H32 = std::integral_constant<int, 32>;
     using H64 = std::integral_constant<int, 64>;

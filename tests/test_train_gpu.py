@@ -272,10 +272,17 @@ def test_unpatchify_split_vs_fused(cuda, dt, B, C, H, r):
         assert float(d.max()) <= 2 * ulp, float(d.max())
 
 
+@pytest.mark.parametrize("tkern", ["1", "0"])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("Nq,Nk,heads,hd", [(3136, 49, 1, 64), (196, 196, 8, 40), (49, 49, 8, 64), (100, 30, 2, 16)])
-def test_attention_bwd(cuda, dt, Nq, Nk, heads, hd):
+@pytest.mark.parametrize("Nq,Nk,heads,hd", [(3136, 49, 1, 64), (196, 196, 8, 40), (49, 49, 8, 64), (100, 30, 2, 16),
+                                            (196, 196, 5, 64), (130, 100, 3, 32), (70, 150, 2, 64)])
+def test_attention_bwd(cuda, monkeypatch, tkern, dt, Nq, Nk, heads, hd):
+    """bf16: the transposed-score dQ kernel (attn_bwd_dq_t, default) and the round-5 one (SVK_ATTN_BWD_T=0), every
+    key-chunk count NKC = 1..4 and both head-dim paddings; f32: the LDS scalar kernel."""
     from svk import ops
+    if dt == torch.float32 and tkern == "0":
+        pytest.skip("the switch selects between bf16 kernels")
+    monkeypatch.setenv("SVK_ATTN_BWD_T", tkern)
     B, C = 2, heads * hd
     q, k, v = _rand(B, Nq, C, seed=1), _rand(B, Nk, C, seed=2), _rand(B, Nk, C, seed=3)
     do = _rand(B, Nq, C, seed=4)
