@@ -838,7 +838,11 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
     const bool vec = (C % 8 == 0) && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 15) == 0;
     const int lds_env = g_tune[TUNE_DW_LDS], rows_env = g_tune[TUNE_DW_ROWS];   // svk_tune knobs
     constexpr bool is_bf16 = std::is_same<T, bf16>::value;   // the opt-in variants below are bf16-only
-    if (is_bf16 && lds_env == 2 && C % 4 == 0 && (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 7) == 0) {
+    // rolling window: by default for the bf16 activation-free conv (the train step's dwconv data gradient with
+    // flipped taps; round 6, profiles/r06/dw_train.txt: 87.8 -> 78.9 us at 88 x 56 x 56 x 256, 43.0 -> 38.9 at
+    // 28 x 28 x 512, 18.0 -> 13.1 at 7 x 7 x 2048), or forced by dw_lds = 2
+    if (is_bf16 && (lds_env == 2 || (lds_env < 0 && act == SVK_ACT_NONE)) && C % 4 == 0 &&
+        (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 7) == 0) {
       constexpr int RR = 8;
       const int nstrip = (H + RR - 1) / RR;
       const long n = (long)B * nstrip * W * (C / 4);

@@ -351,7 +351,7 @@ def test_gemm_ln(cuda, dt, M, N, K, res, bias, monkeypatch):
     _close(h, hd, dt)
 
 
-@pytest.mark.parametrize("lds,rows", [(1, 1), (1, 3), (1, 8), (2, -1)])
+@pytest.mark.parametrize("lds,rows", [(1, 1), (1, 3), (1, 8), (2, -1), (0, -1)])
 def test_dwconv_lds_variant(cuda, lds, rows):
     """The LDS-tiled depthwise conv (svk_tune dw_lds = 1) at several strip heights, with the
     pre-activation store, against fp64."""
@@ -372,6 +372,29 @@ def test_dwconv_lds_variant(cuda, lds, rows):
     finally:
         ops.tune("dw_lds", -1)
         ops.tune("dw_rows", -1)
+
+
+def test_dwconv_identity_default_is_bit_exact_across_kernels(cuda):
+    """The activation-free bf16 depthwise conv (the train step's data gradient: flipped taps, zero bias) runs the
+    rolling-window kernel by default (round 6); it must equal the strip and LDS kernels bit for bit (same f32 tap
+    order) and fp64 to bf16 rounding — including C % 8 != 0 and maps whose height is not a multiple of the strip."""
+    from svk import ops
+    dt = torch.bfloat16
+    try:
+        for B, H, W, C in ((3, 56, 56, 64), (2, 28, 28, 512), (2, 14, 14, 1280), (3, 7, 7, 2048), (2, 19, 5, 68)):
+            x = _rand(B, H, W, C, dt=dt, dev=cuda, seed=71)
+            w = _rand(C, 1, 3, 3, dt=torch.float32, dev="cpu", scale=0.4, seed=72)
+            taps, zero = w.reshape(C, 9).t().contiguous().to(cuda), torch.zeros(C, device=cuda)
+            outs = []
+            for lds in (-1, 0, 1):
+                ops.tune("dw_lds", lds)
+                outs.append(ops.dwconv3x3(x, taps, zero))
+            for o in outs[1:]:
+                assert torch.equal(o, outs[0]), (B, H, W, C)
+            ref = F.conv2d(x.cpu().double().permute(0, 3, 1, 2), w.double(), None, padding=1, groups=C)
+            _close(outs[0], ref.permute(0, 2, 3, 1), dt)
+    finally:
+        ops.tune("dw_lds", -1)
 
 
 @pytest.mark.parametrize("kind", ["conv", "gemm"])
