@@ -306,43 +306,41 @@ struct Cfg {
   static constexpr int HBYTES = DPW * NW * 1024, HSTRIDE = HBYTES + 1024, NHB = 3, GBYTES = NMB * 16 * 128;
   static constexpr int H_OFF = 0, G_OFF = NHB * HSTRIDE, LDS = G_OFF + 2 * GBYTES;
   static constexpr int TILES_PER_FRAME = (WI + R - 1) / R;
-  // packed operands per K-step (svk_mixffn_dw_fc2_pack): A part [4 channel blocks][6][64 lanes] x 16 B (5 dwconv
-  // A fragments + the lane's 4 dwconv biases), then W2 part [2 ks][NW waves][WNB][64 lanes] x 16 B (fc2 A
-  // fragments): every load of the K loop is one contiguous 1 KiB wave-instruction
-  static constexpr int APK = 4 * 6 * 64 * 16, WPK = 2 * NW * WNB * 64 * 16, PK = APK + WPK;
+  // packed operands (svk_mixffn_dw_fc2_pack): per K-step the W2 part [2 ks][NW waves][WNB][64 lanes] x 16 B (fc2 A
+  // fragments: every W2 load of the K loop is one contiguous 1 KiB wave-instruction); after the last K-step the
+  // taps rounded to T, [9][K], and dbias [K] f32, from which each lane builds its one-non-zero dwconv A fragments.
+  // (Round 5 packed those fragments and the biases expanded, 6 KiB per wave per K-step: with W2 that stream
+  // ran the kernel at ~14 TB/s of L2 requests, near the L2 limit; round 6 reads 5 two-byte taps + one bias chunk.)
+  static constexpr int PK = 2 * NW * WNB * 64 * 16;
+  static constexpr long bytes(int K) { return (long)(K / BK) * PK + 9L * K * 2 + 4L * K; }
   static_assert(N % (16 * NW) == 0 && R * SW == 16 * NMB && SW % 8 == 0 && HROWS * SW * 128 <= HBYTES &&
                 SW >= WI + 1 && WNB >= 1 && MPW >= 1, "shape");
 };
 
-// packed operands: one thread per 16-byte chunk (A part, then W2 part, K-step-major)
+// packed operands: one thread per 16-byte chunk (the W2 part K-step-major, then the T taps, then dbias)
 template <typename T, class C>
 __global__ __launch_bounds__(256) void dwfc2_pack(const float* __restrict__ taps, const float* __restrict__ dbias,
                                                   const T* __restrict__ W2, int K, uint4* __restrict__ out) {
   const int nk = K / C::BK;
-  const long id = (long)blockIdx.x * 256 + threadIdx.x;
-  if (id >= (long)nk * (C::PK / 16)) return;
-  const int kt = (int)(id / (C::PK / 16)), r = (int)(id % (C::PK / 16));
-  const int lane = r % 64, fr = lane & 15, fq = lane >> 4;
-  if (r < C::APK / 16) {
-    const int j = (r / 64) % 6, cb = r / (64 * 6);
-    if (j == 5) {                                      // dwconv bias of channels 16 cb + 4 fq .. + 3
-      const float* d = dbias + kt * 64 + 16 * cb + 4 * fq;
-      out[id] = uint4{__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3])};
-      return;
-    }
-    // A fragment kk = j: row = channel 16 cb + fr, k-slot 8 fq + e = (tap 2 kk + (fq >> 1), channel 8 (fq & 1) + e
-    // of the block): tap[t][16 cb + fr] where 8 (fq & 1) + e == fr, 0 elsewhere (and for the padding tap t = 9)
-    const int t = 2 * j + (fq >> 1), e = fr - 8 * (fq & 1);
+  const long id = (long)blockIdx.x * 256 + threadIdx.x, nw2 = (long)nk * (C::PK / 16), ntap = 9L * K / 8;
+  if (id >= nw2 + ntap + K / 4) return;
+  if (id >= nw2 + ntap) {                              // dbias, 4 floats per chunk
+    const float* d = dbias + (id - nw2 - ntap) * 4;
+    out[id] = uint4{__float_as_uint(d[0]), __float_as_uint(d[1]), __float_as_uint(d[2]), __float_as_uint(d[3])};
+    return;
+  }
+  if (id >= nw2) {                                     // taps [9][K] rounded to T (as autocast casts the conv weight)
+    const float* t = taps + (id - nw2) * 8;
     T v[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = from_f<T>(0.f);
-    if (t < 9 && e >= 0 && e < 8) v[e] = from_f<T>(taps[(long)t * K + kt * 64 + 16 * cb + fr]);
+    for (int q = 0; q < 8; ++q) v[q] = from_f<T>(t[q]);
     out[id] = *reinterpret_cast<const uint4*>(v);
-  } else {
-    const int rr = r - C::APK / 16, nb = (rr / 64) % C::WNB, w = (rr / (64 * C::WNB)) % C::NW;
-    const int ks = rr / (64 * C::WNB * C::NW);
-    out[id] = *reinterpret_cast<const uint4*>(W2 + (long)(w * (C::N / C::NW) + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
+    return;
   }
+  const int kt = (int)(id / (C::PK / 16)), rr = (int)(id % (C::PK / 16));
+  const int lane = rr % 64, fr = lane & 15, fq = lane >> 4;
+  const int nb = (rr / 64) % C::WNB, w = (rr / (64 * C::WNB)) % C::NW, ks = rr / (64 * C::WNB * C::NW);
+  out[id] = *reinterpret_cast<const uint4*>(W2 + (long)(w * (C::N / C::NW) + nb * 16 + fr) * K + kt * 64 + ks * 32 + fq * 8);
 }
 
 // gelu_rl's formula on two packed pairs (svk_common.h gelu_pk<5>: the polynomial, squares and the final fma
@@ -440,25 +438,47 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
     const int L = fr + dy * SW + dx - 1, c = 2 * cb + (fq & 1);
     hoff[kk] = (L + 1) * 128 + ((c ^ (L & 7)) << 4);
   }
-  // dwconv A fragments (one non-zero each, built by dwfc2_pack) and the lane's dwconv biases, one K-step
-  // at a time: loaded right after dwconv(k) has read them, for dwconv(k + 1) one iteration later
-  tx8 afr[5];
+  // dwconv A fragment kk: row = channel 16 cb + fr, k-slot 8 fq + e = (tap 2 kk + (fq >> 1), channel 8 (fq & 1) + e
+  // of the block) -> the single non-zero tap[t][16 cb + fr] sits at e = fr - 8 (fq & 1) when 0 <= e < 8 (t = 9 is
+  // the padding tap: zero).  Each lane loads its 5 two-byte taps and its 4 dwconv biases (one K-step at a time:
+  // right after dwconv(k) has read them, for dwconv(k + 1) one iteration later) and builds the fragments in dwconv.
+  const long nk_bytes = (long)(K / C::BK) * C::PK;
+  const char* tapl = pk + nk_bytes + (long)(16 * cb + fr) * 2;                 // + (t K + kt 64) * 2
+  const char* dbl = pk + nk_bytes + 9L * K * 2 + (16 * cb + 4 * fq) * 4;      // + kt 64 * 4
+  const int ae = fr - 8 * (fq & 1);
+  const bool a_lane = ae >= 0 && ae < 8;               // this lane holds the non-zero of its fragments
+  const uint32_t a_sh = 16u * (ae & 1);
+  const int a_dw = (ae >> 1) & 3;
+  uint32_t araw[5];
   f32x4 dbv;
-  const char* pkl = pk + lane * 16;
   auto load_a = [&](int kt) {
-    const char* src = pkl + (long)kt * C::PK + cb * 6 * 1024;
 #pragma unroll
-    for (int kk = 0; kk < 5; ++kk) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(afr[kk]) : "v"(src + kk * 1024) : "memory");
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dbv) : "v"(src + 5 * 1024) : "memory");
+    for (int kk = 0; kk < 5; ++kk) {
+      const int t = min(2 * kk + (fq >> 1), 8);        // (t = 9 loads tap 8; zeroed when the fragment is built)
+      asm volatile("global_load_ushort %0, %1, off" : "=v"(araw[kk]) : "v"(tapl + ((long)t * K + kt * 64) * 2) : "memory");
+    }
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dbv) : "v"(dbl + kt * 256) : "memory");
   };
   auto tie_a = [&]() {
 #pragma unroll
-    for (int kk = 0; kk < 5; ++kk) asm volatile("" : "+v"(afr[kk]));
+    for (int kk = 0; kk < 5; ++kk) asm volatile("" : "+v"(araw[kk]));
     asm volatile("" : "+v"(dbv));
   };
   f32x4 dacc[MPW];
   auto dwconv = [&](int hb) {
     const char* hs = smem + C::H_OFF + hb * C::HSTRIDE + mb0 * 2048;
+    tx8 afr[5];
+#pragma unroll
+    for (int kk = 0; kk < 5; ++kk) {
+      const bool nz = a_lane && 2 * kk + (fq >> 1) < 9;
+      const uint32_t v = nz ? (araw[kk] & 0xFFFFu) << a_sh : 0u;
+      uint4 d;
+      d.x = a_dw == 0 ? v : 0u;
+      d.y = a_dw == 1 ? v : 0u;
+      d.z = a_dw == 2 ? v : 0u;
+      d.w = a_dw == 3 ? v : 0u;
+      afr[kk] = *reinterpret_cast<const tx8*>(&d);
+    }
 #pragma unroll
     for (int m = 0; m < MPW; ++m) dacc[m] = dbv;
 #pragma unroll
@@ -494,8 +514,9 @@ __global__ __launch_bounds__(C::NT, 512 / C::NT) void dwfc2_rw(const T* __restri
   // ---- fc2: wave's n-blocks n0w + 16 nb over the 4 m-blocks, W2 fragments of one K-step (2 x 32 channels)
   const int n0w = wave * (C::N / NW);
   tx8 w2f[2][WNB];
+  const char* pkl = pk + lane * 16;
   auto load_w2 = [&](int kt, int ks) {
-    const char* src = pkl + (long)kt * C::PK + C::APK + (ks * NW + wave) * WNB * 1024;
+    const char* src = pkl + (long)kt * C::PK + (ks * NW + wave) * WNB * 1024;
 #pragma unroll
     for (int nb = 0; nb < WNB; ++nb)
       asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(w2f[ks][nb]) : "v"(src + nb * 1024) : "memory");
@@ -618,7 +639,7 @@ static int launch(const void* H, const void* pk, const float* b2, const void* R,
 
 template <typename T, class C>
 static int pack(const float* taps, const float* db, const void* W2, int K, void* out, hipStream_t st) {
-  const long n = (long)(K / C::BK) * (C::PK / 16);
+  const long n = C::bytes(K) / 16;
   hipLaunchKernelGGL((dwfc2_pack<T, C>), dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, taps, db, (const T*)W2, K,
                      (uint4*)out);
   return check_launch("dw_fc2_pack");
@@ -661,9 +682,9 @@ extern "C" int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, co
 // ---- the stage-3 form with the depthwise conv on MFMA: operands packed once per weight set -------------
 extern "C" long svk_mixffn_dw_fc2_packed_bytes(int dtype, int W, int N, int K) {
   if (!(dtype == SVK_F16 || dtype == SVK_BF16) || K % 64 || K <= 0) return 0;
-  if (W == 14 && N == 320) return (long)(K / 64) * dwrw::Cfg<320, 14>::PK;
-  if (W == 7 && N == 512) return (long)(K / 64) * dwrw::Cfg<512, 7>::PK;
-  if (W == 28 && N == 128) return (long)(K / 64) * dwrw::Cfg<128, 28>::PK;
+  if (W == 14 && N == 320) return dwrw::Cfg<320, 14>::bytes(K);
+  if (W == 7 && N == 512) return dwrw::Cfg<512, 7>::bytes(K);
+  if (W == 28 && N == 128) return dwrw::Cfg<128, 28>::bytes(K);
   return 0;
 }
 

@@ -96,6 +96,7 @@ def check_packed(funcs):
 VMEM_RE = re.compile(r"(global_|buffer_|flat_|scratch_)")
 ASM_LOAD_KERNELS = ("gemm_pk", "dwfc2_rw", "gemm_ln")          # kernels whose global loads are issued from inline asm
 VMCNT_RE = re.compile(r"vmcnt\((\d+)\)")
+LOAD_RE = re.compile(r"global_load_(dword(x2|x4)?|ushort|ubyte|short_d16|sshort)$")   # VGPR-destination loads
 
 
 def check_epilogue_loads(funcs):
@@ -109,7 +110,7 @@ def check_epilogue_loads(funcs):
             continue
         at = {a: k for k, (a, *_rest) in enumerate(ins)}
         for k, (addr, op, ops, _) in enumerate(ins):
-            if not re.match(r"global_load_dword(x2|x4)?$", op):
+            if not LOAD_RE.match(op):
                 continue
             dst = regs(operands(ops)[0])
             seen, stack = {}, [(k + 1, 0, None)]
@@ -178,7 +179,7 @@ def main(objs):
             print(f"isa_check: {os.path.basename(obj)}: epilogue load register touched before its wait: {msg}")
             fails += 1
         nload += sum(1 for f, ins in funcs.items() if any(t in f for t in ASM_LOAD_KERNELS) for _, op, _, _ in ins
-                     if re.match(r"global_load_dword(x2|x4)?$", op))
+                     if LOAD_RE.match(op))
     print(f"isa_check: {len(objs)} objects, {nload} asm-load kernel loads audited ({', '.join(ASM_LOAD_KERNELS)}), "
           f"{fails} violation(s)")
     return 1 if fails else 0

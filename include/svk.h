@@ -147,8 +147,9 @@ int svk_mixffn_dw_fc2(int dtype, const void* H, const float* taps, const float* 
  * 16-bit) with the
  * depthwise conv on the matrix cores
  * (csrc/dwfc2.hip, dwrw): the operands are packed once per weight set — svk_mixffn_dw_fc2_pack writes
- * svk_mixffn_dw_fc2_packed_bytes(...) bytes (16-byte aligned): per 64-channel K-step the dwconv A fragments
- * (taps rounded to the 16-bit type, block-diagonal), the dwconv biases and the W2 fragments, in load order —
+ * svk_mixffn_dw_fc2_packed_bytes(...) bytes (16-byte aligned): per 64-channel K-step the W2 fragments in load
+ * order, then the taps rounded to the 16-bit type [9][K] and the dwconv biases [K] f32 (round 6: the kernel builds
+ * its block-diagonal dwconv A fragments from those; the buffer size changed with that layout) —
  * then svk_mixffn_dw_fc2_packed computes Y = GELU(dwconv3x3(H) + dbias) W2^T + b2 (+ R) from H and the packed
  * buffer (same H / b2 / R / Y contract as svk_mixffn_dw_fc2).  packed_bytes is 0 where there is no packed form;
  * the other two return SVK_EUNSUPPORTED there. */
