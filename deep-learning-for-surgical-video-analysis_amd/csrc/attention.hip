@@ -244,8 +244,11 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16(const T* __restrict__
 // wave then walks its 16-query tiles (tile t = wave, wave + 4, ...), the softmax over all keys
 // computed chunk by chunk exactly as in attention_mfma_bf16.  The output tile goes through a
 // per-wave LDS patch and leaves as 16-byte row pieces (one head row = hd * 2 bytes) instead of
-// 2-byte scattered stores.
-template <typename T, int HDP, int NKC>
+// 2-byte scattered stores.  (Round 6: QB = 64 for the short stage-3 / 4 sequences — one 256-query workgroup per
+// (frame, head) leaves its waves 4 / 3 / 3 / 3 tiles at 196 queries — ran the extraction step 0.7 % SLOWER in three
+// interleaved pairs, profiles/r06/attn_qb64_ab.txt: the fourfold K / V staging costs more than the balance gains.
+// Kept selectable, SVK_ATTN_QB=64, and tested bit-identical.)
+template <typename T, int HDP, int NKC, int QB = 256>
 __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restrict__ Q, long ldq, long sbq,
                                                                const T* __restrict__ K, long ldk, long sbk,
                                                                const T* __restrict__ V, long ldv, long sbv,
@@ -256,7 +259,6 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restri
   constexpr int VLD = NKP + 8;    // sVt row stride (elements)
   constexpr int OLD = HDP + 8;    // per-wave output patch row stride
   constexpr int NKS = HDP / 32, NDT = HDP / 16;
-  constexpr int QB = 256;
   typedef v8_t<T> tx8;
   typedef v4_t<T> tx4;
   __shared__ __attribute__((aligned(16))) T sK[NKP][KLD];
@@ -552,11 +554,18 @@ extern "C" int svk_attention(int dtype, const void* Q, long ldq, long sbq, const
     SVK_DISPATCH_H16(dtype, T, {
       if (res_ok) {
         const int nkc = (Nk + 63) / 64;
-        dim3 rgrid((Nq + 255) / 256, heads, B);
+        // query block 256; SVK_ATTN_QB=64 selects 64-query blocks (read at every call; measured slower, see the kernel)
+        const char* qbe = getenv("SVK_ATTN_QB");
+        const int qb = qbe && atoi(qbe) == 64 ? 64 : 256;
+        dim3 rgrid((Nq + qb - 1) / qb, heads, B);
         auto go = [&](auto hdp_c, auto nkc_c) {
           constexpr int HDP = decltype(hdp_c)::value, NKC = decltype(nkc_c)::value;
-          hipLaunchKernelGGL((attention_mfma_bf16_res<T, HDP, NKC>), rgrid, block, 0, st, (const T*)Q, ldq, sbq,
-                             (const T*)K, ldk, sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
+          if (qb == 64)
+            hipLaunchKernelGGL((attention_mfma_bf16_res<T, HDP, NKC, 64>), rgrid, block, 0, st, (const T*)Q, ldq, sbq,
+                               (const T*)K, ldk, sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
+          else
+            hipLaunchKernelGGL((attention_mfma_bf16_res<T, HDP, NKC>), rgrid, block, 0, st, (const T*)Q, ldq, sbq,
+                               (const T*)K, ldk, sbk, (const T*)V, ldv, sbv, (T*)O, ldo, sbo, Nq, Nk, hd, sl2);
         };
         auto by_nkc = [&](auto hdp) {
           switch (nkc) {

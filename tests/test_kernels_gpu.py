@@ -480,7 +480,9 @@ def test_layernorm(cuda, dt, M, C, eps):
 @pytest.mark.parametrize("B,Nq,Nk,heads,hd", [(2, 3136, 49, 1, 64), (2, 784, 49, 2, 64), (3, 196, 196, 8, 40),
                                               (2, 49, 49, 8, 64), (5, 30, 30, 4, 32), (7, 1, 1, 4, 32),
                                               (2, 196, 49, 5, 32), (1, 100, 256, 1, 64)])
-def test_attention(cuda, dt, B, Nq, Nk, heads, hd):
+def test_attention(cuda, monkeypatch, dt, B, Nq, Nk, heads, hd):
+    """16-bit: the resident-K/V kernel with its default 256-query block, and 64- / 256-query blocks forced
+    (SVK_ATTN_QB; round 6) — bit-identical to each other (same per-tile arithmetic) and within tolerance of fp64."""
     from svk import ops
     C = heads * hd
     q = _rand(B, Nq, C, dt=dt, dev=cuda, seed=13)
@@ -488,6 +490,11 @@ def test_attention(cuda, dt, B, Nq, Nk, heads, hd):
     k, v = kv[:, :, :C], kv[:, :, C:]
     scale = hd ** -0.5
     got = ops.attention(q, k, v, heads, scale)
+    if dt != torch.float32:
+        for qb in ("64", "256"):
+            monkeypatch.setenv("SVK_ATTN_QB", qb)
+            assert torch.equal(ops.attention(q, k, v, heads, scale), got), qb
+        monkeypatch.delenv("SVK_ATTN_QB")
     torch.cuda.synchronize()
     qh = q.cpu().double().reshape(B, Nq, heads, hd).transpose(1, 2)
     kh = k.cpu().double().reshape(B, Nk, heads, hd).transpose(1, 2)
