@@ -274,45 +274,145 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restri
   T* Ob = O + (long)b * sbo + (long)h * hd;
   const T zero = (T)0.f;
 
-  // stage K [key][d] and V^T [d][key] for all keys (zeros past Nk / hd)
-  for (int e = tid; e < NKP * (HDP / 8); e += 256) {
-    const int key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
-    tx8 kv, vv;
-    if (key < Nk && d0 < hd) {
-      kv = *reinterpret_cast<const tx8*>(Kb + (long)key * ldk + d0);
-      vv = *reinterpret_cast<const tx8*>(Vb + (long)key * ldv + d0);
-    } else {
+  // this wave's Q tile rows (zeros past Nq / hd); a tile's rows are loaded one tile ahead (round 6)
+  const int qbase = blockIdx.x * QB;
+  auto load_q = [&](int qt, tx8 (&qf)[NKS]) {
+    const int qr = qbase + qt * 16 + c;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { kv[j] = zero; vv[j] = zero; }
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int d0 = 32 * ks + 8 * g;
+      if (qt < QB / 16 && qr < Nq && d0 < hd) {
+        qf[ks] = *reinterpret_cast<const tx8*>(Qb + (long)qr * ldq + d0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[ks][j] = zero;
+      }
     }
-    *reinterpret_cast<tx8*>(&sK[key][d0]) = kv;
+  };
+  // stage K [key][d] and V^T [d][key] for all keys (zeros past Nk / hd); with several key chunks (round 6) every
+  // thread's K / V pieces are loaded before the first LDS write and each wave's Q tile one tile ahead (at one chunk
+  // the extra registers cost more than the overlap gains: 22.6 -> 24.1 us at 196 x 49, profiles/r06/attn_twopass.txt)
+  constexpr bool PF = NKC > 1;
+  if constexpr (!PF) {
+    for (int e = tid; e < NKP * (HDP / 8); e += 256) {
+      const int key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
+      tx8 kv, vv;
+      if (key < Nk && d0 < hd) {
+        kv = *reinterpret_cast<const tx8*>(Kb + (long)key * ldk + d0);
+        vv = *reinterpret_cast<const tx8*>(Vb + (long)key * ldv + d0);
+      } else {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[j];
+        for (int j = 0; j < 8; ++j) { kv[j] = zero; vv[j] = zero; }
+      }
+      *reinterpret_cast<tx8*>(&sK[key][d0]) = kv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[j];
+    }
+  } else {
+    constexpr int NST = NKP * (HDP / 8) / 256;
+    static_assert(NKP * (HDP / 8) % 256 == 0, "whole staging rounds");
+    tx8 kv[NST], vv[NST];
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int e = tid + 256 * i, key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
+      if (key < Nk && d0 < hd) {
+        kv[i] = *reinterpret_cast<const tx8*>(Kb + (long)key * ldk + d0);
+        vv[i] = *reinterpret_cast<const tx8*>(Vb + (long)key * ldv + d0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { kv[i][j] = zero; vv[i][j] = zero; }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NST; ++i) {
+      const int e = tid + 256 * i, key = e / (HDP / 8), d0 = (e % (HDP / 8)) * 8;
+      *reinterpret_cast<tx8*>(&sK[key][d0]) = kv[i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sVt[d0 + j][key] = vv[i][j];
+    }
   }
+  tx8 qf[NKS];
+  if constexpr (PF) load_q(wave, qf);
   __syncthreads();
 
-  const int qbase = blockIdx.x * QB;
   for (int qt = wave; qt < QB / 16; qt += 4) {
     const int q0 = qbase + qt * 16;
     if (q0 >= Nq) break;
-    tx8 qf[NKS];
-    {
-      const int qr = q0 + c;
+    tx8 qn[NKS];
+    if constexpr (PF) load_q(qt + 4, qn);
+    else load_q(qt, qf);
+    f32x4 o[NDT];
+    float l_run;
+    if constexpr (PF) {
+    // all keys are resident, so the softmax takes two passes over registers instead of an online rescale per key
+    // chunk (round 6: the rescale, the per-chunk max / sum shuffles and the key mask of every chunk were most of the
+    // 4.6 k VALU instructions per wave at 196 keys; only the last chunk can hold padded keys, 64 (NKC - 1) < Nk)
+    f32x4 s[NKC][4];
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int d0 = 32 * ks + 8 * g;
-        if (qr < Nq && d0 < hd) {
-          qf[ks] = *reinterpret_cast<const tx8*>(Qb + (long)qr * ldq + d0);
-        } else {
+    for (int ch = 0; ch < NKC; ++ch)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) qf[ks][j] = zero;
+      for (int t = 0; t < 4; ++t) {
+        s[ch][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const tx8 a = *reinterpret_cast<const tx8*>(&sK[ch * KC + 16 * t + c][32 * ks + 8 * g]);
+          s[ch][t] = mfma16x16x32(a, qf[ks], s[ch][t]);
+        }
+      }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int ch = 0; ch < NKC; ++ch)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (ch < NKC - 1 || ch * KC + 16 * t + 4 * g + r < Nk) mx = fmaxf(mx, s[ch][t][r]);
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mb = mx * scale_log2;
+    l_run = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < NKC; ++ch)
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool real = ch < NKC - 1 || ch * KC + 16 * t + 4 * g + r < Nk;
+          const float p = real ? exp2f(fmaf(s[ch][t][r], scale_log2, -mb)) : 0.f;
+          s[ch][t][r] = p;
+          l_run += p;
+        }
+    l_run += __shfl_xor(l_run, 16, 64);
+    l_run += __shfl_xor(l_run, 32, 64);
+#pragma unroll
+    for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < NKC; ++ch) {
+      const int kc0 = ch * KC;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        tx8 pa;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pa[j] = (T)s[ch][2 * s2][j];
+          pa[4 + j] = (T)s[ch][2 * s2 + 1][j];
+        }
+#pragma unroll
+        for (int dt = 0; dt < NDT; ++dt) {
+          const tx4 v0 = *reinterpret_cast<const tx4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 4 * g]);
+          const tx4 v1 = *reinterpret_cast<const tx4*>(&sVt[16 * dt + c][kc0 + 32 * s2 + 16 + 4 * g]);
+          tx8 vb;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { vb[j] = v0[j]; vb[4 + j] = v1[j]; }
+          o[dt] = mfma16x16x32(pa, vb, o[dt]);
         }
       }
     }
-    f32x4 o[NDT];
+    } else {   // one key chunk: the round-5 online form (one pass)
 #pragma unroll
     for (int dt = 0; dt < NDT; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    float m_run = -INFINITY, l_run = 0.f;
+    float m_run = -INFINITY;
+    l_run = 0.f;
 #pragma unroll
     for (int ch = 0; ch < NKC; ++ch) {
       const int kc0 = ch * KC;
@@ -380,6 +480,7 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restri
         }
       }
     }
+    }
     // normalise; stage the 16 x hd tile in this wave's LDS patch; 16-byte row pieces out
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -397,6 +498,10 @@ __global__ __launch_bounds__(256) void attention_mfma_bf16_res(const T* __restri
       if (q < Nq) *reinterpret_cast<uint4*>(Ob + (long)q * ldo + cc * 8) = *reinterpret_cast<const uint4*>(&sO[wave][row][cc * 8]);
     }
     __builtin_amdgcn_wave_barrier();   // the patch is rewritten by this wave's next tile
+    if constexpr (PF) {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) qf[ks] = qn[ks];
+    }
   }
 }
 
