@@ -841,7 +841,11 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
     // rolling window: by default for the bf16 activation-free conv (the train step's dwconv data gradient with
     // flipped taps; round 6, profiles/r06/dw_train.txt: 87.8 -> 78.9 us at 88 x 56 x 56 x 256, 43.0 -> 38.9 at
     // 28 x 28 x 512, 18.0 -> 13.1 at 7 x 7 x 2048), or forced by dw_lds = 2
-    if (is_bf16 && (lds_env == 2 || (lds_env < 0 && act == SVK_ACT_NONE)) && C % 4 == 0 &&
+    // with GELU (the train forward's stages 3-4, + pre-activation store; profiles/r06/dw_train.txt): the rolling window
+    // at 7 x 7 (20.1 -> 15.7 us at 2048 channels), the LDS halo tile at 14 x 14 with >= 1024 channels (37.2 -> 33.0)
+    const bool auto_roll = lds_env < 0 && (act == SVK_ACT_NONE || W <= 8);
+    const bool auto_lds = lds_env < 0 && act != SVK_ACT_NONE && W > 8 && W <= 16 && C >= 1024;
+    if (is_bf16 && (lds_env == 2 || auto_roll) && C % 4 == 0 &&
         (((uintptr_t)X | (uintptr_t)Y | (uintptr_t)Ypre) & 7) == 0) {
       constexpr int RR = 8;
       const int nstrip = (H + RR - 1) / RR;
@@ -850,7 +854,7 @@ extern "C" int svk_dwconv3x3_ex(int dtype, const void* X, const float* w, const 
                          (bf16*)Ypre, B, H, W, C, act, nstrip);
       return check_launch("dwconv3x3_roll");
     }
-    if (is_bf16 && vec && C % 64 == 0 && lds_env == 1) {
+    if (is_bf16 && vec && C % 64 == 0 && (lds_env == 1 || auto_lds)) {
       // strip height: the tallest strip whose halo tile fits 48 KiB (3 workgroups per CU)
       int R = rows_env > 0 ? rows_env : 49152 / ((W + 2) * 128) - 2;
       R = std::max(1, std::min(R, H));

@@ -14,6 +14,7 @@ from pk_cfg_sweep import timeit  # noqa: E402
 
 SHAPES = [(56, 256), (28, 512), (14, 1280), (7, 2048)]
 VARIANTS = [(0, "strip"), (1, "lds"), (2, "roll4")]
+ACT = os.environ.get("DW_ACT", "")   # "gelu": the training forward's form (GELU + pre-activation store)
 
 
 def main():
@@ -23,10 +24,13 @@ def main():
         x = torch.randn(B, H, H, C, device=dev).to(torch.bfloat16)
         taps = torch.randn(9, C, device=dev)
         zero = torch.zeros(C, device=dev)
+        pre = torch.empty_like(x)
         times, ref, err = {v: [] for v, _ in VARIANTS}, None, {}
 
         def run(v):
             lib.svk_tune(b"dw_lds", v)
+            if ACT:
+                return ops.dwconv3x3(x, taps, zero, act=ACT, pre_out=pre)
             return ops.dwconv3x3(x, taps, zero)
         for v, _ in VARIANTS:
             y = run(v).float()
@@ -36,7 +40,7 @@ def main():
             for v, _ in VARIANTS:
                 times[v].append(timeit(lambda: run(v), 20))
         lib.svk_tune(b"dw_lds", -1)
-        gb = 2 * x.numel() * 2 / 1e9
+        gb = (3 if ACT else 2) * x.numel() * 2 / 1e9
         print(f"[{B},{H},{H},{C}] " + " | ".join(
             f"{nm} {sorted(times[v])[1] * 1e3:6.1f}us {gb / (sorted(times[v])[1] * 1e-3) / 1e3:4.2f}TB/s d={err[v]:.0e}"
             for v, nm in VARIANTS), flush=True)
