@@ -67,6 +67,8 @@ _TILE = np.dtype([("src", "<i8"), ("dst", "<i8"), ("K", "<i4"), ("N", "<i4"), ("
 PACK_TRANSPOSE = os.environ.get("SVK_PACK_TRANSPOSE", "1") == "1"
 # the generic gather 8 elements per thread (svk_pack_params8; 0 = one element per thread)
 PACK_PARAMS8 = os.environ.get("SVK_PACK_PARAMS8", "1") == "1"
+# conv data-gradient packs (.D) through the tiled transpose (A/B switch; 0 = the strided gather)
+PACK_D_TRANSPOSE = os.environ.get("SVK_PACK_D_T", "1") == "1"
 
 
 def is_trainable(name):
@@ -240,7 +242,12 @@ class EVPTrainStep:
             cp = pad_channels(ci) if pad_in else ci
             self.pk[name] = tab.add(o, (co, k, k, cp), (ci * k * k, k, 1, k * k), (co, k, k, ci), view=(co, k * k * cp))
             if dgrad:
-                self.pk[name + ".D"] = tab.add(o, (ci, k, k, co), (k * k, k, 1, ci * k * k), view=(ci, k * k * co))
+                # (ci, k, k, co) = the 2-D transpose of the master's [co][ci * k * k] rows: the tiled transpose
+                # kernel instead of the strided gather (round 6)
+                if PACK_D_TRANSPOSE:
+                    self.pk[name + ".D"] = tab.add(o, (ci * k * k, co), (1, ci * k * k), view=(ci, k * k * co))
+                else:
+                    self.pk[name + ".D"] = tab.add(o, (ci, k, k, co), (k * k, k, 1, ci * k * k), view=(ci, k * k * co))
                 self.pk[name + ".C"] = tab.add(o, (k, k, ci, co), (k, 1, k * k, ci * k * k), view=(k * k * ci, co))
             # weight-gradient scratch in the packed layout, unpacked into the flat grad after backward
             n = co * k * k * cp
