@@ -46,6 +46,31 @@ def test_layernorm_bwd(cuda, M, C):
     _close(db, br.grad, 1e-4)
 
 
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C,affine,res", [(17248, 320, True, False), (4312, 512, True, True), (68992, 128, True, False),
+                                            (5003, 64, False, True), (1001, 320, False, False)])
+def test_layernorm_bwd_many_rows(cuda, dt, M, C, affine, res):
+    """The vectorised backward at the train step's row counts (B = 88): waves walking many row groups (the affine
+    grid is capped at 256 blocks; round 6 issues four row groups' loads per iteration), ragged tails, with and
+    without the residual gradient and the affine gradients."""
+    from svk import ops
+    x, dy, r = _rand(M, C, seed=11), _rand(M, C, seed=12), _rand(M, C, seed=13)
+    g, b = 1 + 0.1 * _rand(C, seed=14), 0.1 * _rand(C, seed=15)
+    xd, dyd, rd = (t.to(dt).double() for t in (x, dy, r))
+    xr = xd.clone().requires_grad_(True)
+    gr, br = g.double().requires_grad_(True), b.double().requires_grad_(True)
+    F.layer_norm(xr, (C,), gr, br, 1e-6).backward(dyd)
+    dg = torch.zeros(C, device=cuda) if affine else None
+    db = torch.zeros(C, device=cuda) if affine else None
+    dx = ops.layernorm_bwd(x.to(cuda, dt), dy.to(cuda, dt), g.to(cuda), 1e-6, dres=r.to(cuda, dt) if res else None,
+                           dgamma=dg, dbeta=db)
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    _close(dx, xr.grad + (rd if res else 0), tol)
+    if affine:
+        _close(dg, gr.grad, tol)
+        _close(db, br.grad, tol)
+
+
 @pytest.mark.parametrize("act", ["gelu", "relu"])
 def test_act_bwd(cuda, act):
     from svk import ops
