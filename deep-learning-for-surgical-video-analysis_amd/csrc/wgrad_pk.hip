@@ -212,10 +212,13 @@ __global__ __launch_bounds__(256) void wgrad_pk(Args p) {
 template <typename T, class C, bool CONV = false>
 static int launch(Args a, int Z, hipStream_t st) {
   const long tiles = (long)((a.N + C::BN - 1) / C::BN) * ((a.K + C::BK - 1) / C::BK);
-  // M split: enough workgroups to fill the chip (~4 per CU), each with >= 128 rows (4 steps), and the f32
+  // M split: enough workgroups to fill the chip (~2 per CU), each with >= 128 rows (4 steps), and the f32
   // atomic bytes (splits x N x K x 4) at most the operand bytes (M x (N + K) x 2): the training step's
-  // weight gradients are mostly short (M = 88 x 49 / 88 x 196 tokens), where the split is what fills the chip
-  const long target = std::max<long>(1, 1024 / std::max<long>(1, tiles * Z));
+  // weight gradients are mostly short (M = 88 x 49 / 88 x 196 tokens), where the split is what fills the chip.
+  // Round 6 (profiles/r06/wgrad_target_ab.txt, train step same box): 512 workgroups 13.61 ms, 1024 13.69, 256 13.75,
+  // 2048 13.76, 128 14.30 — past ~2 per CU the extra splits' atomics cost more than the fill gains (SVK_WGRAD_TARGET)
+  static const long wg_target = getenv("SVK_WGRAD_TARGET") ? std::max(1L, atol(getenv("SVK_WGRAD_TARGET"))) : 512;
+  const long target = std::max<long>(1, wg_target / std::max<long>(1, tiles * Z));
   const long by_rows = std::max<long>(1, a.M / 128);
   const long by_atomics = std::max<long>(1, ((long)a.M * (a.N + a.K) * 2) / std::max<long>(1, (long)a.N * a.K * 4));
   long splits = std::min(target, std::min(by_rows, by_atomics));
