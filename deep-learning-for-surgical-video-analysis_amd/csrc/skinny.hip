@@ -12,6 +12,7 @@
 //   slab into its own full N x K accumulator set, the four waves are summed in LDS and each
 //   workgroup adds its partial with one f32 atomic per output element.
 #include "svk_common.h"
+#include <stdlib.h>
 
 namespace svk {
 
@@ -265,8 +266,11 @@ extern "C" int svk_wgrad_skinny(const void* dY, long ldy, const void* X, long ld
     set_error("svk_wgrad_skinny: bad args (N, K <= 128 with (N/16)*(K/16) <= 16, bf16)"); return SVK_EINVAL;
   }
   if (M == 0) return SVK_OK;
-  // ~512 workgroups, each >= 512 rows, slab-aligned
-  long chunk = std::max<long>(512, (M + 511) / 512);
+  // ~512 workgroups, each >= 512 rows, slab-aligned (SVK_SKINNY_WG: the workgroup target, SVK_SKINNY_MINROWS: the
+  // row floor — A/B knobs)
+  static const long sk_wg = getenv("SVK_SKINNY_WG") ? std::max(1L, atol(getenv("SVK_SKINNY_WG"))) : 512;
+  static const long sk_min = getenv("SVK_SKINNY_MINROWS") ? std::max(128L, atol(getenv("SVK_SKINNY_MINROWS"))) : 512;
+  long chunk = std::max<long>(sk_min, (M + sk_wg - 1) / sk_wg);
   chunk = (chunk + 127) / 128 * 128;
   const int grid = (int)((M + chunk - 1) / chunk);
   SkinnyWgradArgs a{(const bf16*)dY, ldy, (const bf16*)X, ldx, dW, lddw, db, M, N, K, (int)chunk};
