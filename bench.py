@@ -795,8 +795,8 @@ def plumbing(world, rank, local):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", default="extract", choices=sorted(WORKLOADS) + ["plumbing"])
     ap.add_argument("--batch", type=int, default=None, help="frames per GPU per step (256; train: 88)")
     ap.add_argument("--variant", default="mit_b2_evp")
