@@ -1012,10 +1012,12 @@ def other_workloads(args, dev, rank, world):
     B = 256 synthetic batch (VERDICT r05 #8), each dtype with its own roofline."""
     legs = {}
     b3 = "mit_b3_evp"
-    for name, argv in (("train", ["--workload", "train", "--steps", "10", "--warmup", "3", "--variant", args.variant]),
-                       ("e2e_config5", ["--workload", "e2e", "--steps", "10", "--warmup", "3",
+    # 30 timed / 10 warm-up steps each (round 6: at 10 / 3 two back-to-back default runs on one box read the train leg
+    # at 5 758 and 6 467 frames/s)
+    for name, argv in (("train", ["--workload", "train", "--steps", "30", "--warmup", "10", "--variant", args.variant]),
+                       ("e2e_config5", ["--workload", "e2e", "--steps", "30", "--warmup", "10",
                                         "--variant", args.variant]),
-                       ("extract_" + b3, ["--workload", "extract", "--steps", "10", "--warmup", "3", "--variant", b3,
+                       ("extract_" + b3, ["--workload", "extract", "--steps", "30", "--warmup", "10", "--variant", b3,
                                           "--other-dtypes", "fp32"])):
         if name.startswith("extract_") and args.variant == b3:
             continue                                 # the headline already is b3
