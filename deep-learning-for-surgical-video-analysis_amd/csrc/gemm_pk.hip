@@ -140,7 +140,11 @@ __device__ __forceinline__ void gload4(float& v, const char* src) {
 #define PK_DIAG_PARAM
 #define PK_DIAG_ARG
 #endif
-template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
+// PERM (round 6, EXT only): block j's W fragment rows are permuted so that a lane's two blocks 2p, 2p + 1 hold 8
+// CONSECUTIVE output columns (32 p + 8 fq .. + 7) instead of two 4-column pieces 16 apart — the epilogue operands
+// (bias, residual, the activation-backward source U) then load as 16-byte pieces, 16 rows x 64 bytes per
+// wave-instruction instead of 16 x 32.  Each output is the same MFMA reduction as without it (bit-identical).
+template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false, bool PERM = false>
 __global__ __launch_bounds__(Cfg::NT, Cfg::OCC)
 void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_PARAM) {
 #ifndef SVK_DIAG
@@ -269,7 +273,14 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
 #pragma unroll
       for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const tx8*>(sa + (wm * WM + i * 16 + fr) * 128 + cc);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = *reinterpret_cast<const tx8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
+      for (int j = 0; j < TN; ++j) {
+        if constexpr (PERM) {
+          const int rr = wn * WN + 32 * (j >> 1) + 8 * (fr >> 2) + 4 * (j & 1) + (fr & 3);
+          fb[j] = *reinterpret_cast<const tx8*>(sb + rr * 128 + (((ks * 4 + fq) ^ (rr & 7)) * 16));
+        } else {
+          fb[j] = *reinterpret_cast<const tx8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
+        }
+      }
       if (diag & 4) {                   // (diagnostic build) keep the fragment reads alive, skip the MFMAs
 #pragma unroll
         for (int i = 0; i < TM; ++i) asm volatile("" ::"v"(fa[i]));
@@ -294,12 +305,37 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
   constexpr bool LATE = Cfg::LATE;
   static_assert(!(LATE && (EXT || SPLIT)), "big tiles: plain epilogue only");
+  static_assert(!PERM || (EXT && !LATE && !SPLIT && WN % 32 == 0), "PERM: EXT tiles with 32-column wave slices");
+  // output column of block j, accumulator r: n0 + wn WN + colj(j) + r
+  auto colj = [&](int j) { return PERM ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : j * 16 + fq * 4; };
   f32x4 ebias[LATE ? 1 : TN];
-  u32x2 eres[LATE ? 1 : TM][LATE ? 1 : TN], eu[EXT ? TM : 1][EXT ? TN : 1];
+  u32x2 eres[LATE || PERM ? 1 : TM][LATE || PERM ? 1 : TN], eu[EXT && !PERM ? TM : 1][EXT && !PERM ? TN : 1];
+  f32x4 eres4[PERM ? TM : 1][PERM ? TN / 2 : 1], eu4[PERM ? TM : 1][PERM ? TN / 2 : 1];   // PERM: 8 columns each
   float ers[EXT ? TM : 1];
   const T* R = static_cast<const T*>(p.R);
   auto epi_load = [&](int unit) {
-    if constexpr (!SPLIT && !LATE) {
+    if constexpr (PERM) {
+      const int m0 = (unit / ntn) * BM, n0 = (unit % ntn) * BN;
+      const char* zero = reinterpret_cast<const char*>(g_pk_zero);
+      const T* U = static_cast<const T*>(p.U);
+#pragma unroll
+      for (int q = 0; q < TN / 2; ++q) {
+        const int n = min(n0 + wn * WN + 32 * q + 8 * fq, p.N - 8);   // host: N % 8 == 0
+        gload16(ebias[2 * q], p.bias ? reinterpret_cast<const char*>(p.bias + n) : zero);
+        gload16(ebias[2 * q + 1], p.bias ? reinterpret_cast<const char*>(p.bias + n + 4) : zero);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+          gload16(eres4[i][q], R ? reinterpret_cast<const char*>(R + (long)m * p.ldr + n) : zero);
+          gload16(eu4[i][q], U ? reinterpret_cast<const char*>(U + (long)m * p.ldu + n) : zero);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+        gload4(ers[i], p.rscale ? reinterpret_cast<const char*>(p.rscale + m / p.rdiv) : zero);
+      }
+    } else if constexpr (!SPLIT && !LATE) {
       const int m0 = (unit / ntn) * BM, n0 = (unit % ntn) * BN;
       const char* zero = reinterpret_cast<const char*>(g_pk_zero);
 #pragma unroll
@@ -327,6 +363,20 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   };
   auto tie_epi = [&]() {
     if constexpr (LATE) return;
+    if constexpr (PERM) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) asm volatile("" : "+v"(ebias[j]));
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int q = 0; q < TN / 2; ++q) {
+          asm volatile("" : "+v"(eres4[i][q]));
+          asm volatile("" : "+v"(eu4[i][q]));
+        }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(ers[i]));
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       asm volatile("" : "+v"(ebias[j]));
@@ -371,7 +421,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + fq * 4;
+      const int n = n0 + wn * WN + colj(j);
       f32x4 bj;
       if constexpr (LATE) {
         const int nb = min(n, p.N - 4);
@@ -385,6 +435,9 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
         u32x2 rij;
         if constexpr (LATE) {
           rij = R ? *reinterpret_cast<const u32x2*>(R + (long)min(m, p.M - 1) * p.ldr + min(n, p.N - 4)) : u32x2{0u, 0u};
+        } else if constexpr (PERM) {
+          const f32x4 r4 = eres4[i][j >> 1];
+          rij = (j & 1) ? u32x2{__float_as_uint(r4.z), __float_as_uint(r4.w)} : u32x2{__float_as_uint(r4.x), __float_as_uint(r4.y)};
         } else {
           rij = eres[i][j];
         }
@@ -393,7 +446,14 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = apply_act_fast(v[e], p.act) * ers[i];
           if (p.U) {
-            const f32x2 u01 = unpack2<T>(eu[i][j].x), u23 = unpack2<T>(eu[i][j].y);
+            u32x2 uij;
+            if constexpr (PERM) {
+              const f32x4 u4 = eu4[i][j >> 1];
+              uij = (j & 1) ? u32x2{__float_as_uint(u4.z), __float_as_uint(u4.w)} : u32x2{__float_as_uint(u4.x), __float_as_uint(u4.y)};
+            } else {
+              uij = eu[i][j];
+            }
+            const f32x2 u01 = unpack2<T>(uij.x), u23 = unpack2<T>(uij.y);
             v[0] *= act_grad(u01.x, ACT);
             v[1] *= act_grad(u01.y, ACT);
             v[2] *= act_grad(u23.x, ACT);
@@ -412,7 +472,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
         }
         T o[4] = {(T)v[0], (T)v[1], (T)v[2], (T)v[3]};
         if constexpr (ELDS) {
-          const int row = wm * WM + i * 16 + fr, col = wn * WN + j * 16 + fq * 4;
+          const int row = wm * WM + i * 16 + fr, col = wn * WN + colj(j);
           *reinterpret_cast<uint2*>(stile + row * (BN * 2) + (((col >> 3) ^ (row & (CPR - 1))) << 4) + ((col >> 2) & 1) * 8) =
               *reinterpret_cast<const uint2*>(o);
         } else if (m < p.M && n < p.N && !(diag & 2)) {   // N % 4 == 0: a 4-column group is all-in or all-out
@@ -512,7 +572,7 @@ static int pk_slots(const void* fn, int nt) {
   return std::max(1, cus) * std::max(1, per);
 }
 
-template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false>
+template <typename T, class Cfg, bool KTAIL, bool ELDS, int ASRC, bool EXT, bool SPLIT = false, bool PERM = false>
 static int launch_pk(const GemmArgs& a, hipStream_t st) {
   const int ntm = (a.M + Cfg::BM - 1) / Cfg::BM, ntn = (a.N + Cfg::BN - 1) / Cfg::BN;
   const int ks = SPLIT ? a.ksplit : 1;
@@ -524,7 +584,7 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     return SVK_EUNSUPPORTED;
   }
   static const int slots =
-      pk_slots(reinterpret_cast<const void*>(&gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), Cfg::NT);
+      pk_slots(reinterpret_cast<const void*>(&gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT, PERM>), Cfg::NT);
   const int grid = (int)std::min<long>(ntiles, slots);
   PkConv cv{};
   if (ASRC == 1) {
@@ -533,17 +593,18 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
     cv.cin = make_fastdiv((uint32_t)a.Cin);
     cv.kw = make_fastdiv((uint32_t)a.kw);
   }
-  hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
+  hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT, PERM>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
                      (int)ntiles, nk, ks PK_DIAG_ARG);
-  static char name[112];
+  static char name[120];
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", type_name<T>(), Cfg::BM, Cfg::BN,
+    snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s%s>", type_name<T>(), Cfg::BM, Cfg::BN,
              Cfg::WGM, Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC,
-             EXT ? "true" : "false", SPLIT ? "true" : "false");   // the demangled instantiation name
+             EXT ? "true" : "false", SPLIT ? "true" : "false", PERM ? ", true" : "");   // the demangled instantiation name
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
 
+static const int g_pk_perm = getenv("SVK_PK_PERM") ? atoi(getenv("SVK_PK_PERM")) : 1;   // A/B switch (EXT PERM)
 template <typename T, class Cfg, int ASRC>
 static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
@@ -570,6 +631,21 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
       if constexpr (!EXT_OK) {
         return launch_pk_k<T, PkCfg<128, 128, 2, 2, 2>, ASRC>(a, st, elds);
       } else {
+        // PERM: 16-byte epilogue operand pieces (bias, R, U 16-byte aligned with N, ldr, ldu % 8 == 0)
+        // (64 x 64: the PERM epilogue needs one VGPR more than its 5-workgroup occupancy allows — not instantiated)
+        constexpr bool PERM_OK = (Cfg::BN / Cfg::WGN) % 32 == 0 && Cfg::BM * Cfg::BN >= 128 * 64;
+        const bool perm = g_pk_perm && PERM_OK && a.N % 8 == 0 && (!a.bias || al16(a.bias)) &&
+                          (!a.R || (al16(a.R) && a.ldr % 8 == 0)) && (!a.U || (al16(a.U) && a.ldu % 8 == 0));
+        if constexpr (PERM_OK) {
+          if (perm) {
+            if constexpr (Cfg::ELDS_FITS) {
+              if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, true, false, true>(a, st)
+                                    : launch_pk<T, Cfg, false, true, 0, true, false, true>(a, st);
+            }
+            return tail ? launch_pk<T, Cfg, true, false, 0, true, false, true>(a, st)
+                        : launch_pk<T, Cfg, false, false, 0, true, false, true>(a, st);
+          }
+        }
         if constexpr (Cfg::ELDS_FITS) {
           if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, true>(a, st) : launch_pk<T, Cfg, false, true, 0, true>(a, st);
         }
