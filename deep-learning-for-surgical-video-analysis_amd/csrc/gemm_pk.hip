@@ -305,12 +305,12 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   // Lane holds C[m][n .. n+3]: m = row fr of block i, n = 4 fq + r of block j (transposed MFMA).
   constexpr bool LATE = Cfg::LATE;
   static_assert(!(LATE && (EXT || SPLIT)), "big tiles: plain epilogue only");
-  static_assert(!PERM || (EXT && !LATE && !SPLIT && WN % 32 == 0), "PERM: EXT tiles with 32-column wave slices");
+  static_assert(!PERM || (ASRC == 0 && !LATE && !SPLIT && WN % 32 == 0), "PERM: dense tiles with 32-column wave slices");
   // output column of block j, accumulator r: n0 + wn WN + colj(j) + r
   auto colj = [&](int j) { return PERM ? 32 * (j >> 1) + 8 * fq + 4 * (j & 1) : j * 16 + fq * 4; };
   f32x4 ebias[LATE ? 1 : TN];
   u32x2 eres[LATE || PERM ? 1 : TM][LATE || PERM ? 1 : TN], eu[EXT && !PERM ? TM : 1][EXT && !PERM ? TN : 1];
-  f32x4 eres4[PERM ? TM : 1][PERM ? TN / 2 : 1], eu4[PERM ? TM : 1][PERM ? TN / 2 : 1];   // PERM: 8 columns each
+  f32x4 eres4[PERM ? TM : 1][PERM ? TN / 2 : 1], eu4[PERM && EXT ? TM : 1][PERM && EXT ? TN / 2 : 1];   // 8 columns each
   float ers[EXT ? TM : 1];
   const T* R = static_cast<const T*>(p.R);
   auto epi_load = [&](int unit) {
@@ -327,13 +327,15 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
         for (int i = 0; i < TM; ++i) {
           const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
           gload16(eres4[i][q], R ? reinterpret_cast<const char*>(R + (long)m * p.ldr + n) : zero);
-          gload16(eu4[i][q], U ? reinterpret_cast<const char*>(U + (long)m * p.ldu + n) : zero);
+          if constexpr (EXT) gload16(eu4[i][q], U ? reinterpret_cast<const char*>(U + (long)m * p.ldu + n) : zero);
         }
       }
+      if constexpr (EXT) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
-        gload4(ers[i], p.rscale ? reinterpret_cast<const char*>(p.rscale + m / p.rdiv) : zero);
+        for (int i = 0; i < TM; ++i) {
+          const int m = min(m0 + wm * WM + i * 16 + fr, p.M - 1);
+          gload4(ers[i], p.rscale ? reinterpret_cast<const char*>(p.rscale + m / p.rdiv) : zero);
+        }
       }
     } else if constexpr (!SPLIT && !LATE) {
       const int m0 = (unit / ntn) * BM, n0 = (unit % ntn) * BN;
@@ -371,10 +373,12 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
 #pragma unroll
         for (int q = 0; q < TN / 2; ++q) {
           asm volatile("" : "+v"(eres4[i][q]));
-          asm volatile("" : "+v"(eu4[i][q]));
+          if constexpr (EXT) asm volatile("" : "+v"(eu4[i][q]));
         }
+      if constexpr (EXT) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(ers[i]));
+        for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(ers[i]));
+      }
       return;
     }
 #pragma unroll
@@ -604,7 +608,9 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
   return check_launch("gemm_pk");
 }
 
-static const int g_pk_perm = getenv("SVK_PK_PERM") ? atoi(getenv("SVK_PK_PERM")) : 1;   // A/B switch (EXT PERM)
+// PERM (16-byte epilogue operand pieces, bit-identical): 2 = EXT and plain-residual tiles (default; extraction step
+// 6.774 -> 6.715 ms, train 13.59 -> 13.48 same-box, profiles/r06/ext_perm_ab.txt), 1 = EXT only, 0 = off
+static const int g_pk_perm = getenv("SVK_PK_PERM") ? atoi(getenv("SVK_PK_PERM")) : 2;
 template <typename T, class Cfg, int ASRC>
 static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
   auto al16 = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
@@ -650,6 +656,20 @@ static int launch_pk_k(const GemmArgs& a, hipStream_t st, bool elds) {
           if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, true>(a, st) : launch_pk<T, Cfg, false, true, 0, true>(a, st);
         }
         return tail ? launch_pk<T, Cfg, true, false, 0, true>(a, st) : launch_pk<T, Cfg, false, false, 0, true>(a, st);
+      }
+    }
+    // PERM for the plain residual epilogue (SVK_PK_PERM=2, the default)
+    {
+      constexpr bool PERM_OK = Cfg::NSTAGE == 2 && !Cfg::LATE && (Cfg::BN / Cfg::WGN) % 32 == 0 && Cfg::BM * Cfg::BN >= 128 * 64;
+      if constexpr (PERM_OK) {
+        if (g_pk_perm == 2 && a.R && a.N % 8 == 0 && (!a.bias || al16(a.bias)) && al16(a.R) && a.ldr % 8 == 0) {
+          if constexpr (Cfg::ELDS_FITS) {
+            if (elds) return tail ? launch_pk<T, Cfg, true, true, 0, false, false, true>(a, st)
+                                  : launch_pk<T, Cfg, false, true, 0, false, false, true>(a, st);
+          }
+          return tail ? launch_pk<T, Cfg, true, false, 0, false, false, true>(a, st)
+                      : launch_pk<T, Cfg, false, false, 0, false, false, true>(a, st);
+        }
       }
     }
     if constexpr (Cfg::ELDS_FITS) {

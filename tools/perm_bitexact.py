@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "deep-learning-for-surgical-video-analysis_amd"))
 
-SHAPES = [(275968, 256, 64, 3136), (68992, 512, 128, 784), (17248, 1280, 320, 196), (17248, 320, 1280, 196),
+SHAPES = [(50176, 320, 320, 196), (200704, 128, 512, 784), (12544, 512, 512, 49), (275968, 256, 64, 3136), (68992, 512, 128, 784), (17248, 1280, 320, 196), (17248, 320, 1280, 196),
           (2000, 136, 72, 25), (4312, 512, 2048, 49), (1003, 64, 96, 17)]
 
 
@@ -37,6 +37,9 @@ def main():
                                           dact_src=u).cpu()
         out[f"{M}x{N}x{K}_r"] = ops.gemm(a, w, None, residual=r, row_scale=rs, rows_per=rpf).cpu()
         out[f"{M}x{N}x{K}_k"] = ops._last_kernel()
+        a16, w16, r16 = a.to(torch.float16), w.to(torch.float16), r.to(torch.float16)
+        out[f"{M}x{N}x{K}_p16"] = ops.gemm(a16, w16, bias, residual=r16).cpu()      # plain residual epilogue
+        out[f"{M}x{N}x{K}_pk"] = ops._last_kernel()
     torch.save({k: v for k, v in out.items() if torch.is_tensor(v)}, sys.argv[1])
     print({k: v for k, v in out.items() if not torch.is_tensor(v)})
 
