@@ -599,11 +599,13 @@ static int launch_pk(const GemmArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL((gemm_pk<T, Cfg, KTAIL, ELDS, ASRC, EXT, SPLIT, PERM>), dim3(grid), dim3(Cfg::NT), 0, st, a, cv, ntn,
                      (int)ntiles, nk, ks PK_DIAG_ARG);
-  static char name[120];
+  static char name[112];
+  // the demangled instantiation name without PERM: a PERM launch is the same kernel family for the profiles
+  // (tools/pmc_traffic.py kernel_key folds the argument the same way)
   if (!name[0])
-    snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s%s>", type_name<T>(), Cfg::BM, Cfg::BN,
+    snprintf(name, sizeof(name), "gemm_pk<%s, PkCfg<%d, %d, %d, %d, %d>, %s, %s, %d, %s, %s>", type_name<T>(), Cfg::BM, Cfg::BN,
              Cfg::WGM, Cfg::WGN, Cfg::NSTAGE, KTAIL ? "true" : "false", ELDS ? "true" : "false", ASRC,
-             EXT ? "true" : "false", SPLIT ? "true" : "false", PERM ? ", true" : "");   // the demangled instantiation name
+             EXT ? "true" : "false", SPLIT ? "true" : "false");
   set_last_kernel(name);
   return check_launch("gemm_pk");
 }
