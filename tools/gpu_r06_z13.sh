@@ -3,7 +3,7 @@
 # changed after the closing bundle)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r06z13
+O=gpurun_out/r06z17
 mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu_full.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -1 $O/pytest_gpu_full.log
