@@ -175,6 +175,10 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
   uint32_t offA[SOFF ? Cfg::A_LD : 1], offB[SOFF ? Cfg::B_LD : 1];
   // live == false: past the workgroup's last (tile, K-step) — the same instructions run (branch-free
   // around the DMA issue) with every source replaced by the zero block
+  // W-tile chunk swizzle: chunk c of tile row r sits at LDS position c ^ swzB(r).  PERM reads rows 32 q + 8 a + b
+  // (+ 4) per block: (r & 7) takes 4 values over them (a 4-way bank conflict on every fragment read), so PERM tiles
+  // swizzle by ((r >> 1) & 1) | ((r >> 3) & 3) << 1, which is 8 distinct values over each parity's 8 rows
+  auto swzB = [](int r) { return PERM ? (((r >> 1) & 1) | (((r >> 3) & 3) << 1)) : (r & 7); };
   auto issue = [&](int unit, int kt, int buf, bool live) {
     if (diag & 8) { unit = first; kt = 0; }
     const int tile = SPLIT ? unit / ks : unit, part = unit - tile * ks;
@@ -220,7 +224,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
 #pragma unroll
         for (int i = 0; i < Cfg::B_LD; ++i) {
           const int q = (wave * Cfg::B_LD + i) * 64 + lane;
-          const int r = q >> 3, c = (q & 7) ^ (r & 7);
+          const int r = q >> 3, c = (q & 7) ^ swzB(r);
           offB[i] = (uint32_t)min(n0 + r, p.N - 1) * (uint32_t)(p.ldw * 2) + c * 16;
         }
       }
@@ -247,7 +251,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
 #pragma unroll
     for (int i = 0; i < Cfg::B_LD; ++i) {
       const int q = (wave * Cfg::B_LD + i) * 64 + lane;
-      const int r = q >> 3, c = (q & 7) ^ (r & 7);
+      const int r = q >> 3, c = (q & 7) ^ swzB(r);
       const int n = min(n0 + r, p.N - 1), k = k0 + c * 8;
       const char* src = reinterpret_cast<const char*>(Wt + (long)n * p.ldw + k);
       if constexpr (KTAIL) src = k < p.K ? src : zero;
@@ -276,7 +280,7 @@ void gemm_pk(GemmArgs p, PkConv cv, int ntn, int ntiles, int nk, int ks PK_DIAG_
       for (int j = 0; j < TN; ++j) {
         if constexpr (PERM) {
           const int rr = wn * WN + 32 * (j >> 1) + 8 * (fr >> 2) + 4 * (j & 1) + (fr & 3);
-          fb[j] = *reinterpret_cast<const tx8*>(sb + rr * 128 + (((ks * 4 + fq) ^ (rr & 7)) * 16));
+          fb[j] = *reinterpret_cast<const tx8*>(sb + rr * 128 + (((ks * 4 + fq) ^ swzB(rr)) * 16));
         } else {
           fb[j] = *reinterpret_cast<const tx8*>(sb + (wn * WN + j * 16 + fr) * 128 + cc);
         }
