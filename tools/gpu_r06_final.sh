@@ -4,7 +4,7 @@
 # critical path, and the counter passes scoped to the replayed graph steps.  Output: gpurun_out/r06z
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-O=gpurun_out/r06zd
+O=gpurun_out/r06ze
 mkdir -p $O
 step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ "$rc" -eq 0 ] || exit $rc; }
 if [ -z "$SKIP_PYTEST" ]; then
