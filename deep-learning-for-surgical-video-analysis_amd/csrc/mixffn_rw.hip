@@ -887,5 +887,7 @@ extern "C" int svk_mixffn_rw(int dtype, const void* XN, const void* X, const voi
   if (var == 3) return ffnrw::launch<ffnrw::Cfg<64, 56, 28, 2>>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
   if (var == 4 || !gelu_pk_on())   // element-wise GELU (SVK_GELU_PK=0)
     return ffnrw::launch<ffnrw::DCfg<64, 56, 28, 2, false>, true>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
+  if (var == 5)   // whole-frame strips: 2 halo rows of fc1 per 56 rows instead of per 28
+    return ffnrw::launch<ffnrw::DCfg<64, 56, 56, 2>, true>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
   return ffnrw::launch<ffnrw::DCfg<64, 56, 28, 2>, true>(XN, X, W1, b1, taps, dbias, W2, b2, Y, Yn, gamma, beta, eps, B, H, st);
 }
