@@ -1,0 +1,89 @@
+"""The committed round evidence is self-consistent (CPU only, no GPU call): the closing bench line keeps the
+bench.py contract (BASELINE.json's metric, roofline and cpu_baseline objects, frac = achieved / peak), its
+`traffic` is the PMC figure of `pmc_traffic.json` for the same kernel family, and that JSON is reproduced from
+the raw counter CSVs committed beside it by the same tool (tools/pmc_traffic.py)."""
+import glob
+import gzip
+import json
+import os
+import shutil
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+
+def _latest_round():
+    rounds = sorted(d for d in glob.glob(os.path.join(REPO, "profiles", "r[0-9][0-9]"))
+                    if os.path.exists(os.path.join(d, "bench_default.json")))
+    if not rounds:
+        pytest.skip("no profiles/rNN/bench_default.json")
+    return rounds[-1]
+
+
+@pytest.fixture(scope="module")
+def line():
+    with open(os.path.join(_latest_round(), "bench_default.json")) as f:
+        return json.loads(f.read().strip().splitlines()[-1])
+
+
+def test_bench_line_contract(line):
+    with open(os.path.join(REPO, "BASELINE.json")) as f:
+        base = json.load(f)
+    assert line["metric"] == base["metric"]
+    for k in ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["higher_is_better"] is True and line["scaling"] in ("weak", "strong")
+    assert "workload" in line["config"] and line["data"].startswith("synthetic")
+    # value = frames per step / step time
+    assert line["value"] == pytest.approx(line["config"]["global_units_per_step"] / (line["ms_per_step"] * 1e-3),
+                                          rel=2e-3)
+    r = line["roofline"]
+    assert r["bound"] in ("hbm", "mfma") and r["unit"] == ("GB/s" if r["bound"] == "hbm" else "TFLOP/s")
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"], rel=1e-3)
+    per_launch = r["algorithmic_bytes_per_launch"] if r["bound"] == "hbm" else r["algorithmic_flop_per_launch"]
+    scale = 1e9 if r["bound"] == "hbm" else 1e12
+    assert r["achieved"] == pytest.approx(per_launch / (r["avg_launch_us"] * 1e-6) / scale, rel=2e-3)
+    c = line["cpu_baseline"]
+    assert c["kind"] in ("port", "reference") and c["cores"] >= 1 and c["value"] > 0 and c["sample"]
+
+
+def test_traffic_matches_pmc_json(line):
+    r = line["roofline"]
+    if r["traffic"] is None:
+        pytest.skip("no PMC traffic on this line")
+    with open(os.path.join(_latest_round(), "pmc_traffic.json")) as f:
+        pmc = json.load(f)
+    kern = pmc["extract"]["kernels"][r["kernel"]]
+    # the bench reads the JSON committed when it ran; the closing bundle regenerates it afterwards from the same
+    # kernels, so the two collections agree to counter noise
+    assert r["traffic"] == pytest.approx(kern["hbm_bytes_per_launch"], rel=0.01)
+    assert kern["hbm_bytes_per_launch"] >= 0.9 * r["algorithmic_bytes_per_launch"]
+
+
+def test_pmc_traffic_reproduced_from_committed_csvs(tmp_path):
+    import pmc_traffic
+
+    with open(os.path.join(_latest_round(), "pmc_traffic.json")) as f:
+        entry = json.load(f)["extract"]
+    csvs = []
+    for src in entry["source"]:
+        path = os.path.join(REPO, src)
+        assert os.path.exists(path), src
+        out = tmp_path / os.path.basename(src).replace(".gz", "")
+        with gzip.open(path, "rb") as fi, open(out, "wb") as fo:
+            shutil.copyfileobj(fi, fo)
+        csvs.append(str(out))
+    steps = int(entry["scope"].split()[2]) if entry["scope"].startswith("the last") else 0
+    keep_f = pmc_traffic.graph_step_dispatches(csvs[0], steps)[0] if steps else None
+    keep_w = pmc_traffic.graph_step_dispatches(csvs[1], steps)[0] if steps else None
+    fetch = pmc_traffic.per_kernel(csvs[0], "FETCH_SIZE", keep_f)
+    write = pmc_traffic.per_kernel(csvs[1], "WRITE_SIZE", keep_w)
+    for name, k in entry["kernels"].items():
+        f, w = fetch[name], write[name]
+        assert len(f) == k["dispatches"], name
+        got = (2.0 * sum(f) / len(f) + sum(w) / len(w)) * 1024.0
+        assert got == pytest.approx(k["hbm_bytes_per_launch"], abs=1.0), name
