@@ -1,7 +1,7 @@
 """The committed round evidence is self-consistent (CPU only, no GPU call): the closing bench line keeps the
 bench.py contract (BASELINE.json's metric, roofline and cpu_baseline objects, frac = achieved / peak), its
 `traffic` is the PMC figure of `pmc_traffic.json` for the same kernel family, and that JSON is reproduced from
-the raw counter CSVs committed beside it by the same tool (tools/pmc_traffic.py)."""
+the raw counter CSVs committed beside it by the same tools (tools/pmc_traffic.py, tools/pmc_mfma.py)."""
 import glob
 import gzip
 import json
@@ -87,3 +87,24 @@ def test_pmc_traffic_reproduced_from_committed_csvs(tmp_path):
         assert len(f) == k["dispatches"], name
         got = (2.0 * sum(f) / len(f) + sum(w) / len(w)) * 1024.0
         assert got == pytest.approx(k["hbm_bytes_per_launch"], abs=1.0), name
+
+
+def test_pmc_mfma_reproduced_from_committed_csv(tmp_path):
+    import subprocess
+
+    rdir = _latest_round()
+    with open(os.path.join(rdir, "pmc_mfma.json")) as f:
+        want = json.load(f)["extract_fp16"]
+    src = os.path.join(rdir, "pmc", "extract_fp16_graph_m.csv.gz")
+    csv_path = tmp_path / "m.csv"
+    with gzip.open(src, "rb") as fi, open(csv_path, "wb") as fo:
+        shutil.copyfileobj(fi, fo)
+    out = tmp_path / "mfma.json"
+    args = [sys.executable, os.path.join(REPO, "tools", "pmc_mfma.py"), str(csv_path), str(out), "extract_fp16",
+            str(int(want["steps"]))] + (["--graph"] if want["scope"].startswith("the last") else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    with open(out) as f:
+        got = json.load(f)["extract_fp16"]
+    assert got["dispatches"] == want["dispatches"]
+    assert got["step_mfma_busy_frac"] == pytest.approx(want["step_mfma_busy_frac"], rel=1e-9)
