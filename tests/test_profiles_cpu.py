@@ -108,3 +108,15 @@ def test_pmc_mfma_reproduced_from_committed_csv(tmp_path):
         got = json.load(f)["extract_fp16"]
     assert got["dispatches"] == want["dispatches"]
     assert got["step_mfma_busy_frac"] == pytest.approx(want["step_mfma_busy_frac"], rel=1e-9)
+
+
+def test_kernel_family_folds_gemm_pk_perm():
+    """gemm_pk's PERM template argument (the W-row permutation for 16-byte epilogue operands) is one family with
+    the unpermuted instantiation, as bench.py's svk_last_kernel name reports it; other kernels keep their names."""
+    import pmc_traffic
+
+    base = "gemm_pk<_Float16, PkCfg<128, 128, 2, 2, 2>, false, true, 0, false, false"
+    assert pmc_traffic._family(base + ", true>") == base + ">"
+    assert pmc_traffic._family(base + ", false>") == base + ">"
+    assert pmc_traffic._family(base + ">") == base + ">"
+    assert pmc_traffic._family("attn_block<_Float16, 1, 8, 256>") == "attn_block<_Float16, 1, 8, 256>"
